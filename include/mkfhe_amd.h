@@ -1,0 +1,129 @@
+/*
+ * mkfhe_amd.h -- C ABI of the MI355X multi-key blind-rotation accumulator.
+ *
+ * Drop-in boundary for the reference's plugin seam
+ *   class UniEncAccumulator { virtual void EvalAcc(params, ek, Pkey, skf, acc, ct) const; }
+ *   (reference src/binfhe/include/mk-acc.h:55-80; concrete classes
+ *    UniEncAccumulatorXZW   src/binfhe/lib/mk-acc-xzw.cpp:89-130   (MKNTRU)
+ *    UniEncAccumulatorXZW_B src/binfhe/lib/mk-acc-xzw_B.cpp:103-132 (MKNTRU_B, MKNTRU_LWE),
+ *    chosen by BinFHEScheme(BINFHE_METHOD) at binfhe-base-scheme.h:137-151).
+ *
+ * Plain pointers and sizes only.  The caller owns host buffers; a context owns
+ * its device buffers and one HIP stream (calls on one context are serialised).
+ * Every function returns MKACC_OK (0) or a negative MKACC_E* status; the text
+ * of the last error on the calling thread is available from mkacc_last_error().
+ * The C++ host layer (mkfhe_amd/csrc/host/) converts a status into the
+ * reference's exception types (OPENFHE_THROW config_error / math_error,
+ * reference src/core/include/utils/exception.h:162).
+ *
+ * Polynomial layouts at this boundary are the reference's:
+ *   EVAL  = NativePoly in Format::EVALUATION, i.e. the bit-reversed output of
+ *           ForwardTransformToBitReverseInPlace (transformnat-impl.h:300-354)
+ *           with the minimal primitive 2N-th root of unity;
+ *   COEFF = Format::COEFFICIENT.
+ * All words are canonical residues in [0, Q).
+ */
+#ifndef MKFHE_AMD_H
+#define MKFHE_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MKACC_ABI_VERSION 1
+
+/* status codes */
+#define MKACC_OK            0
+#define MKACC_E_ARG        -1  /* bad argument / shape (reference: config_error) */
+#define MKACC_E_UNSUPPORTED -2 /* parameter set outside what the engine supports */
+#define MKACC_E_NOKEYS     -3  /* EvalAcc before keys were uploaded (binfhe-base-scheme.cpp:1075-1080) */
+#define MKACC_E_DEVICE     -4  /* HIP runtime error */
+#define MKACC_E_RANGE      -5  /* an input word is not a canonical residue */
+
+/* BINFHE_METHOD values that reach the accumulator (binfhe-constants.h:129-137) */
+#define MKACC_METHOD_MKNTRU     0  /* UniEncAccumulatorXZW   */
+#define MKACC_METHOD_MKNTRU_B   1  /* UniEncAccumulatorXZW_B */
+#define MKACC_METHOD_MKNTRU_LWE 2  /* UniEncAccumulatorXZW_B */
+
+/* Mirrors the UniEncCryptoParams fields EvalAcc reads
+ * (mk-cryptoparameters.h:124-181). */
+typedef struct mkacc_params {
+    uint32_t method;   /* MKACC_METHOD_* */
+    uint32_t k;        /* number of parties (numUser) */
+    uint32_t n;        /* LWE / NTRU dimension (latticeParam) */
+    uint32_t N;        /* ring dimension; the engine supports N = 2048 */
+    uint64_t Q;        /* ring modulus; the engine supports 2^26 < Q < 2^28, Q = 1 mod 2N */
+    uint64_t q;        /* ciphertext modulus (mod); XZW computes c = floor(ct*2N/q) */
+    uint32_t baseG;    /* gadget base B_g, power of two */
+    uint32_t digitsG;  /* 0 = derive ceil(log Q / log B_g) as the reference does */
+    uint64_t root;     /* 0 = derive the minimal primitive 2N-th root (ilparams.h:90-91) */
+} mkacc_params;
+
+typedef struct mkacc_ctx mkacc_ctx;
+
+/* Parameter-set table (binfhecontext.cpp:129-144).  Fills *out for the named
+ * set (e.g. "STD128_MKNTRU", "STD100_MKNTRU_LWE_2") with Q derived as
+ * PreviousPrime(FirstPrime(27, 4096), 4096).  method selects MKNTRU/…_B/…_LWE. */
+int mkacc_paramset(const char* name, uint32_t method, mkacc_params* out);
+
+/* Create a context on HIP device `device`; derives digitsG / root when 0. */
+int mkacc_create(const mkacc_params* p, int device, mkacc_ctx** out);
+void mkacc_destroy(mkacc_ctx* ctx);
+
+/* Effective parameters (digitsG and root filled in). */
+int mkacc_get_params(const mkacc_ctx* ctx, mkacc_params* out);
+
+/* Element counts of the boundary arrays. */
+size_t mkacc_evk_words(const mkacc_ctx* ctx);   /* k * nk * (n+1) * (digitsG-1) * 2 * N, nk = 2 (XZW) / 1 (XZW_B) */
+size_t mkacc_pkey_words(const mkacc_ctx* ctx);  /* k * (digitsG-1) * N */
+
+/*
+ * Upload the accumulator keys (UniEncACCKeyImpl, mk-acckey.h:44-51) and the
+ * public "Pkey" polynomials that BinFHEScheme passes to EvalAcc.
+ *   evk  [k][nk][n+1][dg][2][N]  EVAL   -- (*ek)[u][j][i] -> GetElements()[digit][0|1]
+ *   pkey [k][dg][N]              EVAL
+ * Keys are converted once into the device layout.  Re-uploading replaces them.
+ */
+int mkacc_upload_keys(mkacc_ctx* ctx, const uint32_t* evk, const uint32_t* pkey);
+int mkacc_upload_keys_u64(mkacc_ctx* ctx, const uint64_t* evk, const uint64_t* pkey);
+
+/*
+ * EvalAcc over a batch of B independent gates (host buffers, synchronous).
+ *   ct      [B][k][n]  raw ciphertext words: XZW mod q (MNTRU GetElements()),
+ *                      XZW_B mod 2N (MK-LWE GetAneg() after ModSwitch to 2N)
+ *   acc_in  [B][k][N]  EVAL, the initial accumulator (BootstrapGateCore test vector)
+ *   acc_out [B][k][N]  EVAL, the accumulator after EvalAcc; may alias acc_in
+ * Equivalent to calling the reference EvalAcc once per gate.
+ */
+int mkacc_eval_batch(mkacc_ctx* ctx, const uint32_t* ct, const uint32_t* acc_in, uint32_t* acc_out, size_t B);
+
+/* Same with DEVICE pointers on the context's device; enqueued on the context
+ * stream and returns without waiting (use mkacc_sync).  Used by bench.py so
+ * the timed region starts with inputs resident in HBM. */
+int mkacc_eval_batch_device(mkacc_ctx* ctx, const uint32_t* d_ct, const uint32_t* d_acc_in,
+                            uint32_t* d_acc_out, size_t B);
+int mkacc_sync(mkacc_ctx* ctx);
+
+/* The context's HIP stream (hipStream_t as void*), for event timing. */
+void* mkacc_stream(mkacc_ctx* ctx);
+
+/* ---- primitives exposed for parity tests (same layouts as above) ---- */
+/* NativePoly::SetFormat(EVALUATION) on `count` polys: COEFF -> EVAL. */
+int mkacc_ntt_forward(mkacc_ctx* ctx, const uint32_t* in, uint32_t* out, size_t count);
+/* NativePoly::SetFormat(COEFFICIENT) on `count` polys: EVAL -> COEFF. */
+int mkacc_ntt_inverse(mkacc_ctx* ctx, const uint32_t* in, uint32_t* out, size_t count);
+/* UniEncAccumulator::SignedDigitDecompose(poly) (mk-acc.cpp:54-80) on `count`
+ * COEFF polys: out [count][dg][N]. */
+int mkacc_sdd(mkacc_ctx* ctx, const uint32_t* in, uint32_t* out, size_t count);
+
+/* Per-thread text of the last error ("" if none). */
+const char* mkacc_last_error(void);
+int mkacc_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MKFHE_AMD_H */

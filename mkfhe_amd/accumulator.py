@@ -1,0 +1,215 @@
+"""Host-side mirror of the reference accumulator plugin interface.
+
+Reference seam: ``class UniEncAccumulator`` (src/binfhe/include/mk-acc.h:55-80)
+with the concrete ``UniEncAccumulatorXZW`` (mk-acc-xzw.cpp:89-130, MKNTRU) and
+``UniEncAccumulatorXZW_B`` (mk-acc-xzw_B.cpp:103-132, MKNTRU_B / MKNTRU_LWE),
+selected by ``BinFHEScheme(BINFHE_METHOD)`` (binfhe-base-scheme.h:137-151).
+
+Every call goes through the HIP engine's C ABI (include/mkfhe_amd.h); there is
+no CPU fallback.  Arrays use the reference's layouts:
+
+* ``ek``   ``[k][nk][n+1][dg][2][N]`` EVAL residues, nk = 2 (XZW) or 1 (XZW_B)
+* ``Pkey`` ``[k][dg][N]`` EVAL
+* ``acc``  ``[k][N]`` EVAL, updated in place by ``EvalAcc``
+* ``ct``   ``[k][n]`` raw ciphertext words (XZW: mod q, XZW_B: mod 2N)
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import MkaccError, MkaccParams, check
+
+MKNTRU = _lib.METHOD_MKNTRU
+MKNTRU_B = _lib.METHOD_MKNTRU_B
+MKNTRU_LWE = _lib.METHOD_MKNTRU_LWE
+
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+
+PARAMSETS = [
+    "STD128_MKNTRU", "STD128_MKNTRU_2", "STD128_MKNTRU_3", "STD128_MKNTRU_4",
+    "STD128_MKNTRU_LWE", "STD128_MKNTRU_LWE_2", "STD128_MKNTRU_LWE_3", "STD128_MKNTRU_LWE_4",
+    "STD100_MKNTRU", "STD100_MKNTRU_2", "STD100_MKNTRU_3", "STD100_MKNTRU_4",
+    "STD100_MKNTRU_LWE", "STD100_MKNTRU_LWE_2", "STD100_MKNTRU_LWE_3", "STD100_MKNTRU_LWE_4",
+]
+
+
+def paramset(name: str, method: int | None = None) -> MkaccParams:
+    """UniEnc parameters of a named BINFHE_PARAMSET (binfhecontext.cpp:129-144).
+
+    ``method`` defaults to MKNTRU_LWE for ``*_LWE*`` sets and MKNTRU otherwise,
+    matching the example programs (boolean-mkntru.cpp:14, boolean-mklwe.cpp:13).
+    """
+    if method is None:
+        method = MKNTRU_LWE if "_LWE" in name else MKNTRU
+    p = MkaccParams()
+    check(_lib.load().mkacc_paramset(name.encode(), method, ctypes.byref(p)))
+    return p
+
+
+def make_params(method: int, k: int, n: int, N: int, Q: int, q: int, baseG: int,
+                digitsG: int = 0, root: int = 0) -> MkaccParams:
+    return MkaccParams(method, k, n, N, Q, q, baseG, digitsG, root)
+
+
+def _u32(a: np.ndarray):
+    return a.ctypes.data_as(_u32p)
+
+
+class MKAccumulatorEngine:
+    """One device context (mkacc_ctx) with its uploaded keys."""
+
+    def __init__(self, params: MkaccParams, device: int = 0):
+        L = _lib.load()
+        h = ctypes.c_void_p()
+        check(L.mkacc_create(ctypes.byref(params), device, ctypes.byref(h)))
+        self._h = h
+        eff = MkaccParams()
+        check(L.mkacc_get_params(h, ctypes.byref(eff)))
+        self.params = eff
+        self.method, self.k, self.n, self.N = eff.method, eff.k, eff.n, eff.N
+        self.Q, self.q, self.baseG, self.digitsG = eff.Q, eff.q, eff.baseG, eff.digitsG
+        self.dg = eff.digitsG - 1
+        self.nk = 2 if eff.method == MKNTRU else 1
+        self.device = device
+        self._key_token = None
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.load().mkacc_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    @property
+    def handle(self):
+        return self._h
+
+    @property
+    def evk_shape(self):
+        return (self.k, self.nk, self.n + 1, self.dg, 2, self.N)
+
+    @property
+    def pkey_shape(self):
+        return (self.k, self.dg, self.N)
+
+    # -- keys -----------------------------------------------------------------
+    def upload_keys(self, evk: np.ndarray, pkey: np.ndarray):
+        L = _lib.load()
+        if evk.size != int(np.prod(self.evk_shape)) or pkey.size != int(np.prod(self.pkey_shape)):
+            raise MkaccError(_lib.MKACC_E_ARG, "key arrays have the wrong size")
+        if evk.dtype == np.uint64 or pkey.dtype == np.uint64:
+            e = np.ascontiguousarray(evk, dtype=np.uint64)
+            p = np.ascontiguousarray(pkey, dtype=np.uint64)
+            check(L.mkacc_upload_keys_u64(self._h, e.ctypes.data_as(_u64p), p.ctypes.data_as(_u64p)))
+        else:
+            e = np.ascontiguousarray(evk, dtype=np.uint32)
+            p = np.ascontiguousarray(pkey, dtype=np.uint32)
+            check(L.mkacc_upload_keys(self._h, _u32(e), _u32(p)))
+        self._key_token = (id(evk), id(pkey))
+
+    # -- evaluation -------------------------------------------------------------
+    def eval_batch(self, ct: np.ndarray, acc: np.ndarray) -> np.ndarray:
+        """EvalAcc on B gates: ct [B][k][n], acc [B][k][N] EVAL -> new acc."""
+        ct32 = np.ascontiguousarray(ct, dtype=np.uint32)
+        acc32 = np.ascontiguousarray(acc, dtype=np.uint32)
+        if ct32.ndim != 3 or ct32.shape[1:] != (self.k, self.n):
+            raise MkaccError(_lib.MKACC_E_ARG, f"ct must be [B][{self.k}][{self.n}]")
+        B = ct32.shape[0]
+        if acc32.shape != (B, self.k, self.N):
+            raise MkaccError(_lib.MKACC_E_ARG, f"acc must be [B][{self.k}][{self.N}]")
+        out = np.empty_like(acc32)
+        check(_lib.load().mkacc_eval_batch(self._h, _u32(ct32), _u32(acc32), _u32(out), B))
+        return out
+
+    def eval_batch_device(self, d_ct, d_acc_in, d_acc_out, B: int):
+        """Device-pointer batch (torch tensors or raw ints); asynchronous on the context stream."""
+        def ptr(t):
+            return ctypes.c_void_p(t if isinstance(t, int) else t.data_ptr())
+        check(_lib.load().mkacc_eval_batch_device(self._h, ptr(d_ct), ptr(d_acc_in), ptr(d_acc_out), B))
+
+    def sync(self):
+        check(_lib.load().mkacc_sync(self._h))
+
+    def stream_handle(self) -> int:
+        return _lib.load().mkacc_stream(self._h) or 0
+
+    # -- primitives -------------------------------------------------------------
+    def _prim(self, fn, a: np.ndarray, out_mul: int):
+        x = np.ascontiguousarray(a, dtype=np.uint32).reshape(-1, self.N)
+        out = np.empty((x.shape[0] * out_mul, self.N), dtype=np.uint32)
+        check(fn(self._h, _u32(x), _u32(out), x.shape[0]))
+        return out
+
+    def ntt_forward(self, a: np.ndarray) -> np.ndarray:
+        """NativePoly::SetFormat(EVALUATION) on rows of a."""
+        return self._prim(_lib.load().mkacc_ntt_forward, a, 1)
+
+    def ntt_inverse(self, a: np.ndarray) -> np.ndarray:
+        """NativePoly::SetFormat(COEFFICIENT) on rows of a."""
+        return self._prim(_lib.load().mkacc_ntt_inverse, a, 1)
+
+    def sdd(self, a: np.ndarray) -> np.ndarray:
+        """SignedDigitDecompose (mk-acc.cpp:54-80): rows -> [rows][dg][N]."""
+        out = self._prim(_lib.load().mkacc_sdd, a, self.dg)
+        return out.reshape(-1, self.dg, self.N)
+
+
+class UniEncAccumulator:
+    """Mirror of the reference's abstract accumulator (mk-acc.h:55-80)."""
+
+    method: int = -1
+
+    def __init__(self, params: MkaccParams, device: int = 0):
+        if params.method not in self._methods:
+            raise MkaccError(_lib.MKACC_E_ARG, "method is invalid for this accumulator")
+        self.engine = MKAccumulatorEngine(params, device)
+
+    def _ensure_keys(self, ek, Pkey):
+        token = (id(ek), id(Pkey))
+        if self.engine._key_token != token:
+            self.engine.upload_keys(np.asarray(ek), np.asarray(Pkey))
+            self.engine._key_token = token
+
+    def EvalAcc(self, ek, Pkey, skf, acc: np.ndarray, ct) -> None:
+        """EvalAcc(params, ek, Pkey, skf, acc, ct): acc [k][N] EVAL updated in place.
+
+        ``skf`` is accepted for signature parity and ignored, as in the reference
+        (it is only read by commented-out debug code, mk-acc-xzw.cpp:115-120).
+        """
+        if ek is None:
+            raise MkaccError(_lib.MKACC_E_NOKEYS, "Bootstrapping keys have not been generated. "
+                                                  "Please call MKBTKeyGen before calling bootstrapping.")
+        self._ensure_keys(ek, Pkey)
+        out = self.engine.eval_batch(np.asarray(ct)[None], np.asarray(acc)[None])
+        acc[...] = out[0]
+
+    def EvalAccBatch(self, ek, Pkey, acc: np.ndarray, ct: np.ndarray) -> np.ndarray:
+        """Batch extension: B independent gates, acc [B][k][N], ct [B][k][n]."""
+        self._ensure_keys(ek, Pkey)
+        return self.engine.eval_batch(ct, acc)
+
+
+class UniEncAccumulatorXZW(UniEncAccumulator):
+    """MKNTRU accumulator, ternary secret (mk-acc-xzw.cpp)."""
+
+    _methods = (MKNTRU,)
+
+
+class UniEncAccumulatorXZW_B(UniEncAccumulator):
+    """MKNTRU_B / MKNTRU_LWE accumulator, binary secret (mk-acc-xzw_B.cpp)."""
+
+    _methods = (MKNTRU_B, MKNTRU_LWE)
+
+
+def accumulator_for(params: MkaccParams, device: int = 0) -> UniEncAccumulator:
+    """BinFHEScheme(BINFHE_METHOD) accumulator choice (binfhe-base-scheme.h:137-151)."""
+    if params.method == MKNTRU:
+        return UniEncAccumulatorXZW(params, device)
+    if params.method in (MKNTRU_B, MKNTRU_LWE):
+        return UniEncAccumulatorXZW_B(params, device)
+    raise MkaccError(_lib.MKACC_E_ARG, "method is invalid")

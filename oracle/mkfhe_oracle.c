@@ -1,0 +1,519 @@
+/*
+ * mkfhe_oracle.c -- CPU restatement of the MKFHE multi-key accumulator.
+ *
+ * TEST INFRASTRUCTURE ONLY: this is the parity checker for the HIP engine.
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg load
+ * it.  Nothing under mkfhe_amd/ links or calls it.
+ *
+ * Every function cites the reference file:line it restates (paths relative to
+ * the reference's src/).  Pinning status is documented in mkfhe_oracle.h and
+ * DESIGN.md section 3.
+ */
+#include "mkfhe_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+typedef unsigned __int128 u128;
+
+/* ------------------------------------------------------------------------ */
+/* modular helpers                                                          */
+/* ------------------------------------------------------------------------ */
+
+uint64_t orc_mulmod(uint64_t a, uint64_t b, uint64_t Q) {
+    if (Q <= 0xFFFFFFFFull) return (a * b) % Q; /* a,b < Q < 2^32: product fits */
+    return (uint64_t)(((u128)a * b) % Q);
+}
+
+uint64_t orc_powmod(uint64_t a, uint64_t e, uint64_t Q) {
+    uint64_t r = 1 % Q;
+    a %= Q;
+    while (e) {
+        if (e & 1) r = orc_mulmod(r, a, Q);
+        a = orc_mulmod(a, a, Q);
+        e >>= 1;
+    }
+    return r;
+}
+
+static inline uint64_t addmod(uint64_t a, uint64_t b, uint64_t Q) {
+    uint64_t s = a + b;
+    return s >= Q ? s - Q : s;
+}
+static inline uint64_t submod(uint64_t a, uint64_t b, uint64_t Q) {
+    return a >= b ? a - b : a + Q - b;
+}
+
+uint64_t orc_modinv(uint64_t a, uint64_t Q) {
+    /* extended Euclid over signed 128-bit */
+    __int128 t = 0, nt = 1, r = (__int128)Q, nr = (__int128)(a % Q);
+    while (nr != 0) {
+        __int128 qt = r / nr, tmp;
+        tmp = t - qt * nt; t = nt; nt = tmp;
+        tmp = r - qt * nr; r = nr; nr = tmp;
+    }
+    if (r != 1) return 0;
+    if (t < 0) t += (__int128)Q;
+    return (uint64_t)t;
+}
+
+/* ------------------------------------------------------------------------ */
+/* number theory                                                            */
+/* ------------------------------------------------------------------------ */
+
+/* Miller-Rabin with the deterministic base set for 64-bit n.  The reference
+ * (nbtheory-impl.h:258-287) uses random witnesses; for primes both accept,
+ * so FirstPrime/PreviousPrime return the same values. */
+int orc_is_prime(uint64_t n) {
+    static const uint64_t bases[] = {2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37};
+    if (n < 2) return 0;
+    for (int i = 0; i < 12; ++i) {
+        if (n == bases[i]) return 1;
+        if (n % bases[i] == 0) return 0;
+    }
+    uint64_t d = n - 1;
+    int s = 0;
+    while ((d & 1) == 0) { d >>= 1; ++s; }
+    for (int i = 0; i < 12; ++i) {
+        uint64_t x = orc_powmod(bases[i], d, n);
+        if (x == 1 || x == n - 1) continue;
+        int comp = 1;
+        for (int r = 1; r < s; ++r) {
+            x = (uint64_t)(((u128)x * x) % n);
+            if (x == n - 1) { comp = 0; break; }
+        }
+        if (comp) return 0;
+    }
+    return 1;
+}
+
+/* FirstPrime: nbtheory-impl.h:334-357.  Smallest prime q > 2^nbits with q = 1 mod m. */
+uint64_t orc_first_prime(uint32_t nbits, uint64_t m) {
+    uint64_t q = 1ull << nbits;
+    uint64_t r = q % m;
+    uint64_t q2 = q + 1;
+    if (r > 0) q2 += (m - r);
+    while (!orc_is_prime(q2)) q2 += m;
+    return q2;
+}
+
+/* PreviousPrime: nbtheory-impl.h:369-377. */
+uint64_t orc_previous_prime(uint64_t q, uint64_t m) {
+    uint64_t c = q - m;
+    while (!orc_is_prime(c)) c -= m;
+    return c;
+}
+
+/* RootOfUnity: nbtheory-impl.h:183-231.  The reference finds a random
+ * generator, raises it to (Q-1)/m and then returns the MINIMUM over all
+ * primitive m-th roots (odd powers for power-of-two m) -- a value that does
+ * not depend on the generator.  We do the same from a deterministic generator. */
+uint64_t orc_root_of_unity(uint64_t m, uint64_t Q) {
+    if ((Q - 1) % m != 0) return 0;
+    /* factor Q-1 by trial division (Q < 2^62; fine for the moduli used here) */
+    uint64_t fac[64];
+    int nf = 0;
+    uint64_t t = Q - 1;
+    for (uint64_t p = 2; p * p <= t; p += (p == 2 ? 1 : 2)) {
+        if (t % p == 0) {
+            fac[nf++] = p;
+            while (t % p == 0) t /= p;
+        }
+    }
+    if (t > 1) fac[nf++] = t;
+    uint64_t g = 2;
+    for (;; ++g) {
+        int ok = 1;
+        for (int i = 0; i < nf; ++i)
+            if (orc_powmod(g, (Q - 1) / fac[i], Q) == 1) { ok = 0; break; }
+        if (ok) break;
+    }
+    uint64_t w = orc_powmod(g, (Q - 1) / m, Q);
+    /* cycle over powers coprime to m; m is a power of two here -> odd powers */
+    uint64_t w2 = orc_mulmod(w, w, Q), x = w, best = w;
+    for (uint64_t e = 1; e < m; e += 2) {
+        if (x < best && x != 1) best = x;
+        x = orc_mulmod(x, w2, Q);
+    }
+    return best;
+}
+
+/* mk-cryptoparameters.h:141-142: digitsG = ceil(log(Q)/log(baseG)) in double. */
+uint32_t orc_digits_g(uint64_t Q, uint32_t baseG) {
+    double logQ = log((double)Q);
+    return (uint32_t)ceil(logQ / log((double)baseG));
+}
+
+/* ------------------------------------------------------------------------ */
+/* NTT (transformnat-impl.h)                                                */
+/* ------------------------------------------------------------------------ */
+
+static uint32_t brv(uint32_t x, uint32_t bits) {
+    uint32_t r = 0;
+    for (uint32_t i = 0; i < bits; ++i) r |= ((x >> i) & 1u) << (bits - 1 - i);
+    return r;
+}
+static uint32_t ilog2u(uint32_t x) { uint32_t r = 0; while ((1u << r) < x) ++r; return r; }
+
+/* Tables exactly as ChineseRemainderTransformFTTNat::PreCompute
+ * (transformnat-impl.h:705-760): table[brv(i)] = psi^i, tableI[brv(i)] = psi^-i. */
+static void make_tables(uint64_t* tab, uint64_t* tabI, uint32_t N, uint64_t Q, uint64_t psi) {
+    uint32_t lg = ilog2u(N);
+    uint64_t x = 1, xi = 1, psiI = orc_modinv(psi, Q);
+    for (uint32_t i = 0; i < N; ++i) {
+        uint32_t r = brv(i, lg);
+        tab[r] = x;
+        tabI[r] = xi;
+        x = orc_mulmod(x, psi, Q);
+        xi = orc_mulmod(xi, psiI, Q);
+    }
+}
+
+/* ForwardTransformToBitReverseInPlace, transformnat-impl.h:300-354. */
+static void ntt_fwd_tab(uint64_t* a, uint32_t N, uint64_t Q, const uint64_t* tab) {
+    uint32_t t = N;
+    for (uint32_t m = 1; m < N; m <<= 1) {
+        t >>= 1;
+        for (uint32_t i = 0; i < m; ++i) {
+            uint64_t w = tab[m + i];
+            uint32_t j1 = 2 * i * t;
+            for (uint32_t j = j1; j < j1 + t; ++j) {
+                uint64_t U = a[j], V = orc_mulmod(a[j + t], w, Q);
+                a[j] = addmod(U, V, Q);
+                a[j + t] = submod(U, V, Q);
+            }
+        }
+    }
+}
+
+/* InverseTransformFromBitReverseInPlace, transformnat-impl.h:492-552
+ * (stride-1 stage first with N^-1 fused, then GS stages of growing stride). */
+static void ntt_inv_tab(uint64_t* a, uint32_t N, uint64_t Q, const uint64_t* tabI, uint64_t Ninv) {
+    for (uint32_t i = 0; i < N; i += 2) {
+        uint64_t w = tabI[(i + N) >> 1];
+        uint64_t lo = a[i], hi = a[i + 1];
+        uint64_t d = submod(lo, hi, Q);
+        lo = addmod(lo, hi, Q);
+        a[i] = orc_mulmod(lo, Ninv, Q);
+        a[i + 1] = orc_mulmod(orc_mulmod(d, w, Q), Ninv, Q);
+    }
+    for (uint32_t m = N >> 2, t = 2; m >= 1; m >>= 1, t <<= 1) {
+        for (uint32_t i = 0; i < m; ++i) {
+            uint64_t w = tabI[i + m];
+            uint32_t j1 = 2 * i * t;
+            for (uint32_t j = j1; j < j1 + t; ++j) {
+                uint64_t lo = a[j], hi = a[j + t];
+                a[j] = addmod(lo, hi, Q);
+                a[j + t] = orc_mulmod(submod(lo, hi, Q), w, Q);
+            }
+        }
+    }
+}
+
+void orc_ntt_forward(uint64_t* a, uint32_t N, uint64_t Q, uint64_t psi) {
+    uint64_t* tab = (uint64_t*)malloc(sizeof(uint64_t) * N * 2);
+    make_tables(tab, tab + N, N, Q, psi);
+    ntt_fwd_tab(a, N, Q, tab);
+    free(tab);
+}
+
+void orc_ntt_inverse(uint64_t* a, uint32_t N, uint64_t Q, uint64_t psi) {
+    uint64_t* tab = (uint64_t*)malloc(sizeof(uint64_t) * N * 2);
+    make_tables(tab, tab + N, N, Q, psi);
+    ntt_inv_tab(a, N, Q, tab + N, orc_modinv(N, Q));
+    free(tab);
+}
+
+/* PolyImpl::AutomorphismTransform EVALUATION branch (poly-impl.h:348-355) with k = 2N-1. */
+void orc_transpose_eval(const uint64_t* in, uint64_t* out, uint32_t N) {
+    uint32_t logn = ilog2u(N), mask = N - 1, k = 2 * N - 1;
+    uint64_t jk = k;
+    for (uint32_t j = 0; j < N; ++j, jk += 2ull * k) {
+        uint32_t jrev = brv(j, logn);
+        uint32_t idxrev = brv((uint32_t)((jk >> 1) & mask), logn);
+        out[jrev] = in[idxrev];
+    }
+}
+
+/* PolyImpl::AutomorphismTransform COEFFICIENT branch (poly-impl.h:357-361).
+ * Note: reproduces the reference's q - 0 = q (non-canonical) for zero entries. */
+void orc_automorphism_coeff(const uint64_t* in, uint64_t* out, uint32_t N, uint64_t Q, uint32_t k) {
+    uint32_t logn = ilog2u(N), mask = N - 1;
+    uint64_t jk = 0;
+    for (uint32_t j = 0; j < N; ++j, jk += k)
+        out[jk & mask] = ((jk >> logn) & 1) ? Q - in[j] : in[j];
+}
+
+/* ------------------------------------------------------------------------ */
+/* SignedDigitDecompose (mk-acc.cpp:54-80)                                   */
+/* ------------------------------------------------------------------------ */
+
+static inline int64_t sext_low(int64_t d, uint32_t gBits) {
+    /* (d << (W - gBits)) >> (W - gBits): sign-extend the low gBits bits */
+    uint64_t m = 1ull << gBits;
+    uint64_t low = (uint64_t)d & (m - 1);
+    return (low >= (m >> 1)) ? (int64_t)low - (int64_t)m : (int64_t)low;
+}
+
+void orc_sdd(const uint64_t* in, uint64_t* out, uint32_t N, uint64_t Q, uint32_t baseG, uint32_t dg) {
+    uint64_t QHalf = Q >> 1;
+    uint32_t gBits = (uint32_t)__builtin_ctz(baseG);
+    for (uint32_t k = 0; k < N; ++k) {
+        uint64_t t0 = in[k];
+        int64_t d0 = t0 < QHalf ? (int64_t)t0 : (int64_t)t0 - (int64_t)Q;
+        int64_t r0 = sext_low(d0, gBits);
+        d0 = (d0 - r0) >> gBits; /* lowest digit dropped (approximate gadget) */
+        for (uint32_t d = 0; d < dg; ++d) {
+            r0 = sext_low(d0, gBits);
+            d0 = (d0 - r0) >> gBits;
+            if (r0 < 0) r0 += (int64_t)Q;
+            out[(size_t)d * N + k] = (uint64_t)r0;
+        }
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* accumulator context                                                       */
+/* ------------------------------------------------------------------------ */
+
+struct orc_ctx {
+    orc_params p;
+    uint32_t dg, nk;
+    uint64_t Ninv;
+    uint64_t* tab;   /* forward table [N] */
+    uint64_t* tabI;  /* inverse table [N] */
+    uint64_t* mono;  /* [2N][N] monomials X^m - 1 in EVAL (mk-cryptoparameters.cpp:51-70) */
+};
+
+orc_ctx* orc_ctx_create(const orc_params* p) {
+    if (!p || p->N < 4 || (p->N & (p->N - 1)) || p->k == 0 || p->n == 0) return NULL;
+    if (p->baseG < 2 || (p->baseG & (p->baseG - 1))) return NULL;
+    orc_ctx* c = (orc_ctx*)calloc(1, sizeof(orc_ctx));
+    c->p = *p;
+    if (c->p.digitsG == 0) c->p.digitsG = orc_digits_g(p->Q, p->baseG);
+    if (c->p.psi == 0) c->p.psi = orc_root_of_unity(2ull * p->N, p->Q);
+    c->dg = c->p.digitsG - 1;
+    c->nk = (p->method == ORC_XZW) ? 2 : 1;
+    uint32_t N = p->N;
+    uint64_t Q = p->Q;
+    c->Ninv = orc_modinv(N, Q);
+    c->tab = (uint64_t*)malloc(sizeof(uint64_t) * N);
+    c->tabI = (uint64_t*)malloc(sizeof(uint64_t) * N);
+    make_tables(c->tab, c->tabI, N, Q, c->p.psi);
+    c->mono = (uint64_t*)calloc((size_t)2 * N * N, sizeof(uint64_t));
+    for (uint32_t i = 0; i < N; ++i) {               /* X^i - 1 */
+        uint64_t* a = c->mono + (size_t)i * N;
+        a[0] = submod(a[0], 1, Q);
+        a[i] = addmod(a[i], 1, Q);
+        ntt_fwd_tab(a, N, Q, c->tab);
+    }
+    for (uint32_t i = 0; i < N; ++i) {               /* -X^i - 1 (= X^(N+i) - 1) */
+        uint64_t* a = c->mono + (size_t)(N + i) * N;
+        a[0] = submod(a[0], 1, Q);
+        a[i] = submod(a[i], 1, Q);
+        ntt_fwd_tab(a, N, Q, c->tab);
+    }
+    return c;
+}
+
+void orc_ctx_destroy(orc_ctx* c) {
+    if (!c) return;
+    free(c->tab); free(c->tabI); free(c->mono); free(c);
+}
+
+size_t orc_evk_words(const orc_params* p) {
+    uint32_t dg = (p->digitsG ? p->digitsG : orc_digits_g(p->Q, p->baseG)) - 1;
+    uint32_t nk = (p->method == ORC_XZW) ? 2 : 1;
+    return (size_t)p->k * nk * (p->n + 1) * dg * 2 * p->N;
+}
+
+/* key poly pointer: evk[u][j][i][digit][part] */
+static inline const uint64_t* keyp(const orc_ctx* c, const uint64_t* evk, uint32_t u, uint32_t j, uint32_t i,
+                                   uint32_t digit, uint32_t part) {
+    size_t N = c->p.N;
+    size_t idx = ((((size_t)u * c->nk + j) * (c->p.n + 1) + i) * c->dg + digit) * 2 + part;
+    return evk + idx * N;
+}
+
+/* HbProd: mk-acc-xzw.cpp:231-290 (identical in mk-acc-xzw_B.cpp:221-279).
+ *   acc[u] <- sum_i NTT(g^-1(iNTT(acc[u])))_i * d_i            for every u
+ *   acc[index] += sum_i NTT(g^-1(iNTT(sum_u sum_i dct_{u,i} * P[u][i])))_i * f_i */
+static void hbprod(const orc_ctx* c, const uint64_t* d, const uint64_t* f, uint32_t index,
+                   const uint64_t* pkey, uint64_t* acc, uint64_t* scratch) {
+    const uint32_t N = c->p.N, k = c->p.k, dg = c->dg;
+    const uint64_t Q = c->p.Q;
+    uint64_t* ct = scratch;                  /* N */
+    uint64_t* dct = ct + N;                  /* dg*N */
+    uint64_t* sumV = dct + (size_t)dg * N;   /* N */
+    memset(sumV, 0, sizeof(uint64_t) * N);
+    for (uint32_t u = 0; u < k; ++u) {
+        memcpy(ct, acc + (size_t)u * N, sizeof(uint64_t) * N);
+        ntt_inv_tab(ct, N, Q, c->tabI, c->Ninv);
+        orc_sdd(ct, dct, N, Q, c->p.baseG, dg);
+        for (uint32_t i = 0; i < dg; ++i) ntt_fwd_tab(dct + (size_t)i * N, N, Q, c->tab);
+        uint64_t* out = acc + (size_t)u * N;
+        const uint64_t* Pu = pkey + (size_t)u * dg * N;
+        for (uint32_t s = 0; s < N; ++s) {
+            uint64_t uj = 0, v = 0;
+            for (uint32_t i = 0; i < dg; ++i) {
+                uint64_t g = dct[(size_t)i * N + s];
+                uj = addmod(uj, orc_mulmod(g, d[(size_t)i * N + s], Q), Q);
+                v = addmod(v, orc_mulmod(g, Pu[(size_t)i * N + s], Q), Q);
+            }
+            sumV[s] = addmod(sumV[s], v, Q);
+            out[s] = uj;
+        }
+    }
+    ntt_inv_tab(sumV, N, Q, c->tabI, c->Ninv);
+    orc_sdd(sumV, dct, N, Q, c->p.baseG, dg);
+    for (uint32_t i = 0; i < dg; ++i) ntt_fwd_tab(dct + (size_t)i * N, N, Q, c->tab);
+    uint64_t* out = acc + (size_t)index * N;
+    for (uint32_t s = 0; s < N; ++s) {
+        uint64_t w = 0;
+        for (uint32_t i = 0; i < dg; ++i)
+            w = addmod(w, orc_mulmod(dct[(size_t)i * N + s], f[(size_t)i * N + s], Q), Q);
+        out[s] = addmod(out[s], w, Q);
+    }
+}
+
+static int evalacc_one(const orc_ctx* c, const uint64_t* evk, const uint64_t* pkey, const uint64_t* ct,
+                       uint64_t* acc, uint64_t* work) {
+    const uint32_t N = c->p.N, k = c->p.k, n = c->p.n, dg = c->dg;
+    const uint64_t Q = c->p.Q, M = 2ull * N;
+    uint64_t* d = work;                          /* dg*N */
+    uint64_t* f = d + (size_t)dg * N;            /* dg*N */
+    uint64_t* acctemp = f + (size_t)dg * N;      /* k*N */
+    uint64_t* scratch = acctemp + (size_t)k * N; /* (dg+2)*N */
+    for (uint32_t u = 0; u < k; ++u) {
+        for (uint32_t i = 0; i < n; ++i) {
+            uint64_t raw = ct[(size_t)u * n + i];
+            uint64_t cval;
+            if (c->p.method == ORC_XZW) {
+                if (raw >= c->p.q) return 2;
+                cval = raw * 2 * N / c->p.q;          /* mk-acc-xzw.cpp:110,125: floor(ct*2N/q) */
+            } else {
+                if (raw > M) return 2;
+                cval = raw;                           /* mk-acc-xzw_B.cpp:119,124 */
+            }
+            uint32_t ipos = (uint32_t)(cval == M ? 0 : cval);
+            uint32_t ineg = (uint32_t)(cval == 0 ? 0 : M - cval); /* ModSubFast(0 - c) mod 2N */
+            if (ineg == M) ineg = 0;
+            const uint64_t* mono = c->mono + (size_t)ipos * N;
+            const uint64_t* monoN = c->mono + (size_t)ineg * N;
+            int first = (u == 0 && i == 0);
+            for (uint32_t dgt = 0; dgt < dg; ++dgt) {
+                for (uint32_t part = 0; part < 2; ++part) {
+                    uint64_t* out = (part == 0 ? d : f) + (size_t)dgt * N;
+                    const uint64_t* e1 = keyp(c, evk, u, 0, i, dgt, part);
+                    if (c->p.method == ORC_XZW) {
+                        const uint64_t* e2 = keyp(c, evk, u, 1, i, dgt, part);
+                        if (first) {
+                            /* AddToAccXZW0 xzw.cpp:375-378: evs + ev1*(X^c-1) + ev2*(X^-c-1) */
+                            const uint64_t* es = keyp(c, evk, u, 0, n, dgt, part);
+                            for (uint32_t s = 0; s < N; ++s)
+                                out[s] = addmod(addmod(es[s], orc_mulmod(e1[s], mono[s], Q), Q),
+                                                orc_mulmod(e2[s], monoN[s], Q), Q);
+                        } else {
+                            /* AddToAccXZW xzw.cpp:322-325: ev1 - ev2*(X^-c-1) - ev2 */
+                            for (uint32_t s = 0; s < N; ++s)
+                                out[s] = submod(submod(e1[s], orc_mulmod(e2[s], monoN[s], Q), Q), e2[s], Q);
+                        }
+                    } else {
+                        if (first) {
+                            /* AddToAccXZW0 xzw_B.cpp:368-371: evs + ev1*(X^c-1) */
+                            const uint64_t* es = keyp(c, evk, u, 0, n, dgt, part);
+                            for (uint32_t s = 0; s < N; ++s)
+                                out[s] = addmod(es[s], orc_mulmod(e1[s], mono[s], Q), Q);
+                        } else {
+                            /* AddToAccXZW xzw_B.cpp:311-314: d = ev1 */
+                            memcpy(out, e1, sizeof(uint64_t) * N);
+                        }
+                    }
+                }
+            }
+            if (first) {
+                hbprod(c, d, f, u, pkey, acc, scratch); /* acc is REPLACED (xzw.cpp:380) */
+            } else {
+                /* acctemp = acc * (X^c - 1); HbProd(acctemp); acc += acctemp (xzw.cpp:327-344) */
+                for (uint32_t w = 0; w < k; ++w)
+                    for (uint32_t s = 0; s < N; ++s)
+                        acctemp[(size_t)w * N + s] = orc_mulmod(acc[(size_t)w * N + s], mono[s], Q);
+                hbprod(c, d, f, u, pkey, acctemp, scratch);
+                for (size_t s = 0; s < (size_t)k * N; ++s) acc[s] = addmod(acc[s], acctemp[s], Q);
+            }
+        }
+    }
+    return 0;
+}
+
+static size_t work_words(const orc_ctx* c) {
+    return (size_t)c->p.N * (2 * c->dg + c->p.k + c->dg + 2);
+}
+
+int orc_evalacc(const orc_ctx* c, const uint64_t* evk, const uint64_t* pkey, const uint64_t* ct, uint64_t* acc) {
+    if (!c) return 1;
+    uint64_t* work = (uint64_t*)malloc(sizeof(uint64_t) * work_words(c));
+    int rc = evalacc_one(c, evk, pkey, ct, acc, work);
+    free(work);
+    return rc;
+}
+
+int orc_evalacc_batch(const orc_ctx* c, const uint64_t* evk, const uint64_t* pkey, const uint64_t* ct,
+                      uint64_t* acc, size_t B, int threads) {
+    if (!c) return 1;
+    int rc = 0;
+    const size_t ctw = (size_t)c->p.k * c->p.n, accw = (size_t)c->p.k * c->p.N;
+#ifdef _OPENMP
+    if (threads < 1) threads = 1;
+#pragma omp parallel num_threads(threads) reduction(| : rc)
+    {
+        uint64_t* work = (uint64_t*)malloc(sizeof(uint64_t) * work_words(c));
+#pragma omp for schedule(dynamic, 1)
+        for (long g = 0; g < (long)B; ++g) rc |= evalacc_one(c, evk, pkey, ct + g * ctw, acc + g * accw, work);
+        free(work);
+    }
+#else
+    (void)threads;
+    uint64_t* work = (uint64_t*)malloc(sizeof(uint64_t) * work_words(c));
+    for (size_t g = 0; g < B; ++g) rc |= evalacc_one(c, evk, pkey, ct + g * ctw, acc + g * accw, work);
+    free(work);
+#endif
+    return rc;
+}
+
+/* ------------------------------------------------------------------------ */
+/* test vectors                                                              */
+/* ------------------------------------------------------------------------ */
+
+static inline uint64_t splitmix64(uint64_t* s) {
+    uint64_t z = (*s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+/* Uniform in [0, bound) by 128-bit multiply-shift of a SplitMix64 stream
+ * (bias < 2^-32 for bound < 2^32, irrelevant for bit-exactness tests). */
+void orc_fill_uniform(uint64_t* out, size_t n, uint64_t bound, uint64_t seed) {
+    uint64_t s = seed;
+    for (size_t i = 0; i < n; ++i) out[i] = (uint64_t)(((u128)splitmix64(&s) * bound) >> 64);
+}
+
+void orc_fill_uniform_u32(uint32_t* out, size_t n, uint64_t bound, uint64_t seed) {
+    uint64_t s = seed;
+    for (size_t i = 0; i < n; ++i) out[i] = (uint32_t)(((u128)splitmix64(&s) * bound) >> 64);
+}
+
+/* BootstrapGateCore (MNTRU) test vector, binfhe-base-scheme.cpp:1085-1115:
+ * Q2p = Q/(2p)+1; Rx[j] = j < N/2 ? Q - Q2p : Q2p; acc[0] = NTT(Rx); acc[u>0] = 0. */
+void orc_mntru_testvector(const orc_ctx* c, uint64_t p, uint64_t* acc) {
+    const uint32_t N = c->p.N;
+    const uint64_t Q = c->p.Q, Q2p = Q / (2 * p) + 1, Q2pNeg = Q - Q2p;
+    memset(acc, 0, sizeof(uint64_t) * (size_t)c->p.k * N);
+    for (uint32_t j = 0; j < N; ++j) acc[j] = j < N / 2 ? Q2pNeg : Q2p;
+    ntt_fwd_tab(acc, N, Q, c->tab);
+}

@@ -1,0 +1,162 @@
+"""Bit-exact parity of the HIP engine (through the C ABI) against the CPU oracle.
+
+Small-n cases run every code path (first KDM step, later steps, both methods,
+every supported digit count) at the real ring size N = 2048; the full-size
+cases run the reference parameter sets end to end on a few gates.
+"""
+import numpy as np
+import pytest
+
+from conftest import Q_MK, make_case
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def mk():
+    import mkfhe_amd
+    return mkfhe_amd
+
+
+def _engine(mk, method, k, n, q, baseG):
+    p = mk.make_params(method, k, n, 2048, Q_MK, q, baseG)
+    return mk.MKAccumulatorEngine(p)
+
+
+def test_native_library_loaded(mk):
+    import mkfhe_amd._lib as L
+    lib = L.load()
+    assert lib.mkacc_abi_version() == 1
+
+
+def test_ntt_forward_inverse_parity(mk, oracle):
+    eng = _engine(mk, mk.MKNTRU, 2, 4, 45181, 1 << 9)
+    psi = oracle.root_of_unity(4096, Q_MK)
+    a = oracle.fill_uniform(7 * 2048, Q_MK, 77).reshape(7, 2048)
+    fw = eng.ntt_forward(a.astype(np.uint32))
+    for i in range(7):
+        assert np.array_equal(fw[i], oracle.ntt_forward(a[i], Q_MK, psi).astype(np.uint32)), i
+    inv = eng.ntt_inverse(fw)
+    assert np.array_equal(inv, a.astype(np.uint32))
+    for i in range(7):
+        assert np.array_equal(eng.ntt_inverse(a[i:i + 1].astype(np.uint32))[0],
+                              oracle.ntt_inverse(a[i], Q_MK, psi).astype(np.uint32))
+
+
+def test_ntt_edge_values(mk, oracle):
+    eng = _engine(mk, mk.MKNTRU, 2, 4, 45181, 1 << 9)
+    psi = oracle.root_of_unity(4096, Q_MK)
+    cases = np.stack([np.zeros(2048), np.full(2048, Q_MK - 1), np.eye(1, 2048, 0)[0],
+                      np.eye(1, 2048, 2047)[0]]).astype(np.uint64)
+    fw = eng.ntt_forward(cases.astype(np.uint32))
+    for i in range(len(cases)):
+        assert np.array_equal(fw[i], oracle.ntt_forward(cases[i], Q_MK, psi).astype(np.uint32))
+
+
+@pytest.mark.parametrize("logB", [9, 7, 6, 5])
+def test_sdd_parity(mk, oracle, logB):
+    eng = _engine(mk, mk.MKNTRU, 2, 4, 45181, 1 << logB)
+    x = oracle.fill_uniform(3 * 2048, Q_MK, 5 + logB).reshape(3, 2048)
+    x[0, :8] = [0, 1, Q_MK // 2 - 1, Q_MK // 2, Q_MK // 2 + 1, Q_MK - 1, (1 << logB) // 2, (1 << logB)]
+    got = eng.sdd(x.astype(np.uint32))
+    for i in range(3):
+        exp = oracle.sdd(x[i], Q_MK, 1 << logB, eng.dg)
+        assert np.array_equal(got[i], exp.astype(np.uint32))
+
+
+CASES = [
+    # method, k, n, q, baseG, B
+    ("XZW", 2, 4, 45181, 1 << 9, 3),      # STD100_MKNTRU shape, dg=2
+    ("XZW", 2, 5, 45181, 1 << 7, 2),      # STD128_MKNTRU shape, dg=3
+    ("XZW", 3, 3, 45181, 1 << 6, 2),      # dg=4
+    ("XZW", 2, 3, 45181, 1 << 5, 2),      # dg=5 (STD128_MKNTRU_4 base)
+    ("XZW_B", 2, 4, 32749, 1 << 9, 3),    # STD100_MKNTRU_LWE shape
+    ("XZW_B", 4, 3, 32749, 1 << 9, 2),    # 4 parties
+    ("XZW_B", 2, 3, 32749, 1 << 7, 2),    # dg=3
+    ("XZW", 1, 6, 45181, 1 << 9, 2),      # single party
+    ("XZW", 5, 2, 45181, 1 << 9, 5),      # odd party count, odd batch
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[f"{c[0]}-k{c[1]}-n{c[2]}-B{c[4]}" for c in CASES])
+def test_evalacc_small_parity(mk, oracle, case):
+    meth, k, n, q, baseG, B = case
+    om = oracle.XZW if meth == "XZW" else oracle.XZW_B
+    em = mk.MKNTRU if meth == "XZW" else mk.MKNTRU_LWE
+    orc, evk, pkey, ct, acc = make_case(oracle, om, k, n, q, baseG, B, seed=k * 100 + n)
+    # exercise the monomial edge cases c = 0 and c = 2N-1 (and 2N for XZW_B)
+    ct[0, 0, 0] = 0
+    if om == oracle.XZW:
+        ct[0, k - 1, n - 1] = q - 1
+    else:
+        ct[0, k - 1, n - 1] = 4096
+        ct[-1, 0, n - 1] = 4095
+    exp = orc.evalacc_batch(evk, pkey, ct, acc, 8)
+    eng = mk.MKAccumulatorEngine(mk.make_params(em, k, n, 2048, Q_MK, q, baseG))
+    eng.upload_keys(evk.astype(np.uint32), pkey.astype(np.uint32))
+    got = eng.eval_batch(ct.astype(np.uint32), acc.astype(np.uint32))
+    assert np.array_equal(got, exp.astype(np.uint32))
+    # u64 upload path gives the same
+    eng.upload_keys(evk, pkey)
+    assert np.array_equal(eng.eval_batch(ct.astype(np.uint32), acc.astype(np.uint32)), got)
+
+
+def test_interface_mirror_evalacc(mk, oracle):
+    """UniEncAccumulatorXZW.EvalAcc updates acc in place like the reference."""
+    orc, evk, pkey, ct, acc = make_case(oracle, oracle.XZW, 2, 3, 45181, 1 << 9, 1, seed=9)
+    exp = orc.evalacc(evk, pkey, ct[0], acc[0]).astype(np.uint32)
+    accm = mk.accumulator_for(mk.make_params(mk.MKNTRU, 2, 3, 2048, Q_MK, 45181, 1 << 9))
+    assert isinstance(accm, mk.UniEncAccumulatorXZW)
+    a = acc[0].astype(np.uint32).copy()
+    accm.EvalAcc(evk.astype(np.uint32), pkey.astype(np.uint32), None, a, ct[0].astype(np.uint32))
+    assert np.array_equal(a, exp)
+
+
+@pytest.mark.parametrize("name,B", [("STD100_MKNTRU", 2), ("STD128_MKNTRU", 2), ("STD100_MKNTRU_LWE", 2)])
+def test_evalacc_full_paramset_parity(mk, oracle, name, B):
+    p = mk.paramset(name)
+    om = oracle.XZW if p.method == mk.MKNTRU else oracle.XZW_B
+    orc, evk, pkey, ct, acc = make_case(oracle, om, p.k, p.n, p.q, p.baseG, B, seed=p.n)
+    # start from the BootstrapGateCore test vector (binfhe-base-scheme.cpp:1093-1115)
+    acc[:] = orc.mntru_testvector(4)
+    exp = orc.evalacc_batch(evk, pkey, ct, acc, 8)
+    eng = mk.MKAccumulatorEngine(p)
+    eng.upload_keys(evk.astype(np.uint32), pkey.astype(np.uint32))
+    got = eng.eval_batch(ct.astype(np.uint32), acc.astype(np.uint32))
+    assert np.array_equal(got, exp.astype(np.uint32))
+
+
+def test_batch_invariance(mk, oracle):
+    """Gates are independent: permuting / duplicating the batch permutes the output."""
+    orc, evk, pkey, ct, acc = make_case(oracle, oracle.XZW, 2, 4, 45181, 1 << 7, 9, seed=3)
+    eng = _engine(mk, mk.MKNTRU, 2, 4, 45181, 1 << 7)
+    eng.upload_keys(evk.astype(np.uint32), pkey.astype(np.uint32))
+    out = eng.eval_batch(ct.astype(np.uint32), acc.astype(np.uint32))
+    perm = np.array([8, 3, 3, 0, 7, 1, 1, 2, 5])
+    out2 = eng.eval_batch(ct[perm].astype(np.uint32), acc[perm].astype(np.uint32))
+    assert np.array_equal(out2, out[perm])
+    single = eng.eval_batch(ct[4:5].astype(np.uint32), acc[4:5].astype(np.uint32))
+    assert np.array_equal(single[0], out[4])
+
+
+def test_errors(mk, oracle):
+    eng = _engine(mk, mk.MKNTRU, 2, 3, 45181, 1 << 9)
+    ct = np.zeros((1, 2, 3), np.uint32)
+    acc = np.zeros((1, 2, 2048), np.uint32)
+    with pytest.raises(mk.MkaccError) as e:
+        eng.eval_batch(ct, acc)                          # keys not uploaded
+    assert e.value.code == -3
+    evk = np.zeros(eng.evk_shape, np.uint32)
+    pkey = np.zeros(eng.pkey_shape, np.uint32)
+    eng.upload_keys(evk, pkey)
+    with pytest.raises(mk.MkaccError) as e:
+        eng.eval_batch(np.full((1, 2, 3), 45181, np.uint32), acc)   # ct >= q
+    assert e.value.code == -5
+    with pytest.raises(mk.MkaccError) as e:
+        eng.eval_batch(ct, np.full((1, 2, 2048), Q_MK, np.uint32))  # non-canonical acc
+    assert e.value.code == -5
+    bad = evk.copy()
+    bad.flat[123] = Q_MK
+    with pytest.raises(mk.MkaccError):
+        eng.upload_keys(bad, pkey)
+    assert eng.eval_batch(ct[:0], acc[:0]).shape == (0, 2, 2048)

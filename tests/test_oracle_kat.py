@@ -1,0 +1,67 @@
+"""Pin the CPU oracle against the reference's own known-answer vectors.
+
+Every expected value below is copied from a reference unit test (the test
+file:line is cited per case).  These are the only reference-held vectors that
+touch this path: the reference has no MK/accumulator tests.
+"""
+import numpy as np
+import pytest
+
+
+def test_first_prime_kat(oracle):
+    # src/core/unittest/UnitTestNbTheory.cpp:170-175 and :178-185
+    assert oracle.first_prime(30, 2048) == 1073750017
+    assert oracle.first_prime(49, 4096) == 562949953548289
+
+
+def test_mk_ring_modulus_and_root(oracle):
+    # binfhecontext.cpp:157-158: Q = PreviousPrime(FirstPrime(27, 4096), 4096); SURVEY.md s0 [probe]
+    Q = oracle.previous_prime(oracle.first_prime(27, 4096), 4096)
+    assert Q == 134176769
+    assert oracle.root_of_unity(4096, Q) == 100530
+    # cfg5 stress modulus/root quoted in SURVEY.md s0 item 2 [probe]
+    assert oracle.root_of_unity(4096, 1125899906826241) == 1080667890455
+
+
+def test_switch_format_forward_kat(oracle):
+    # src/core/unittest/UnitTestPolyElements.cpp:388-399 (m=8, q=73, root 22)
+    assert list(oracle.ntt_forward([2, 1, 3, 2], 73, 22)) == [69, 65, 44, 49]
+
+
+def test_switch_format_inverse_kat(oracle):
+    # src/core/unittest/UnitTestPolyElements.cpp:401-411
+    assert list(oracle.ntt_inverse([2, 3, 1, 2], 73, 22)) == [2, 3, 50, 3]
+
+
+def test_transpose_kat(oracle):
+    # src/core/unittest/UnitTestPolyElements.cpp:540-571
+    x = oracle.ntt_forward([31, 21, 15, 34], 73, 22)
+    y = oracle.ntt_inverse(oracle.transpose_eval(x), 73, 22)
+    assert list(y) == [31, 39, 58, 52]
+
+
+def test_automorphism_kat(oracle):
+    # src/core/unittest/UnitTestPolyElements.cpp:512-521
+    assert list(oracle.automorphism_coeff([56, 1, 37, 2], 73, 3)) == [56, 2, 36, 1]
+
+
+def test_crt_polynomial_mult_kat(oracle):
+    # src/core/unittest/UnitTestTransform.cpp:58-93 (q=113, m=8, RootOfUnity(8,113))
+    root = oracle.root_of_unity(8, 113)
+    A = oracle.ntt_forward([1, 2, 4, 1], 113, root)
+    assert list(oracle.ntt_inverse(A * A % 113, 113, root)) == [94, 109, 11, 18]
+
+
+def test_root_is_minimal_primitive(oracle):
+    # nbtheory-impl.h:212-230: the minimum over all primitive m-th roots
+    Q, m = 134176769, 4096
+    psi = oracle.root_of_unity(m, Q)
+    roots = [pow(psi, e, Q) for e in range(1, m, 2)]
+    assert psi == min(roots)
+    assert pow(psi, m // 2, Q) == Q - 1
+
+
+@pytest.mark.parametrize("logB,expect", [(5, 6), (6, 5), (7, 4), (9, 3)])
+def test_digits_g(oracle, logB, expect):
+    # mk-cryptoparameters.h:141-142; SURVEY.md Appendix A "digitsG" column
+    assert oracle.digits_g(134176769, 1 << logB) == expect
