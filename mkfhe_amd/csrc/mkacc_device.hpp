@@ -102,9 +102,10 @@ __device__ __forceinline__ uint32_t jC(uint32_t l, uint32_t r) { return (l << 5)
 __device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0); }
 
 __device__ __forceinline__ void wave_lds_sync() {
-    // LDS ops of one wave execute in order; this keeps the compiler from
-    // moving reads above writes and waits for the writes to land.
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // A wave's LDS instructions execute in issue order, so a read after the
+    // wave's own writes sees them and later writes cannot overtake earlier
+    // reads: only the compiler must be kept from reordering (no s_waitcnt).
+    asm volatile("" ::: "memory");
 }
 
 template <int LAYOUT>
@@ -130,16 +131,28 @@ __device__ __forceinline__ void transpose(uint32_t (&x)[kRegs], uint32_t* lds, u
 
 // ---- forward NTT (Cooley-Tukey, reference table indexing) -------------------
 // tw[i] = { psi^brv(i), companion }, i in [0, N): reference rootOfUnityTable.
+// Lazy (Harvey) butterflies: the forward NTT keeps values in [0, 4Q), the
+// inverse in [0, 2Q) (4Q < 2^29, so nothing overflows 32 bits).  Shoup's
+// product q*Q - x*w is formed negated so both outputs take one instruction.
 __device__ __forceinline__ void ct_bfly(uint32_t& a, uint32_t& b, uint2 w, uint32_t Q) {
-    uint32_t V = mul_shoup(b, w.x, w.y, Q);
-    uint32_t U = a;
-    a = add_mod(U, V, Q);
-    b = sub_mod(U, V, Q);
+    const uint32_t X = min(a, a - 2u * Q);                      // [0, 2Q)
+    const uint32_t q = __umulhi(b, w.y);
+    const uint32_t Tn = q * Q - b * w.x;                         // -(b*w mod~ Q), T in [0, 2Q)
+    a = X - Tn;                                                  // X + T      in [0, 4Q)
+    b = X + Tn + 2u * Q;                                         // X - T + 2Q in (0, 4Q)
 }
 __device__ __forceinline__ void gs_bfly(uint32_t& a, uint32_t& b, uint2 w, uint32_t Q) {
-    uint32_t lo = a, hi = b;
-    a = add_mod(lo, hi, Q);
-    b = mul_shoup(sub_mod(lo, hi, Q), w.x, w.y, Q);
+    const uint32_t lo = a, hi = b;                               // [0, 2Q)
+    const uint32_t s = lo + hi;
+    a = min(s, s - 2u * Q);                                      // [0, 2Q)
+    const uint32_t d = lo - hi + 2u * Q;                         // (0, 4Q)
+    const uint32_t q = __umulhi(d, w.y);
+    b = d * w.x - q * Q;                                         // [0, 2Q)
+}
+// [0, 4Q) -> [0, Q)
+__device__ __forceinline__ uint32_t canon4(uint32_t x, uint32_t Q) {
+    x = min(x, x - 2u * Q);
+    return min(x, x - Q);
 }
 
 // Wave-uniform table reads go through the constant address space so they are
@@ -186,30 +199,43 @@ __device__ __forceinline__ void load_pairs(uint2 (&w)[NP], const uint2* p) {
 // forward pass-B stage s (5..9) on bit 10-s: twiddle 2^s + (lhi << (s-5)) + (r >> (10-s))
 template <int S>
 __device__ __forceinline__ void fwd_stage_b(uint32_t (&x)[kRegs], const uint2* tw, uint32_t lhi, uint32_t Q) {
-    constexpr int NP = 1 << (S - 5), H = 1 << (9 - S);
-    uint2 w[NP];
-    load_pairs<NP>(w, tw + (1u << S) + (lhi << (S - 5)));
+    // twiddle runs longer than 8 pairs are processed in chunks of 8 to cap the
+    // live twiddle registers at 16
+    constexpr int NP = 1 << (S - 5), H = 1 << (9 - S), CH = NP > 8 ? 8 : NP, SH = 10 - S;
 #pragma unroll
-    for (int r = 0; r < kRegs; ++r) {
-        if (r & H) continue;
-        ct_bfly(x[r], x[r + H], w[r >> (10 - S)], Q);
+    for (int c0 = 0; c0 < NP; c0 += CH) {
+        uint2 w[CH];
+        load_pairs<CH>(w, tw + (1u << S) + (lhi << (S - 5)) + c0);
+#pragma unroll
+        for (int r = 0; r < kRegs; ++r) {
+            if (r & H) continue;
+            const int m = r >> SH;
+            if (m < c0 || m >= c0 + CH) continue;
+            ct_bfly(x[r], x[r + H], w[m - c0], Q);
+        }
+        sched_fence();
     }
-    sched_fence();
 }
 // inverse pass-B stage on bit B (1..5): twiddle 2^(10-B) + (lhi << (5-B)) + (r >> B)
 template <int B>
 __device__ __forceinline__ void inv_stage_b(uint32_t (&x)[kRegs], const uint2* twi, uint32_t lhi, uint32_t Q) {
-    constexpr int NP = 1 << (5 - B), H = 1 << (B - 1);
-    uint2 w[NP];
-    load_pairs<NP>(w, twi + (1u << (10 - B)) + (lhi << (5 - B)));
+    constexpr int NP = 1 << (5 - B), H = 1 << (B - 1), CH = NP > 8 ? 8 : NP;
 #pragma unroll
-    for (int r = 0; r < kRegs; ++r) {
-        if (r & H) continue;
-        gs_bfly(x[r], x[r + H], w[r >> B], Q);
+    for (int c0 = 0; c0 < NP; c0 += CH) {
+        uint2 w[CH];
+        load_pairs<CH>(w, twi + (1u << (10 - B)) + (lhi << (5 - B)) + c0);
+#pragma unroll
+        for (int r = 0; r < kRegs; ++r) {
+            if (r & H) continue;
+            const int m = r >> B;
+            if (m < c0 || m >= c0 + CH) continue;
+            gs_bfly(x[r], x[r + H], w[m - c0], Q);
+        }
+        sched_fence();
     }
-    sched_fence();
 }
 
+// Input residues in [0, 4Q); output EVAL values in [0, 4Q) (not canonical).
 __device__ __forceinline__ void ntt_fwd(uint32_t (&x)[kRegs], uint32_t* lds, const uint2* tw_in,
                                         uint32_t l, uint32_t Q) {
     const uint2* tw = opaque(tw_in);
@@ -249,6 +275,7 @@ __device__ __forceinline__ void ntt_fwd(uint32_t (&x)[kRegs], uint32_t* lds, con
 
 // ---- inverse NTT WITHOUT the N^-1 factor (Gentleman-Sande) -------------------
 // twi[i] = { psi^-brv(i), companion }: reference rootOfUnityInverseTable.
+// Input residues in [0, 2Q); output canonical coefficients in [0, Q).
 __device__ __forceinline__ void ntt_inv_noscale(uint32_t (&x)[kRegs], uint32_t* lds, const uint2* twi_in,
                                                 uint32_t l, uint32_t Q) {
     const uint2* twi = opaque(twi_in);
@@ -284,6 +311,8 @@ __device__ __forceinline__ void ntt_inv_noscale(uint32_t (&x)[kRegs], uint32_t* 
         }
         sched_fence();
     }
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) x[r] = min(x[r], x[r] - Q);
 }
 
 // ---- device EVAL layout in HBM ("C4") --------------------------------------
@@ -351,6 +380,9 @@ struct PackedDigits {
         }
         if (kPer == 1 || (r % kPer) == 0) w[r / kPer] = acc;
         else w[r / kPer] |= acc << kSlot;
+        // pin the packed word here: otherwise the compiler sinks the packing to
+        // the later unpack and keeps every unpacked digit live across the NTTs
+        if ((r % kPer) == kPer - 1) asm volatile("" : "+v"(w[r / kPer]));
         return g0;
     }
     // digit i (1..DG-1) of element r as a residue

@@ -114,56 +114,48 @@ __device__ __forceinline__ uint32_t key_eff(uint32_t k1, uint32_t k2, uint32_t k
     }
 }
 
-// MAC of digit i of party u into the accumulator output and the sumV scratch:
-//   out[u] (+)= NTT(g_i) * d_i                (xzw.cpp:263-266, acc[u] = uj)
-//   sumV   (+)= NTT(g_i) * P[u][i]            (xzw.cpp:264-269)
+// Register-resident HbProd (mk-acc-xzw.cpp:231-290) for one gate per wave.
+// The per-slot sums uj_u = sum_i g_i d_i, sumV = sum_u sum_i g_i P[u][i] and
+// w = sum_i h_i f_i are kept as lazy 64-bit accumulators (v_mad_u64_u32) and
+// reduced once; every operand is canonical, so a sum of up to 16 products
+// stays below 2^58 (reduce58).
 template <int DG, int METHOD, bool FIRST>
-__device__ __forceinline__ void mac_party(const uint32_t (&g)[kRegs], int i, uint32_t u, const StepArgs& a,
-                                          __amdgpu_buffer_rsrc_t rin, __amdgpu_buffer_rsrc_t rout,
-                                          __amdgpu_buffer_rsrc_t rv, __amdgpu_buffer_rsrc_t rk1,
-                                          __amdgpu_buffer_rsrc_t rk2, __amdgpu_buffer_rsrc_t rks,
-                                          __amdgpu_buffer_rsrc_t rpk, __amdgpu_buffer_rsrc_t rpp, uint32_t c,
-                                          uint32_t cneg, uint32_t l) {
+__device__ __forceinline__ void mac_digit(const uint32_t (&g)[kRegs], int i, uint32_t u, const StepArgs& a,
+                                          uint64_t (&uj)[kRegs], uint64_t (&sv)[kRegs],
+                                          __amdgpu_buffer_rsrc_t rk1, __amdgpu_buffer_rsrc_t rk2,
+                                          __amdgpu_buffer_rsrc_t rks, __amdgpu_buffer_rsrc_t rpk,
+                                          __amdgpu_buffer_rsrc_t rpp, uint32_t c, uint32_t cneg, uint32_t l) {
     const uint32_t Q = a.m.Q;
     const uint32_t polyB = kN * 4u, vo = l * 16u;
-    const uint32_t uoff = u * polyB;
     const uint32_t koff = (uint32_t)(2 * i) * polyB;
     const uint32_t poff = (u * DG + (uint32_t)i) * polyB;
-    const bool first_v = (u == 0 && i == 0);
 #pragma unroll
     for (int gq = 0; gq < 8; ++gq) {
         const uint32_t go = gq * 1024u;
         const uint32_t lq = opaque_v(l);   // keep slot exponents from being hoisted (VGPR pressure)
         const u32x4 k1 = bload4(rk1, vo, koff + go);
         const u32x4 pk = bload4(rpk, vo, poff + go);
-        u32x4 k2 = {0, 0, 0, 0}, ks = {0, 0, 0, 0}, prev = {0, 0, 0, 0}, vv = {0, 0, 0, 0};
+        u32x4 k2 = {0, 0, 0, 0}, ks = {0, 0, 0, 0};
         if (METHOD == XZW) k2 = bload4(rk2, vo, koff + go);
         if (FIRST) ks = bload4(rks, vo, koff + go);
-        if (!(FIRST && i == 0)) prev = bload4(i == 0 ? rin : rout, vo, uoff + go);
-        if (!first_v) vv = bload4(rv, vo, go);
-        u32x4 o;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const int r = 4 * gq + e;
             const uint32_t deff = key_eff<METHOD, FIRST>(k1[e], k2[e], ks[e], rpp, c, cneg, lq, r, Q);
-            o[e] = reduce58(mad64(g[r], deff, prev[e]), a.m);
-            vv[e] = reduce58(mad64(g[r], pk[e], vv[e]), a.m);
+            uj[r] = mad64(g[r], deff, uj[r]);
+            sv[r] = mad64(g[r], pk[e], sv[r]);
         }
-        bstore4(o, rout, vo, uoff + go);
-        bstore4(vv, rv, vo, go);
         sched_fence();
     }
 }
 
-// acc[index] += NTT(h_i) * f_i                   (xzw.cpp:281-288)
 template <int METHOD, bool FIRST>
-__device__ __forceinline__ void mac_index(const uint32_t (&h)[kRegs], int i, const StepArgs& a,
-                                          __amdgpu_buffer_rsrc_t rout, __amdgpu_buffer_rsrc_t rk1,
-                                          __amdgpu_buffer_rsrc_t rk2, __amdgpu_buffer_rsrc_t rks,
-                                          __amdgpu_buffer_rsrc_t rpp, uint32_t c, uint32_t cneg, uint32_t l) {
+__device__ __forceinline__ void mac_index(const uint32_t (&h)[kRegs], int i, const StepArgs& a, uint64_t (&w)[kRegs],
+                                          __amdgpu_buffer_rsrc_t rk1, __amdgpu_buffer_rsrc_t rk2,
+                                          __amdgpu_buffer_rsrc_t rks, __amdgpu_buffer_rsrc_t rpp, uint32_t c,
+                                          uint32_t cneg, uint32_t l) {
     const uint32_t Q = a.m.Q;
     const uint32_t polyB = kN * 4u, vo = l * 16u;
-    const uint32_t ioff = a.index * polyB;
     const uint32_t koff = (uint32_t)(2 * i + 1) * polyB;
 #pragma unroll
     for (int gq = 0; gq < 8; ++gq) {
@@ -173,27 +165,29 @@ __device__ __forceinline__ void mac_index(const uint32_t (&h)[kRegs], int i, con
         u32x4 k2 = {0, 0, 0, 0}, ks = {0, 0, 0, 0};
         if (METHOD == XZW) k2 = bload4(rk2, vo, koff + go);
         if (FIRST) ks = bload4(rks, vo, koff + go);
-        u32x4 t = bload4(rout, vo, ioff + go);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const int r = 4 * gq + e;
             const uint32_t feff = key_eff<METHOD, FIRST>(k1[e], k2[e], ks[e], rpp, c, cneg, lq, r, Q);
-            t[e] = reduce58(mad64(h[r], feff, t[e]), a.m);
+            w[r] = mad64(h[r], feff, w[r]);
         }
-        bstore4(t, rout, vo, ioff + go);
         sched_fence();
     }
 }
 
 template <int DG, int METHOD, bool FIRST>
-__global__ __launch_bounds__(kThreads, 3) void mk_step_kernel(StepArgs a) {
+__global__ __launch_bounds__(kThreads, 2) void mk_step_kernel(StepArgs a) {
+    // register allocation fits without spills when the digit loop is unrolled
+    // for DG = 2 and kept rolled for DG >= 3 (measured, hipcc ROCm 7.2)
+    constexpr int kDigitUnroll = DG == 2 ? 2 : 1;
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const uint32_t l = threadIdx.x & 63u;
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t gate = blockIdx.x * kWavesPerBlock + wv;
     if (gate >= a.B) return;
     uint32_t* lds = smem + wv * kLdsWords;
-    const uint32_t Q = a.m.Q;
+    const Mod m = a.m;
+    const uint32_t Q = m.Q;
     const uint32_t c = __builtin_amdgcn_readfirstlane(a.cvals[gate]);
     const uint32_t cneg = (2u * kN - c) & (2u * kN - 1u);
     const uint32_t k = a.k;
@@ -202,12 +196,15 @@ __global__ __launch_bounds__(kThreads, 3) void mk_step_kernel(StepArgs a) {
 
     const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.acc_in + (size_t)gate * k * kN, k * polyB);
     const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.acc_out + (size_t)gate * k * kN, k * polyB);
-    const __amdgpu_buffer_rsrc_t rv = make_rsrc(a.sumv + (size_t)gate * kN, polyB);
     const __amdgpu_buffer_rsrc_t rk1 = make_rsrc(a.key1, DG * 2 * polyB);
     const __amdgpu_buffer_rsrc_t rk2 = make_rsrc(a.key2, DG * 2 * polyB);
     const __amdgpu_buffer_rsrc_t rks = make_rsrc(a.keys, DG * 2 * polyB);
     const __amdgpu_buffer_rsrc_t rpk = make_rsrc(a.pkey, k * DG * polyB);
     const __amdgpu_buffer_rsrc_t rpp = make_rsrc(a.psi_pow, 2u * kN * 8u);
+
+    uint64_t sv[kRegs];
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) sv[r] = 0;
 
     for (uint32_t u = 0; u < k; ++u) {
         uint32_t x[kRegs];
@@ -233,37 +230,71 @@ __global__ __launch_bounds__(kThreads, 3) void mk_step_kernel(StepArgs a) {
         // SignedDigitDecompose (mk-acc.cpp:54-80): digit 0 -> x, digits 1.. packed
         PackedDigits<DG> pd;
 #pragma unroll
-        for (int r = 0; r < kRegs; ++r) x[r] = pd.put(r, x[r], Q, a.qhalf, a.gbits);
-        ntt_fwd(x, lds, a.tw_fwd, l, Q);
-        mac_party<DG, METHOD, FIRST>(x, 0, u, a, rin, rout, rv, rk1, rk2, rks, rpk, rpp, c, cneg, l);
+        for (int r = 0; r < kRegs; ++r) {
+            x[r] = pd.put(r, x[r], Q, a.qhalf, a.gbits);
+            if ((r & 7) == 7) sched_fence();
+        }
+        uint64_t uj[kRegs];
 #pragma unroll
-        for (int i = 1; i < DG; ++i) {
+        for (int r = 0; r < kRegs; ++r) uj[r] = 0;
+#pragma unroll kDigitUnroll
+        for (int i = 0; i < DG; ++i) {
+            if (i > 0) {
 #pragma unroll
-            for (int r = 0; r < kRegs; ++r) x[r] = pd.get(r, i, Q);
+                for (int r = 0; r < kRegs; ++r) x[r] = pd.get(r, i, Q);
+            }
             ntt_fwd(x, lds, a.tw_fwd, l, Q);
-            mac_party<DG, METHOD, FIRST>(x, i, u, a, rin, rout, rv, rk1, rk2, rks, rpk, rpp, c, cneg, l);
+#pragma unroll
+            for (int r = 0; r < kRegs; ++r) x[r] = canon4(x[r], Q);
+            mac_digit<DG, METHOD, FIRST>(x, i, u, a, uj, sv, rk1, rk2, rks, rpk, rpp, c, cneg, l);
+        }
+        // acc_u <- (FIRST ? 0 : acc_u) + uj_u   (xzw.cpp:270, 342-344); sumV reduced per party
+#pragma unroll
+        for (int gq = 0; gq < 8; ++gq) {
+            u32x4 t = {0, 0, 0, 0};
+            if (!FIRST) t = bload4(rin, vo, u * polyB + gq * 1024u);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int r = 4 * gq + e;
+                t[e] = reduce58(uj[r] + t[e], m);
+                sv[r] = reduce58(sv[r], m);
+            }
+            bstore4(t, rout, vo, u * polyB + gq * 1024u);
         }
     }
 
     // second half of HbProd: iNTT(sumV) -> SDD -> NTT -> acc[index] += <., f>
     uint32_t x[kRegs];
 #pragma unroll
-    for (int gq = 0; gq < 8; ++gq) {
-        const u32x4 t = bload4(rv, vo, gq * 1024u);
-        x[4 * gq] = t.x; x[4 * gq + 1] = t.y; x[4 * gq + 2] = t.z; x[4 * gq + 3] = t.w;
-    }
+    for (int r = 0; r < kRegs; ++r) x[r] = (uint32_t)sv[r];
     ntt_inv_noscale(x, lds, a.tw_inv, l, Q);
     PackedDigits<DG> pd;
 #pragma unroll
-    for (int r = 0; r < kRegs; ++r) x[r] = pd.put(r, x[r], Q, a.qhalf, a.gbits);
-    ntt_fwd(x, lds, a.tw_fwd, l, Q);
-    mac_index<METHOD, FIRST>(x, 0, a, rout, rk1, rk2, rks, rpp, c, cneg, l);
+    for (int r = 0; r < kRegs; ++r) {
+        x[r] = pd.put(r, x[r], Q, a.qhalf, a.gbits);
+        if ((r & 7) == 7) sched_fence();
+    }
+    uint64_t w[kRegs];
 #pragma unroll
-    for (int i = 1; i < DG; ++i) {
+    for (int r = 0; r < kRegs; ++r) w[r] = 0;
+#pragma unroll kDigitUnroll
+    for (int i = 0; i < DG; ++i) {
+        if (i > 0) {
 #pragma unroll
-        for (int r = 0; r < kRegs; ++r) x[r] = pd.get(r, i, Q);
+            for (int r = 0; r < kRegs; ++r) x[r] = pd.get(r, i, Q);
+        }
         ntt_fwd(x, lds, a.tw_fwd, l, Q);
-        mac_index<METHOD, FIRST>(x, i, a, rout, rk1, rk2, rks, rpp, c, cneg, l);
+#pragma unroll
+        for (int r = 0; r < kRegs; ++r) x[r] = canon4(x[r], Q);
+        mac_index<METHOD, FIRST>(x, i, a, w, rk1, rk2, rks, rpp, c, cneg, l);
+    }
+    const uint32_t ioff = a.index * polyB;
+#pragma unroll
+    for (int gq = 0; gq < 8; ++gq) {
+        u32x4 t = bload4(rout, vo, ioff + gq * 1024u);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) t[e] = reduce58(w[4 * gq + e] + t[e], m);
+        bstore4(t, rout, vo, ioff + gq * 1024u);
     }
 }
 
@@ -315,7 +346,7 @@ __global__ __launch_bounds__(kThreads) void ntt_fwd_kernel(const uint32_t* __res
     ntt_fwd(x, smem + wv * kLdsWords, twf, l, Q);
     uint32_t* dst = out + (size_t)p * kN;
 #pragma unroll
-    for (int r = 0; r < kRegs; ++r) dst[jC(l, r)] = x[r];
+    for (int r = 0; r < kRegs; ++r) dst[jC(l, r)] = canon4(x[r], Q);
 }
 
 __global__ __launch_bounds__(kThreads) void ntt_inv_kernel(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
