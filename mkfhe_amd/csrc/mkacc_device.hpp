@@ -179,33 +179,32 @@ __device__ __forceinline__ const uint2* opaque(const uint2* p) {
     return (const uint2*)v;
 }
 
-// NP consecutive (w, w') pairs of a per-lane twiddle run starting at p:
-// dwordx4 loads off one 64-bit base with immediate offsets.
-template <int NP>
-__device__ __forceinline__ void load_pairs(uint2 (&w)[NP], const uint2* p) {
-    if (NP == 1) {
-        w[0] = p[0];
-    } else {
-        const uint4* q = reinterpret_cast<const uint4*>(p);
-#pragma unroll
-        for (int j = 0; j < NP / 2; ++j) {
-            const uint4 t = q[j];
-            w[2 * j] = make_uint2(t.x, t.y);
-            w[2 * j + 1] = make_uint2(t.z, t.w);
-        }
-    }
-}
+// ---- per-lane twiddles, staged in LDS ------------------------------------------
+// Pass B (stages 5..9) and pass C (stage 10) need per-lane twiddles.  They are
+// copied once per workgroup into LDS in an interleaved order so that a wave's
+// read of "twiddle m" is one conflict-free ds_read_b64 at a lane-dependent
+// base plus an immediate offset:
+//   stage s in 5..9 : pair (m, lhi) at  twl_off(s) + 32*m + lhi   (lhi = lane >> 1)
+//   stage 10        : pair (m, lane) at kTwlC + 64*m + lane
+// Entry (m, lhi) of stage s is reference table index 2^s + lhi*2^(s-5) + m, and
+// entry (m, lane) of stage 10 is 1024 + 16*lane + m (transformnat-impl.h:705-760);
+// the inverse NTT's bit-B stage uses the layout of stage s = 10 - B.
+__host__ __device__ constexpr int twl_off(int s) { return 32 * ((1 << (s - 5)) - 1); }
+constexpr int kTwlC = 992;                 // = twl_off(10)
+constexpr int kTwlPairs = kTwlC + 1024;    // 2016 pairs per direction
 
-// forward pass-B stage s (5..9) on bit 10-s: twiddle 2^s + (lhi << (s-5)) + (r >> (10-s))
+// forward pass-B stage s (5..9) on bit 10-s
 template <int S>
-__device__ __forceinline__ void fwd_stage_b(uint32_t (&x)[kRegs], const uint2* tw, uint32_t lhi, uint32_t Q) {
+__device__ __forceinline__ void fwd_stage_b(uint32_t (&x)[kRegs], const uint2* twl, uint32_t lhi, uint32_t Q) {
     // twiddle runs longer than 8 pairs are processed in chunks of 8 to cap the
     // live twiddle registers at 16
     constexpr int NP = 1 << (S - 5), H = 1 << (9 - S), CH = NP > 8 ? 8 : NP, SH = 10 - S;
+    const uint2* t = twl + twl_off(S) + lhi;
 #pragma unroll
     for (int c0 = 0; c0 < NP; c0 += CH) {
         uint2 w[CH];
-        load_pairs<CH>(w, tw + (1u << S) + (lhi << (S - 5)) + c0);
+#pragma unroll
+        for (int j = 0; j < CH; ++j) w[j] = t[32 * (c0 + j)];
 #pragma unroll
         for (int r = 0; r < kRegs; ++r) {
             if (r & H) continue;
@@ -216,14 +215,16 @@ __device__ __forceinline__ void fwd_stage_b(uint32_t (&x)[kRegs], const uint2* t
         sched_fence();
     }
 }
-// inverse pass-B stage on bit B (1..5): twiddle 2^(10-B) + (lhi << (5-B)) + (r >> B)
+// inverse pass-B stage on bit B (1..5)
 template <int B>
-__device__ __forceinline__ void inv_stage_b(uint32_t (&x)[kRegs], const uint2* twi, uint32_t lhi, uint32_t Q) {
+__device__ __forceinline__ void inv_stage_b(uint32_t (&x)[kRegs], const uint2* twl, uint32_t lhi, uint32_t Q) {
     constexpr int NP = 1 << (5 - B), H = 1 << (B - 1), CH = NP > 8 ? 8 : NP;
+    const uint2* t = twl + twl_off(10 - B) + lhi;
 #pragma unroll
     for (int c0 = 0; c0 < NP; c0 += CH) {
         uint2 w[CH];
-        load_pairs<CH>(w, twi + (1u << (10 - B)) + (lhi << (5 - B)) + c0);
+#pragma unroll
+        for (int j = 0; j < CH; ++j) w[j] = t[32 * (c0 + j)];
 #pragma unroll
         for (int r = 0; r < kRegs; ++r) {
             if (r & H) continue;
@@ -235,12 +236,15 @@ __device__ __forceinline__ void inv_stage_b(uint32_t (&x)[kRegs], const uint2* t
     }
 }
 
+// Forward negacyclic NTT of one polynomial per wave, reference EVAL order.
+//   tw_g : reference forward table (pairs) in global memory, pass A reads it
+//          with scalar loads (wave-uniform indices 1..31)
+//   twl  : this direction's per-lane LDS table (layout above)
 // Input residues in [0, 4Q); output EVAL values in [0, 4Q) (not canonical).
-__device__ __forceinline__ void ntt_fwd(uint32_t (&x)[kRegs], uint32_t* lds, const uint2* tw_in,
+__device__ __forceinline__ void ntt_fwd(uint32_t (&x)[kRegs], uint32_t* lds, const uint2* tw_g, const uint2* twl,
                                         uint32_t l, uint32_t Q) {
-    const uint2* tw = opaque(tw_in);
     // pass A: stages 0..4 (bits 10..6); twiddle index uniform across the wave
-    const ConstTable twc{(const_u64*)tw};
+    const ConstTable twc{(const_u64*)opaque(tw_g)};
 #pragma unroll
     for (int s = 0; s < 5; ++s) {
         const int h = 16 >> s;
@@ -256,17 +260,19 @@ __device__ __forceinline__ void ntt_fwd(uint32_t (&x)[kRegs], uint32_t* lds, con
     // pass B: stages 5..9 (bits 5..1)
     const uint32_t lo = opaque_v(l);
     const uint32_t lhi = lo >> 1;
-    fwd_stage_b<5>(x, tw, lhi, Q);
-    fwd_stage_b<6>(x, tw, lhi, Q);
-    fwd_stage_b<7>(x, tw, lhi, Q);
-    fwd_stage_b<8>(x, tw, lhi, Q);
-    fwd_stage_b<9>(x, tw, lhi, Q);
+    fwd_stage_b<5>(x, twl, lhi, Q);
+    fwd_stage_b<6>(x, twl, lhi, Q);
+    fwd_stage_b<7>(x, twl, lhi, Q);
+    fwd_stage_b<8>(x, twl, lhi, Q);
+    fwd_stage_b<9>(x, twl, lhi, Q);
     transpose<1, 2>(x, lds, l);
-    // pass C: stage 10 (bit 0): index 1024 + (l << 4) + r/2, in two halves
+    // pass C: stage 10 (bit 0), in two halves of 8 twiddles
+    const uint2* tc = twl + kTwlC + lo;
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
         uint2 w[8];
-        load_pairs<8>(w, tw + 1024u + (lo << 4) + 8u * hf);
+#pragma unroll
+        for (int m = 0; m < 8; ++m) w[m] = tc[64 * (8 * hf + m)];
 #pragma unroll
         for (int m = 0; m < 8; ++m) ct_bfly(x[16 * hf + 2 * m], x[16 * hf + 2 * m + 1], w[m], Q);
         sched_fence();
@@ -274,17 +280,18 @@ __device__ __forceinline__ void ntt_fwd(uint32_t (&x)[kRegs], uint32_t* lds, con
 }
 
 // ---- inverse NTT WITHOUT the N^-1 factor (Gentleman-Sande) -------------------
-// twi[i] = { psi^-brv(i), companion }: reference rootOfUnityInverseTable.
+// Reference inverse table (psi^-brv(i)); same split as the forward transform.
 // Input residues in [0, 2Q); output canonical coefficients in [0, Q).
-__device__ __forceinline__ void ntt_inv_noscale(uint32_t (&x)[kRegs], uint32_t* lds, const uint2* twi_in,
-                                                uint32_t l, uint32_t Q) {
-    const uint2* twi = opaque(twi_in);
+__device__ __forceinline__ void ntt_inv_noscale(uint32_t (&x)[kRegs], uint32_t* lds, const uint2* twi_g,
+                                                const uint2* twl, uint32_t l, uint32_t Q) {
     const uint32_t lo = opaque_v(l);
     // pass C: bit 0
+    const uint2* tc = twl + kTwlC + lo;
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
         uint2 w[8];
-        load_pairs<8>(w, twi + 1024u + (lo << 4) + 8u * hf);
+#pragma unroll
+        for (int m = 0; m < 8; ++m) w[m] = tc[64 * (8 * hf + m)];
 #pragma unroll
         for (int m = 0; m < 8; ++m) gs_bfly(x[16 * hf + 2 * m], x[16 * hf + 2 * m + 1], w[m], Q);
         sched_fence();
@@ -292,14 +299,14 @@ __device__ __forceinline__ void ntt_inv_noscale(uint32_t (&x)[kRegs], uint32_t* 
     transpose<2, 1>(x, lds, l);
     // pass B: bits 1..5
     const uint32_t lhi = lo >> 1;
-    inv_stage_b<1>(x, twi, lhi, Q);
-    inv_stage_b<2>(x, twi, lhi, Q);
-    inv_stage_b<3>(x, twi, lhi, Q);
-    inv_stage_b<4>(x, twi, lhi, Q);
-    inv_stage_b<5>(x, twi, lhi, Q);
+    inv_stage_b<1>(x, twl, lhi, Q);
+    inv_stage_b<2>(x, twl, lhi, Q);
+    inv_stage_b<3>(x, twl, lhi, Q);
+    inv_stage_b<4>(x, twl, lhi, Q);
+    inv_stage_b<5>(x, twl, lhi, Q);
     transpose<1, 0>(x, lds, l);
     // pass A: bits 6..10 ; uniform twiddles
-    const ConstTable twc{(const_u64*)twi};
+    const ConstTable twc{(const_u64*)opaque(twi_g)};
 #pragma unroll
     for (int b = 6; b <= 10; ++b) {
         const int h = 1 << (b - 6);
@@ -337,58 +344,60 @@ __host__ __device__ __forceinline__ uint32_t c4_index(uint32_t j) {
     return ((r >> 2) << 8) | (l << 2) | (r & 3u);
 }
 
-// ---- signed digit decomposition helpers (mk-acc.cpp:54-80) ------------------
-// sext of the low gbits bits: (d << (W-gBits)) >> (W-gBits)
-__device__ __forceinline__ int32_t sext_low(int32_t d, uint32_t gbits) {
-    return __builtin_amdgcn_sbfe(d, 0, gbits);
+// ---- signed digit decomposition (mk-acc.cpp:54-80) -----------------------------
+// The reference centres t (d = t < Q/2 ? t : t - Q), then repeatedly takes the
+// balanced low digit r = sext_b(d), d = (d - r) >> b; digit 0 is dropped and
+// digits 1..dg are emitted as r < 0 ? r + Q : r.
+//
+// Equivalent closed form used on the GPU: with C = sum_{i<G} 2^(b-1) 2^(b*i)
+// (G = digitsG) and D = d + C (0 <= D < 2^32 when b*G <= 32), every balanced
+// digit is r_i = bfe(D, b*i, b) - 2^(b-1).  By induction on i: D >> (b*i) equals
+// the reference's running d_i plus sum_{j=i}^{G-1} 2^(b-1) 2^(b(j-i)), whose
+// residue mod 2^b is d_i + 2^(b-1) = r_i + 2^(b-1) (in [0, 2^b)).
+// The NTT consumes r_i + Q (in [Q - 2^(b-1), Q + 2^(b-1)) subset [0, 2Q)), the
+// same residue class as the reference digit; the canonical form is r_i + Q mod Q.
+struct SddConsts {
+    uint32_t qhalf;    // Q >> 1
+    uint32_t cpos;     // C          (added when t <  Q/2)
+    uint32_t cneg;     // C - Q      (added when t >= Q/2), mod 2^32
+    uint32_t gbits;    // b
+    uint32_t qm;       // Q - 2^(b-1)
+};
+__device__ __forceinline__ uint32_t sdd_offset(uint32_t t, const SddConsts& s) {
+    return t + (t < s.qhalf ? s.cpos : s.cneg);
 }
-// centred value with the lowest digit already dropped
-__device__ __forceinline__ int32_t sdd_start(uint32_t t, uint32_t Q, uint32_t qhalf, uint32_t gbits) {
-    int32_t d = t < qhalf ? (int32_t)t : (int32_t)t - (int32_t)Q;
-    int32_t r = sext_low(d, gbits);
-    return (d - r) >> gbits;
-}
-// next digit as a residue; advances the running value
-__device__ __forceinline__ uint32_t sdd_next(int32_t& d, uint32_t Q, uint32_t gbits) {
-    int32_t r = sext_low(d, gbits);
-    d = (d - r) >> gbits;
-    return r < 0 ? (uint32_t)(r + (int32_t)Q) : (uint32_t)r;
+// digit i (1..dg) of offset word D as an NTT input in [0, 2Q)
+__device__ __forceinline__ uint32_t sdd_digit(uint32_t D, uint32_t i, const SddConsts& s) {
+    return __builtin_amdgcn_ubfe(D, i * s.gbits, s.gbits) + s.qm;
 }
 
-// Digits 1..DG-1 of every element packed as signed bitfields: two elements per
-// register when DG <= 3 (16-bit slots), one otherwise.  Digit 0 goes straight
-// into the NTT, so only the rest is kept -- 16 VGPRs instead of a 32-VGPR
-// running remainder for the common parameter sets.
+// Digits 2..DG of every element, kept between the digit NTTs.  DG <= 3: the
+// (DG-1)*b <= 16 bits of digits 2..DG of two elements share one register
+// (b = 9 at DG = 2, b <= 8 at DG = 3); otherwise the offset word D is kept.
 template <int DG>
 struct PackedDigits {
-    static constexpr int kPer = DG <= 3 ? 2 : 1;           // elements per register
-    static constexpr int kSlot = 32 / kPer;                // bits per element
-    static constexpr int kField = kSlot / (DG - 1 > 0 ? DG - 1 : 1);
-    static constexpr int kWords = kRegs / kPer;
+    static constexpr bool kPack = DG <= 3;
+    static constexpr int kWords = kPack ? kRegs / 2 : kRegs;
     uint32_t w[kWords];
 
-    // decompose coefficient t: returns digit 0 (as residue), stores 1..DG-1
-    __device__ __forceinline__ uint32_t put(int r, uint32_t t, uint32_t Q, uint32_t qhalf, uint32_t gbits) {
-        int32_t d = sdd_start(t, Q, qhalf, gbits);
-        const uint32_t g0 = sdd_next(d, Q, gbits);
-        uint32_t acc = 0;
-#pragma unroll
-        for (int i = 1; i < DG; ++i) {
-            const int32_t rr = sext_low(d, gbits);
-            d = (d - rr) >> gbits;
-            acc |= ((uint32_t)rr & ((1u << kField) - 1u)) << ((i - 1) * kField);
+    // element r with offset word D: returns digit 1 (NTT input), stores the rest
+    __device__ __forceinline__ uint32_t put(int r, uint32_t D, const SddConsts& s) {
+        if (kPack) {
+            const uint32_t f = __builtin_amdgcn_ubfe(D, 2u * s.gbits, 16u);   // digits 2..DG (bits above G*b are 0 here)
+            if ((r & 1) == 0) w[r >> 1] = f;
+            else w[r >> 1] |= f << 16;
+            // pin the packed word: otherwise the compiler sinks the packing to
+            // the later unpack and keeps every D live across the NTTs
+            if (r & 1) asm volatile("" : "+v"(w[r >> 1]));
+        } else {
+            w[r] = D;
         }
-        if (kPer == 1 || (r % kPer) == 0) w[r / kPer] = acc;
-        else w[r / kPer] |= acc << kSlot;
-        // pin the packed word here: otherwise the compiler sinks the packing to
-        // the later unpack and keeps every unpacked digit live across the NTTs
-        if ((r % kPer) == kPer - 1) asm volatile("" : "+v"(w[r / kPer]));
-        return g0;
+        return sdd_digit(D, 1, s);
     }
-    // digit i (1..DG-1) of element r as a residue
-    __device__ __forceinline__ uint32_t get(int r, int i, uint32_t Q) const {
-        const int32_t rr = __builtin_amdgcn_sbfe((int32_t)w[r / kPer], (r % kPer) * kSlot + (i - 1) * kField, kField);
-        return rr < 0 ? (uint32_t)(rr + (int32_t)Q) : (uint32_t)rr;
+    // digit i (2..DG) of element r as an NTT input
+    __device__ __forceinline__ uint32_t get(int r, int i, const SddConsts& s) const {
+        if (kPack) return __builtin_amdgcn_ubfe(w[r >> 1], (r & 1) * 16u + (uint32_t)(i - 2) * s.gbits, s.gbits) + s.qm;
+        return sdd_digit(w[r], (uint32_t)i, s);
     }
 };
 

@@ -46,8 +46,25 @@ int fail(int code, const std::string& msg) {
             return fail(MKACC_E_DEVICE, std::string(#expr) + ": " + hipGetErrorString(_e));    \
     } while (0)
 
-constexpr int kWavesPerBlock = 4;
+constexpr int kWavesPerBlock = 8;                 // one 512-thread workgroup per CU (2 waves / SIMD)
 constexpr int kThreads = 64 * kWavesPerBlock;
+
+// LDS image shared by a workgroup (built once per context, copied in at kernel start):
+//   [0, kTwlPairs)                forward per-lane twiddles (mkacc_device.hpp layout)
+//   [kTwlPairs, 2 kTwlPairs)      inverse per-lane twiddles
+//   [2 kTwlPairs, + 2N)           psi^e (e in [0, 2N)) with Shoup companion, at psi_pos(e)
+// followed by one transpose scratch of kLdsWords per wave.
+constexpr int kPsiPairs = 2 * kN;
+constexpr int kImgPairs = 2 * kTwlPairs + kPsiPairs;
+constexpr int kImgWords = 2 * kImgPairs;
+constexpr size_t kStepLdsBytes = (size_t)(kImgWords + kWavesPerBlock * kLdsWords) * 4;
+static_assert(kImgWords % 4 == 0, "LDS image is copied with dwordx4");
+static_assert(kStepLdsBytes <= 160 * 1024, "LDS budget");
+
+// Bank-spreading position of psi^e in the LDS table: the exponents a wave
+// gathers (c * (2 brv(j) + 1) mod 2N) repeat in their low 5 bits across lanes;
+// xor-ing in the next 5 bits gives ~2.6-way instead of ~10-way conflicts.
+__host__ __device__ __forceinline__ uint32_t psi_pos(uint32_t e) { return e ^ ((e >> 5) & 31u); }
 
 enum { XZW = 0, XZW_B = 1 };
 
@@ -59,137 +76,198 @@ struct StepArgs {
     const uint32_t* key2;      // ev2 = (*ek)[u][1][i] (XZW)
     const uint32_t* keys;      // evs = (*ek)[0][0][n] (first step)
     const uint32_t* pkey;      // [k][dg][N]
-    uint32_t* sumv;            // [B][N] scratch: sumV of HbProd
-    const uint2* tw_fwd;       // [N]
+    const uint32_t* img;       // LDS image [kImgWords]
+    const uint2* tw_fwd;       // [N] reference forward table (pass A, scalar reads)
     const uint2* tw_inv;       // [N]
-    const uint2* psi_pow;      // [2N] psi^e with Shoup companion
     uint32_t B, k, index;
     Mod m;
-    uint32_t qhalf, gbits;
+    SddConsts sd;
 };
 
-// EVAL exponent base of slot j = (lane << 5) | r: the reference stores
-// a(psi^(2*brv(j)+1)) at position j (transformnat-impl.h:705-760).
-__device__ __forceinline__ uint32_t slot_odd(uint32_t l, uint32_t r) {
-    uint32_t j = (l << 5) | r;
-    return ((__brev(j) >> 21) << 1) | 1u;
+// Copy the LDS image (twiddles + psi table) into this workgroup's LDS.
+__device__ __forceinline__ void load_image(uint32_t* smem, const uint32_t* img) {
+    const uint4* src = reinterpret_cast<const uint4*>(img);
+    uint4* dst = reinterpret_cast<uint4*>(smem);
+    for (int i = threadIdx.x; i < kImgWords / 4; i += blockDim.x) dst[i] = src[i];
+    __syncthreads();
 }
 
-// One accumulator step for one gate per wavefront.
-//   FIRST:  AddToAccXZW0 (mk-acc-xzw.cpp:347-381 / xzw_B.cpp:333-381): acc <- HbProd(acc)
-//   else:   AddToAccXZW  (mk-acc-xzw.cpp:292-345 / xzw_B.cpp:281-330):
-//           acc <- acc + HbProd(acc * (X^c - 1))
-// HbProd is mk-acc-xzw.cpp:231-290.  All sums are exact mod Q, so the
-// reordering below (d/f formed per slot, sums reduced lazily) is bit-exact.
-
-// monomial value X^e at this lane's slot r (EVAL) with its Shoup companion
-__device__ __forceinline__ uint2 mono_at(__amdgpu_buffer_rsrc_t pp, uint32_t c, uint32_t l, int r) {
-    const uint32_t e = __umul24(c, slot_odd(l, (uint32_t)r)) & (2u * kN - 1u);
-    const u32x2 t = bload2(pp, e * 8u, 0);
-    return make_uint2(t.x, t.y);
+struct Tables {
+    const uint2* twf;   // LDS
+    const uint2* twi;   // LDS
+    const uint2* psi;   // LDS
+};
+__device__ __forceinline__ Tables tables(uint32_t* smem) {
+    const uint2* b = reinterpret_cast<const uint2*>(smem);
+    return Tables{b, b + kTwlPairs, b + 2 * kTwlPairs};
 }
 
-// effective key word d_i / f_i of mk-acc-xzw(_B).cpp AddToAccXZW{,0}
+// Monomial X^e at EVAL slot j = (lane << 5) | r: the reference stores
+// a(psi^(2 brv(j) + 1)) at position j (transformnat-impl.h:705-760), so
+// X^c -> psi^(c (2 brv(j) + 1)), with 2 brv(j) + 1 = 128 brv5(r) + (2 brv6(lane) + 1).
+// `co` = c * (2 brv6(lane) + 1) per lane; the r part is wave-uniform.
+struct Mono {
+    uint32_t co;        // per-lane c * (2 brv6(l) + 1)
+    uint32_t c;         // wave-uniform exponent
+    __device__ __forceinline__ uint2 at(const uint2* psi, int r) const {
+        constexpr uint32_t kBr5[32] = {0, 16, 8, 24, 4, 20, 12, 28, 2, 18, 10, 26, 6, 22, 14, 30,
+                                       1, 17, 9, 25, 5, 21, 13, 29, 3, 19, 11, 27, 7, 23, 15, 31};
+        // opaque: keeps the 32 per-slot exponents from being hoisted out of the
+        // party / digit loops (they would stay live in VGPRs across the NTTs)
+        const uint32_t e = (opaque_v(co) + c * (128u * kBr5[r])) & (2u * kN - 1u);
+        return psi[psi_pos(e)];
+    }
+};
+__device__ __forceinline__ Mono make_mono(uint32_t c, uint32_t l) {
+    const uint32_t o = ((__brev(l) >> 26) << 1) | 1u;   // 2 brv6(l) + 1
+    return Mono{(uint32_t)__umul24(c, o), c};
+}
+
+// Lazy Shoup product x*w in [0, 2Q) (x < 2^32)
+__device__ __forceinline__ uint32_t mul_shoup_lazy(uint32_t x, uint2 w, uint32_t Q) {
+    return x * w.x - __umulhi(x, w.y) * Q;
+}
+
+// effective key word d_i / f_i of mk-acc-xzw(_B).cpp AddToAccXZW{,0}, canonical
 template <int METHOD, bool FIRST>
-__device__ __forceinline__ uint32_t key_eff(uint32_t k1, uint32_t k2, uint32_t ks, __amdgpu_buffer_rsrc_t pp,
-                                            uint32_t c, uint32_t cneg, uint32_t l, int r, uint32_t Q) {
+__device__ __forceinline__ uint32_t key_eff(uint32_t k1, uint32_t k2, uint32_t ks, const uint2* psi,
+                                            const Mono& mp, const Mono& mn, int r, uint32_t Q) {
     if (METHOD == XZW) {
-        const uint2 tn = mono_at(pp, cneg, l, r);
+        const uint2 tn = mn.at(psi, r);
         if (FIRST) {
             // evs + ev1*(X^c-1) + ev2*(X^-c-1)          (xzw.cpp:375-378)
-            const uint2 tp = mono_at(pp, c, l, r);
+            const uint2 tp = mp.at(psi, r);
             const uint32_t t1 = sub_mod(mul_shoup(k1, tp.x, tp.y, Q), k1, Q);
             const uint32_t t2 = sub_mod(mul_shoup(k2, tn.x, tn.y, Q), k2, Q);
             return add_mod(add_mod(ks, t1, Q), t2, Q);
         }
         // ev1 - ev2*(X^-c - 1) - ev2  ==  ev1 - ev2*X^-c   (xzw.cpp:322-325)
-        return sub_mod(k1, mul_shoup(k2, tn.x, tn.y, Q), Q);
+        uint32_t d = k1 + 2u * Q - mul_shoup_lazy(k2, tn, Q);    // (0, 3Q)
+        d = min(d, d - 2u * Q);                                  // [0, 2Q)
+        return min(d, d - Q);
     } else {
         if (FIRST) {
             // evs + ev1*(X^c-1)                            (xzw_B.cpp:368-371)
-            const uint2 tp = mono_at(pp, c, l, r);
+            const uint2 tp = mp.at(psi, r);
             return add_mod(ks, sub_mod(mul_shoup(k1, tp.x, tp.y, Q), k1, Q), Q);
         }
         return k1;                                        // (xzw_B.cpp:311-314)
     }
 }
 
-// Register-resident HbProd (mk-acc-xzw.cpp:231-290) for one gate per wave.
-// The per-slot sums uj_u = sum_i g_i d_i, sumV = sum_u sum_i g_i P[u][i] and
-// w = sum_i h_i f_i are kept as lazy 64-bit accumulators (v_mad_u64_u32) and
-// reduced once; every operand is canonical, so a sum of up to 16 products
-// stays below 2^58 (reduce58).
+// Bounds of the lazy 64-bit sums (reduce58 needs < 2^58): digit NTT outputs are
+// left in [0, 4Q) when DG <= 3 (sum of DG products < 3 * 4Q^2 < 2^58) and
+// brought to [0, 2Q) otherwise (5 * 2Q^2 < 2^58); keys are canonical.
+template <int DG>
+__device__ __forceinline__ void digit_range(uint32_t (&x)[kRegs], uint32_t Q) {
+    if (DG > 3) {
+#pragma unroll
+        for (int r = 0; r < kRegs; ++r) x[r] = min(x[r], x[r] - 2u * Q);
+    }
+}
+
+// Key words of one 4-register group of a MAC: software-pipelined kPrefetch
+// groups ahead so the L2 latency of the step's key block overlaps the arithmetic.
+constexpr int kPrefetch = 1;
+struct KeyGroup {
+    u32x4 k1, k2, ks, pk;
+};
+
+// uj_u += g * d_i ; sv += g * P[u][i]          (xzw.cpp:263-269)
 template <int DG, int METHOD, bool FIRST>
-__device__ __forceinline__ void mac_digit(const uint32_t (&g)[kRegs], int i, uint32_t u, const StepArgs& a,
-                                          uint64_t (&uj)[kRegs], uint64_t (&sv)[kRegs],
-                                          __amdgpu_buffer_rsrc_t rk1, __amdgpu_buffer_rsrc_t rk2,
-                                          __amdgpu_buffer_rsrc_t rks, __amdgpu_buffer_rsrc_t rpk,
-                                          __amdgpu_buffer_rsrc_t rpp, uint32_t c, uint32_t cneg, uint32_t l) {
-    const uint32_t Q = a.m.Q;
-    const uint32_t polyB = kN * 4u, vo = l * 16u;
+__device__ __forceinline__ void mac_digit(const uint32_t (&g)[kRegs], int i, uint32_t u, uint64_t (&uj)[kRegs],
+                                          uint64_t (&sv)[kRegs], __amdgpu_buffer_rsrc_t rk1,
+                                          __amdgpu_buffer_rsrc_t rk2, __amdgpu_buffer_rsrc_t rks,
+                                          __amdgpu_buffer_rsrc_t rpk, const uint2* psi, const Mono& mp,
+                                          const Mono& mn, uint32_t vo, uint32_t Q) {
+    const uint32_t polyB = kN * 4u;
     const uint32_t koff = (uint32_t)(2 * i) * polyB;
     const uint32_t poff = (u * DG + (uint32_t)i) * polyB;
+    KeyGroup kg[kPrefetch + 1];
+    auto issue = [&](KeyGroup& t, int gq) {
+        const uint32_t go = gq * 1024u;
+        t.k1 = bload4(rk1, vo, koff + go);
+        t.pk = bload4(rpk, vo, poff + go);
+        if (METHOD == XZW) t.k2 = bload4(rk2, vo, koff + go);
+        if (FIRST) t.ks = bload4(rks, vo, koff + go);
+    };
+#pragma unroll
+    for (int j = 0; j < kPrefetch; ++j) issue(kg[j], j);
 #pragma unroll
     for (int gq = 0; gq < 8; ++gq) {
-        const uint32_t go = gq * 1024u;
-        const uint32_t lq = opaque_v(l);   // keep slot exponents from being hoisted (VGPR pressure)
-        const u32x4 k1 = bload4(rk1, vo, koff + go);
-        const u32x4 pk = bload4(rpk, vo, poff + go);
-        u32x4 k2 = {0, 0, 0, 0}, ks = {0, 0, 0, 0};
-        if (METHOD == XZW) k2 = bload4(rk2, vo, koff + go);
-        if (FIRST) ks = bload4(rks, vo, koff + go);
+        if (gq + kPrefetch < 8) issue(kg[(gq + kPrefetch) % (kPrefetch + 1)], gq + kPrefetch);
+        const KeyGroup& t = kg[gq % (kPrefetch + 1)];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const int r = 4 * gq + e;
-            const uint32_t deff = key_eff<METHOD, FIRST>(k1[e], k2[e], ks[e], rpp, c, cneg, lq, r, Q);
+            const uint32_t deff = key_eff<METHOD, FIRST>(t.k1[e], t.k2[e], t.ks[e], psi, mp, mn, r, Q);
             uj[r] = mad64(g[r], deff, uj[r]);
-            sv[r] = mad64(g[r], pk[e], sv[r]);
+            sv[r] = mad64(g[r], t.pk[e], sv[r]);
         }
         sched_fence();
     }
 }
 
+// w += h * f_i                                  (xzw.cpp:281-288)
 template <int METHOD, bool FIRST>
-__device__ __forceinline__ void mac_index(const uint32_t (&h)[kRegs], int i, const StepArgs& a, uint64_t (&w)[kRegs],
+__device__ __forceinline__ void mac_index(const uint32_t (&h)[kRegs], int i, uint64_t (&w)[kRegs],
                                           __amdgpu_buffer_rsrc_t rk1, __amdgpu_buffer_rsrc_t rk2,
-                                          __amdgpu_buffer_rsrc_t rks, __amdgpu_buffer_rsrc_t rpp, uint32_t c,
-                                          uint32_t cneg, uint32_t l) {
-    const uint32_t Q = a.m.Q;
-    const uint32_t polyB = kN * 4u, vo = l * 16u;
+                                          __amdgpu_buffer_rsrc_t rks, const uint2* psi, const Mono& mp,
+                                          const Mono& mn, uint32_t vo, uint32_t Q) {
+    const uint32_t polyB = kN * 4u;
     const uint32_t koff = (uint32_t)(2 * i + 1) * polyB;
+    KeyGroup kg[kPrefetch + 1];
+    auto issue = [&](KeyGroup& t, int gq) {
+        const uint32_t go = gq * 1024u;
+        t.k1 = bload4(rk1, vo, koff + go);
+        if (METHOD == XZW) t.k2 = bload4(rk2, vo, koff + go);
+        if (FIRST) t.ks = bload4(rks, vo, koff + go);
+    };
+#pragma unroll
+    for (int j = 0; j < kPrefetch; ++j) issue(kg[j], j);
 #pragma unroll
     for (int gq = 0; gq < 8; ++gq) {
-        const uint32_t go = gq * 1024u;
-        const uint32_t lq = opaque_v(l);
-        const u32x4 k1 = bload4(rk1, vo, koff + go);
-        u32x4 k2 = {0, 0, 0, 0}, ks = {0, 0, 0, 0};
-        if (METHOD == XZW) k2 = bload4(rk2, vo, koff + go);
-        if (FIRST) ks = bload4(rks, vo, koff + go);
+        if (gq + kPrefetch < 8) issue(kg[(gq + kPrefetch) % (kPrefetch + 1)], gq + kPrefetch);
+        const KeyGroup& t = kg[gq % (kPrefetch + 1)];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const int r = 4 * gq + e;
-            const uint32_t feff = key_eff<METHOD, FIRST>(k1[e], k2[e], ks[e], rpp, c, cneg, lq, r, Q);
+            const uint32_t feff = key_eff<METHOD, FIRST>(t.k1[e], t.k2[e], t.ks[e], psi, mp, mn, r, Q);
             w[r] = mad64(h[r], feff, w[r]);
         }
         sched_fence();
     }
 }
 
+// One accumulator step for one gate per wavefront.
+//   FIRST:  AddToAccXZW0 (mk-acc-xzw.cpp:347-381 / xzw_B.cpp:333-381): acc <- HbProd(acc)
+//   else:   AddToAccXZW  (mk-acc-xzw.cpp:292-345 / xzw_B.cpp:281-330):
+//           acc <- acc + HbProd(acc * (X^c - 1))
+// HbProd is mk-acc-xzw.cpp:231-290, register resident: the per-slot sums
+// uj_u = sum_i g_i d_i, sumV = sum_u sum_i g_i P[u][i] and w = sum_i h_i f_i are
+// lazy 64-bit accumulators (v_mad_u64_u32) reduced once; all sums are exact
+// mod Q, so the reordering is bit-exact.
 template <int DG, int METHOD, bool FIRST>
 __global__ __launch_bounds__(kThreads, 2) void mk_step_kernel(StepArgs a) {
     // register allocation fits without spills when the digit loop is unrolled
     // for DG = 2 and kept rolled for DG >= 3 (measured, hipcc ROCm 7.2)
     constexpr int kDigitUnroll = DG == 2 ? 2 : 1;
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    load_image(smem, a.img);
+    const Tables tb = tables(smem);
     const uint32_t l = threadIdx.x & 63u;
-    const uint32_t wv = threadIdx.x >> 6;
+    // wave-uniform (SGPR) gate index: the per-gate buffer descriptors must be
+    // scalar, otherwise every load through them becomes a waterfall loop
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t gate = blockIdx.x * kWavesPerBlock + wv;
     if (gate >= a.B) return;
-    uint32_t* lds = smem + wv * kLdsWords;
+    uint32_t* lds = smem + kImgWords + wv * kLdsWords;
     const Mod m = a.m;
     const uint32_t Q = m.Q;
+    const SddConsts sd = a.sd;
     const uint32_t c = __builtin_amdgcn_readfirstlane(a.cvals[gate]);
     const uint32_t cneg = (2u * kN - c) & (2u * kN - 1u);
+    const Mono mp = make_mono(c, l), mn = make_mono(cneg, l);
     const uint32_t k = a.k;
     const uint32_t polyB = kN * 4u;
     const uint32_t vo = l * 16u;   // lane offset of a C4 dwordx4
@@ -200,7 +278,6 @@ __global__ __launch_bounds__(kThreads, 2) void mk_step_kernel(StepArgs a) {
     const __amdgpu_buffer_rsrc_t rk2 = make_rsrc(a.key2, DG * 2 * polyB);
     const __amdgpu_buffer_rsrc_t rks = make_rsrc(a.keys, DG * 2 * polyB);
     const __amdgpu_buffer_rsrc_t rpk = make_rsrc(a.pkey, k * DG * polyB);
-    const __amdgpu_buffer_rsrc_t rpp = make_rsrc(a.psi_pow, 2u * kN * 8u);
 
     uint64_t sv[kRegs];
 #pragma unroll
@@ -215,23 +292,23 @@ __global__ __launch_bounds__(kThreads, 2) void mk_step_kernel(StepArgs a) {
         }
         if (!FIRST) {
             // acctemp = acc * (X^c - 1)                     (xzw.cpp:336-338)
+            // x canonical -> x*X^c - x + Q in (0, 3Q) -> [0, 2Q)
 #pragma unroll
             for (int r0 = 0; r0 < kRegs; r0 += 8) {
-                const uint32_t lq = opaque_v(l);
 #pragma unroll
                 for (int r = r0; r < r0 + 8; ++r) {
-                    const uint2 t = mono_at(rpp, c, lq, r);
-                    x[r] = sub_mod(mul_shoup(x[r], t.x, t.y, Q), x[r], Q);
+                    const uint32_t y = mul_shoup_lazy(x[r], mp.at(tb.psi, r), Q) + Q - x[r];
+                    x[r] = min(y, y - 2u * Q);
                 }
                 sched_fence();
             }
         }
-        ntt_inv_noscale(x, lds, a.tw_inv, l, Q);
-        // SignedDigitDecompose (mk-acc.cpp:54-80): digit 0 -> x, digits 1.. packed
+        ntt_inv_noscale(x, lds, a.tw_inv, tb.twi, l, Q);
+        // SignedDigitDecompose (mk-acc.cpp:54-80): digit 1 -> x, digits 2.. packed
         PackedDigits<DG> pd;
 #pragma unroll
         for (int r = 0; r < kRegs; ++r) {
-            x[r] = pd.put(r, x[r], Q, a.qhalf, a.gbits);
+            x[r] = pd.put(r, sdd_offset(x[r], sd), sd);
             if ((r & 7) == 7) sched_fence();
         }
         uint64_t uj[kRegs];
@@ -241,12 +318,11 @@ __global__ __launch_bounds__(kThreads, 2) void mk_step_kernel(StepArgs a) {
         for (int i = 0; i < DG; ++i) {
             if (i > 0) {
 #pragma unroll
-                for (int r = 0; r < kRegs; ++r) x[r] = pd.get(r, i, Q);
+                for (int r = 0; r < kRegs; ++r) x[r] = pd.get(r, i + 1, sd);
             }
-            ntt_fwd(x, lds, a.tw_fwd, l, Q);
-#pragma unroll
-            for (int r = 0; r < kRegs; ++r) x[r] = canon4(x[r], Q);
-            mac_digit<DG, METHOD, FIRST>(x, i, u, a, uj, sv, rk1, rk2, rks, rpk, rpp, c, cneg, l);
+            ntt_fwd(x, lds, a.tw_fwd, tb.twf, l, Q);
+            digit_range<DG>(x, Q);
+            mac_digit<DG, METHOD, FIRST>(x, i, u, uj, sv, rk1, rk2, rks, rpk, tb.psi, mp, mn, vo, Q);
         }
         // acc_u <- (FIRST ? 0 : acc_u) + uj_u   (xzw.cpp:270, 342-344); sumV reduced per party
 #pragma unroll
@@ -267,11 +343,11 @@ __global__ __launch_bounds__(kThreads, 2) void mk_step_kernel(StepArgs a) {
     uint32_t x[kRegs];
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) x[r] = (uint32_t)sv[r];
-    ntt_inv_noscale(x, lds, a.tw_inv, l, Q);
+    ntt_inv_noscale(x, lds, a.tw_inv, tb.twi, l, Q);
     PackedDigits<DG> pd;
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) {
-        x[r] = pd.put(r, x[r], Q, a.qhalf, a.gbits);
+        x[r] = pd.put(r, sdd_offset(x[r], sd), sd);
         if ((r & 7) == 7) sched_fence();
     }
     uint64_t w[kRegs];
@@ -281,12 +357,11 @@ __global__ __launch_bounds__(kThreads, 2) void mk_step_kernel(StepArgs a) {
     for (int i = 0; i < DG; ++i) {
         if (i > 0) {
 #pragma unroll
-            for (int r = 0; r < kRegs; ++r) x[r] = pd.get(r, i, Q);
+            for (int r = 0; r < kRegs; ++r) x[r] = pd.get(r, i + 1, sd);
         }
-        ntt_fwd(x, lds, a.tw_fwd, l, Q);
-#pragma unroll
-        for (int r = 0; r < kRegs; ++r) x[r] = canon4(x[r], Q);
-        mac_index<METHOD, FIRST>(x, i, a, w, rk1, rk2, rks, rpp, c, cneg, l);
+        ntt_fwd(x, lds, a.tw_fwd, tb.twf, l, Q);
+        digit_range<DG>(x, Q);
+        mac_index<METHOD, FIRST>(x, i, w, rk1, rk2, rks, tb.psi, mp, mn, vo, Q);
     }
     const uint32_t ioff = a.index * polyB;
 #pragma unroll
@@ -334,45 +409,55 @@ __global__ void c4_to_eval_kernel(const uint32_t* __restrict__ in, uint32_t* __r
 // ---- primitive kernels (parity tests of the NTT / SDD building blocks) -------
 
 __global__ __launch_bounds__(kThreads) void ntt_fwd_kernel(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
-                                                            uint32_t count, const uint2* __restrict__ twf, uint32_t Q) {
+                                                            uint32_t count, const uint32_t* img, const uint2* twf,
+                                                            uint32_t Q) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    const uint32_t l = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    load_image(smem, img);
+    const Tables tb = tables(smem);
+    const uint32_t l = threadIdx.x & 63u, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t p = blockIdx.x * kWavesPerBlock + wv;
     if (p >= count) return;
     const uint32_t* src = in + (size_t)p * kN;
     uint32_t x[kRegs];
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) x[r] = src[jA(l, r)];
-    ntt_fwd(x, smem + wv * kLdsWords, twf, l, Q);
+    ntt_fwd(x, smem + kImgWords + wv * kLdsWords, twf, tb.twf, l, Q);
     uint32_t* dst = out + (size_t)p * kN;
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) dst[jC(l, r)] = canon4(x[r], Q);
 }
 
 __global__ __launch_bounds__(kThreads) void ntt_inv_kernel(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
-                                                            uint32_t count, const uint2* __restrict__ twi, uint32_t Q,
-                                                            uint32_t ninv, uint32_t ninvp) {
+                                                            uint32_t count, const uint32_t* img, const uint2* twi,
+                                                            uint32_t Q, uint32_t ninv, uint32_t ninvp) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    const uint32_t l = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    load_image(smem, img);
+    const Tables tb = tables(smem);
+    const uint32_t l = threadIdx.x & 63u, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t p = blockIdx.x * kWavesPerBlock + wv;
     if (p >= count) return;
     const uint32_t* src = in + (size_t)p * kN;
     uint32_t x[kRegs];
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) x[r] = src[jC(l, r)];
-    ntt_inv_noscale(x, smem + wv * kLdsWords, twi, l, Q);
+    ntt_inv_noscale(x, smem + kImgWords + wv * kLdsWords, twi, tb.twi, l, Q);
     uint32_t* dst = out + (size_t)p * kN;
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) dst[jA(l, r)] = mul_shoup(x[r], ninv, ninvp, Q);
 }
 
+// SignedDigitDecompose through the same offset-word digits the step kernel
+// feeds its NTTs, reduced to the reference's canonical residues.
 __global__ void sdd_kernel(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint32_t count, uint32_t dg,
-                           uint32_t Q, uint32_t qhalf, uint32_t gbits) {
+                           uint32_t Q, SddConsts sd) {
     const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= (size_t)count * kN) return;
     const size_t p = idx / kN, j = idx % kN;
-    int32_t d = sdd_start(in[idx], Q, qhalf, gbits);
-    for (uint32_t i = 0; i < dg; ++i) out[(p * dg + i) * kN + j] = sdd_next(d, Q, gbits);
+    const uint32_t D = sdd_offset(in[idx], sd);
+    for (uint32_t i = 0; i < dg; ++i) {
+        const uint32_t v = sdd_digit(D, i + 1, sd);
+        out[(p * dg + i) * kN + j] = v >= Q ? v - Q : v;
+    }
 }
 
 // ---- kernel table -------------------------------------------------------------
@@ -405,12 +490,12 @@ struct mkacc_ctx {
     int method_class = XZW;   // XZW or XZW_B
     uint32_t dg = 0, nk = 0;
     Mod mod{};
-    uint32_t qhalf = 0, gbits = 0;
+    SddConsts sd{};
     uint32_t ninv = 0, ninvp = 0, nval = 0, nvalp = 0;
     hipStream_t stream = nullptr;
     uint2* d_twf = nullptr;
     uint2* d_twi = nullptr;
-    uint2* d_psi = nullptr;
+    uint32_t* d_img = nullptr;    // LDS image: per-lane twiddles + psi table
     uint32_t* d_keys = nullptr;   // [k][n+1][nk][dg][2][N] C4, scaled
     uint32_t* d_pkey = nullptr;   // [k][dg][N] C4, scaled
     bool have_keys = false;
@@ -472,7 +557,7 @@ int launch_batch(mkacc_ctx* c, const uint32_t* d_ct, const uint32_t* d_in, uint3
     uint32_t* cur = c->d_acc0;
     uint32_t* nxt = c->d_acc1;
     const dim3 grid((unsigned)((B + kWavesPerBlock - 1) / kWavesPerBlock)), block(kThreads);
-    const size_t lds = kWavesPerBlock * kLdsWords * sizeof(uint32_t);
+    const size_t lds = kStepLdsBytes;
     for (uint32_t u = 0; u < k; ++u) {
         for (uint32_t i = 0; i < n; ++i) {
             const bool first = (u == 0 && i == 0);
@@ -484,16 +569,14 @@ int launch_batch(mkacc_ctx* c, const uint32_t* d_ct, const uint32_t* d_in, uint3
             a.key2 = c->nk == 2 ? key_step(c, u, i, 1) : a.key1;
             a.keys = key_step(c, 0, n, 0);
             a.pkey = c->d_pkey;
-            a.sumv = c->d_sumv;
             a.tw_fwd = c->d_twf;
             a.tw_inv = c->d_twi;
-            a.psi_pow = c->d_psi;
+            a.img = c->d_img;
             a.B = (uint32_t)B;
             a.k = k;
             a.index = u;
             a.m = c->mod;
-            a.qhalf = c->qhalf;
-            a.gbits = c->gbits;
+            a.sd = c->sd;
             StepFn fn = step_fn((int)c->dg, c->method_class, first);
             hipLaunchKernelGGL(fn, grid, block, lds, c->stream, a);
             std::swap(cur, nxt);
@@ -572,18 +655,18 @@ int prim_launch(mkacc_ctx* c, const uint32_t* in, uint32_t* out, size_t count, s
     HIP_TRY(hipMalloc(&din, count * kN * 4));
     HIP_TRY(hipMalloc(&dout, count * kN * 4 * out_mul));
     HIP_TRY(hipMemcpyAsync(din, in, count * kN * 4, hipMemcpyHostToDevice, c->stream));
-    const size_t lds = kWavesPerBlock * kLdsWords * sizeof(uint32_t);
+    const size_t lds = kStepLdsBytes;
     const dim3 grid((unsigned)((count + kWavesPerBlock - 1) / kWavesPerBlock)), block(kThreads);
     if (which == 0)
-        hipLaunchKernelGGL(ntt_fwd_kernel, grid, block, lds, c->stream, din, dout, (uint32_t)count, c->d_twf,
+        hipLaunchKernelGGL(ntt_fwd_kernel, grid, block, lds, c->stream, din, dout, (uint32_t)count, c->d_img, c->d_twf,
                            c->mod.Q);
     else if (which == 1)
-        hipLaunchKernelGGL(ntt_inv_kernel, grid, block, lds, c->stream, din, dout, (uint32_t)count, c->d_twi,
+        hipLaunchKernelGGL(ntt_inv_kernel, grid, block, lds, c->stream, din, dout, (uint32_t)count, c->d_img, c->d_twi,
                            c->mod.Q, c->ninv, c->ninvp);
     else {
         const size_t tot = count * kN;
         hipLaunchKernelGGL(sdd_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, c->stream, din, dout,
-                           (uint32_t)count, c->dg, c->mod.Q, c->qhalf, c->gbits);
+                           (uint32_t)count, c->dg, c->mod.Q, c->sd);
     }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(out, dout, count * kN * 4 * out_mul, hipMemcpyDeviceToHost, c->stream));
@@ -638,6 +721,10 @@ int mkacc_create(const mkacc_params* pin, int device, mkacc_ctx** out) {
     if (p.root == 0) p.root = root_of_unity(2ull * p.N, p.Q);
     const uint32_t dg = p.digitsG - 1;
     if (dg < 2 || dg > 5) return fail(MKACC_E_UNSUPPORTED, "engine supports 2..5 used gadget digits");
+    if ((uint32_t)__builtin_ctz(p.baseG) * p.digitsG > 32)
+        return fail(MKACC_E_UNSUPPORTED, "engine supports log2(baseG) * digitsG <= 32");
+    if (dg <= 3 && ((uint32_t)__builtin_ctz(p.baseG) * (dg - 1) > 16))
+        return fail(MKACC_E_UNSUPPORTED, "engine packs digits 2..dg into 16 bits");
     if (!is_primitive_root(p.root, 2ull * p.N, p.Q)) return fail(MKACC_E_ARG, "root is not a primitive 2N-th root");
 
     auto c = std::make_unique<mkacc_ctx>();
@@ -648,8 +735,17 @@ int mkacc_create(const mkacc_params* pin, int device, mkacc_ctx** out) {
     c->nk = c->method_class == XZW ? 2 : 1;
     c->mod.Q = (uint32_t)p.Q;
     c->mod.mu = (uint32_t)((1ull << 58) / p.Q);
-    c->qhalf = (uint32_t)(p.Q >> 1);
-    c->gbits = (uint32_t)__builtin_ctz(p.baseG);
+    {
+        // offset-word digit decomposition constants (mkacc_device.hpp)
+        const uint32_t b = (uint32_t)__builtin_ctz(p.baseG);
+        uint64_t C = 0;
+        for (uint32_t i = 0; i < p.digitsG; ++i) C += (1ull << (b - 1)) << (b * i);
+        c->sd.qhalf = (uint32_t)(p.Q >> 1);
+        c->sd.cpos = (uint32_t)C;
+        c->sd.cneg = (uint32_t)(C - p.Q);
+        c->sd.gbits = b;
+        c->sd.qm = (uint32_t)(p.Q - (1ull << (b - 1)));
+    }
     const uint64_t ninv = modinv(p.N, p.Q);
     c->ninv = (uint32_t)ninv;
     c->ninvp = (uint32_t)(((unsigned __int128)ninv << 32) / p.Q);
@@ -676,22 +772,36 @@ int mkacc_create(const mkacc_params* pin, int device, mkacc_ctx** out) {
     auto htf = shoup_table(tf, p.Q), hti = shoup_table(ti, p.Q), hpw = shoup_table(pw, p.Q);
     HIP_TRY(hipMalloc(&c->d_twf, htf.size() * sizeof(uint2)));
     HIP_TRY(hipMalloc(&c->d_twi, hti.size() * sizeof(uint2)));
-    HIP_TRY(hipMalloc(&c->d_psi, hpw.size() * sizeof(uint2)));
+    // LDS image: per-lane twiddle runs of both directions + swizzled psi table
+    std::vector<uint2> img(kImgPairs);
+    for (int dir = 0; dir < 2; ++dir) {
+        const std::vector<uint2>& T = dir == 0 ? htf : hti;
+        uint2* L = img.data() + dir * kTwlPairs;
+        for (int st = 5; st <= 9; ++st) {
+            const int NP = 1 << (st - 5);
+            for (int lhi = 0; lhi < 32; ++lhi)
+                for (int m = 0; m < NP; ++m) L[twl_off(st) + 32 * m + lhi] = T[(1 << st) + lhi * NP + m];
+        }
+        for (int ln = 0; ln < 64; ++ln)
+            for (int m = 0; m < 16; ++m) L[kTwlC + 64 * m + ln] = T[1024 + 16 * ln + m];
+    }
+    for (uint32_t e = 0; e < 2u * kN; ++e) img[2 * kTwlPairs + psi_pos(e)] = hpw[e];
+    HIP_TRY(hipMalloc(&c->d_img, img.size() * sizeof(uint2)));
     HIP_TRY(hipMemcpy(c->d_twf, htf.data(), htf.size() * sizeof(uint2), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->d_twi, hti.data(), hti.size() * sizeof(uint2), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(c->d_psi, hpw.data(), hpw.size() * sizeof(uint2), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c->d_img, img.data(), img.size() * sizeof(uint2), hipMemcpyHostToDevice));
     *out = c.release();
     return MKACC_OK;
 }
 
 void mkacc_destroy(mkacc_ctx* c) {
     if (!c) return;
-    hipSetDevice(c->device);
-    if (c->stream) hipStreamSynchronize(c->stream);
-    for (void* p : {(void*)c->d_twf, (void*)c->d_twi, (void*)c->d_psi, (void*)c->d_keys, (void*)c->d_pkey,
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (void* p : {(void*)c->d_twf, (void*)c->d_twi, (void*)c->d_img, (void*)c->d_keys, (void*)c->d_pkey,
                     (void*)c->d_acc0, (void*)c->d_acc1, (void*)c->d_cvals, (void*)c->d_sumv, (void*)c->d_ct, (void*)c->d_io})
-        if (p) hipFree(p);
-    if (c->stream) hipStreamDestroy(c->stream);
+        if (p) (void)hipFree(p);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
 

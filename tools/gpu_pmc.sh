@@ -3,12 +3,12 @@
 TAG=$1; shift
 export TMPDIR=/tmp
 mkdir -p gpurun_out/pmc_$TAG
-rocprofv3 -L > gpurun_out/pmc_$TAG/counters_list.txt 2>&1 || true
 i=0
 for CS in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
           "SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INST_CYCLES_VMEM GRBM_GUI_ACTIVE" \
+          "SQ_INSTS_VALU_MUL_U32 SQ_INSTS_SMEM SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA TCP_TOTAL_CACHE_ACCESSES_sum TCC_HIT_sum TCC_MISS_sum GRBM_COUNT" \
           "FETCH_SIZE" "WRITE_SIZE" ; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $CS -d gpurun_out/pmc_$TAG/p$i -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --cpu-baseline 0 --n-override 32 "$@" > gpurun_out/pmc_$TAG/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 gpurun_out/pmc_$TAG/p$i.log; }
 done
-ls gpurun_out/pmc_$TAG/*
+python3 tools/pmc_summary.py gpurun_out/pmc_$TAG

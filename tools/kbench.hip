@@ -61,11 +61,16 @@ int main() {
     CHK(hipMemcpy(dti, hti.data(), kN * 8, hipMemcpyHostToDevice));
     hipEvent_t e0, e1; CHK(hipEventCreate(&e0)); CHK(hipEventCreate(&e1));
     const char* names[] = {"ntt_fwd", "ntt_inv", "2 transposes"};
+    // occupancy forced through the dynamic LDS size: 4 waves per block,
+    // blocks per CU = 160 KiB / lds  ->  waves per SIMD = blocks per CU
+    for (int occ : {4, 2, 1})
     for (int mode = 0; mode < 3; ++mode) {
         auto fn = mode == 0 ? chain<0> : (mode == 1 ? chain<1> : chain<2>);
+        const size_t lds = occ == 4 ? 4 * kLdsWords * 4 : (occ == 2 ? 64 * 1024 : 100 * 1024);
+        if (mode == 0) printf("-- %d waves/SIMD\n", occ);
         for (int rep = 0; rep < 3; ++rep) {
             CHK(hipEventRecord(e0));
-            hipLaunchKernelGGL(fn, dim3(waves / 4), dim3(256), 4 * kLdsWords * 4, 0, d, dtf, dti, iters, (uint32_t)Q);
+            hipLaunchKernelGGL(fn, dim3(waves / 4), dim3(256), lds, 0, d, dtf, dti, iters, (uint32_t)Q);
             CHK(hipEventRecord(e1)); CHK(hipEventSynchronize(e1));
             float ms; CHK(hipEventElapsedTime(&ms, e0, e1));
             double per = ms * 1e3 / iters;   // us per "one op on every wave"
