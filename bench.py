@@ -166,7 +166,7 @@ def main():
         "vs_baseline": None,
         "dtype": "u32 (27-bit residues mod Q)",
         "data": "synthetic: uniform keys/ciphertexts, MNTRU test-vector accumulators",
-        "config": {"workload": f"EvalAcc of {args.paramset} 2-party MK-NTRU gate bootstraps "
+        "config": {"workload": f"EvalAcc of {args.paramset} {p.k}-party {'MK-NTRU' if p.method == 0 else 'MK-LWE'} gate bootstraps "
                                f"(k={p.k}, n={p.n}, N={p.N}, dg={dg}); gate tail (extraction/ModSwitch/"
                                f"KeySwitch) not included",
                    "paramset": args.paramset, "batch_per_gpu": B, "global_batch": world * B,

@@ -371,33 +371,41 @@ __device__ __forceinline__ uint32_t sdd_digit(uint32_t D, uint32_t i, const SddC
     return __builtin_amdgcn_ubfe(D, i * s.gbits, s.gbits) + s.qm;
 }
 
-// Digits 2..DG of every element, kept between the digit NTTs.  DG <= 3: the
-// (DG-1)*b <= 16 bits of digits 2..DG of two elements share one register
-// (b = 9 at DG = 2, b <= 8 at DG = 3); otherwise the offset word D is kept.
+// Digits 2..DG of every element, kept between the digit NTTs as the field
+// F = bits [2b, 2b + (DG-1) b) of the offset word D.
+//   DG <= 3: (DG-1) b <= 16 (b = 9..13 at DG = 2, b = 7..8 at DG = 3): two
+//            elements per register (16 VGPRs).
+//   DG >= 4: (DG-1) b <= 20 (b = 6 at DG = 4, b = 5 at DG = 5): the low 16 bits
+//            two per register, the high 4 bits eight per register (20 VGPRs).
 template <int DG>
 struct PackedDigits {
-    static constexpr bool kPack = DG <= 3;
-    static constexpr int kWords = kPack ? kRegs / 2 : kRegs;
-    uint32_t w[kWords];
+    static constexpr bool kWide = DG > 3;
+    uint32_t lo[kRegs / 2];
+    uint32_t hi[kWide ? kRegs / 8 : 1];
 
     // element r with offset word D: returns digit 1 (NTT input), stores the rest
     __device__ __forceinline__ uint32_t put(int r, uint32_t D, const SddConsts& s) {
-        if (kPack) {
-            const uint32_t f = __builtin_amdgcn_ubfe(D, 2u * s.gbits, 16u);   // digits 2..DG (bits above G*b are 0 here)
-            if ((r & 1) == 0) w[r >> 1] = f;
-            else w[r >> 1] |= f << 16;
-            // pin the packed word: otherwise the compiler sinks the packing to
-            // the later unpack and keeps every D live across the NTTs
-            if (r & 1) asm volatile("" : "+v"(w[r >> 1]));
-        } else {
-            w[r] = D;
+        const uint32_t f = __builtin_amdgcn_ubfe(D, 2u * s.gbits, kWide ? 20u : 16u);
+        if ((r & 1) == 0) lo[r >> 1] = kWide ? (f & 0xFFFFu) : f;
+        else lo[r >> 1] |= f << 16;
+        if (kWide) {
+            const uint32_t h = f >> 16;
+            if ((r & 7) == 0) hi[r >> 3] = h;
+            else hi[r >> 3] |= h << (4 * (r & 7));
+            if ((r & 7) == 7) asm volatile("" : "+v"(hi[r >> 3]));
         }
+        // pin the packed word: otherwise the compiler sinks the packing to
+        // the later unpack and keeps every D live across the NTTs
+        if (r & 1) asm volatile("" : "+v"(lo[r >> 1]));
         return sdd_digit(D, 1, s);
     }
     // digit i (2..DG) of element r as an NTT input
     __device__ __forceinline__ uint32_t get(int r, int i, const SddConsts& s) const {
-        if (kPack) return __builtin_amdgcn_ubfe(w[r >> 1], (r & 1) * 16u + (uint32_t)(i - 2) * s.gbits, s.gbits) + s.qm;
-        return sdd_digit(w[r], (uint32_t)i, s);
+        if (!kWide)
+            return __builtin_amdgcn_ubfe(lo[r >> 1], (r & 1) * 16u + (uint32_t)(i - 2) * s.gbits, s.gbits) + s.qm;
+        const uint32_t f = __builtin_amdgcn_ubfe(lo[r >> 1], (r & 1) * 16u, 16u) |
+                           (__builtin_amdgcn_ubfe(hi[r >> 3], 4u * (r & 7), 4u) << 16);
+        return __builtin_amdgcn_ubfe(f, (uint32_t)(i - 2) * s.gbits, s.gbits) + s.qm;
     }
 };
 

@@ -155,12 +155,13 @@ __device__ __forceinline__ uint32_t key_eff(uint32_t k1, uint32_t k2, uint32_t k
     }
 }
 
-// Bounds of the lazy 64-bit sums (reduce58 needs < 2^58): digit NTT outputs are
-// left in [0, 4Q) when DG <= 3 (sum of DG products < 3 * 4Q^2 < 2^58) and
-// brought to [0, 2Q) otherwise (5 * 2Q^2 < 2^58); keys are canonical.
+// Bounds of the lazy 64-bit sums (reduce58 needs < 2^58, Q < 2^27): digit NTT
+// outputs are left in [0, 4Q) when DG <= 4 (DG products plus a residue stay
+// below 16 Q^2 < 2^58) and brought to [0, 2Q) at DG = 5 (10 Q^2 + Q < 2^58);
+// keys are canonical.
 template <int DG>
 __device__ __forceinline__ void digit_range(uint32_t (&x)[kRegs], uint32_t Q) {
-    if (DG > 3) {
+    if (DG > 4) {
 #pragma unroll
         for (int r = 0; r < kRegs; ++r) x[r] = min(x[r], x[r] - 2u * Q);
     }
@@ -168,7 +169,8 @@ __device__ __forceinline__ void digit_range(uint32_t (&x)[kRegs], uint32_t Q) {
 
 // Key words of one 4-register group of a MAC: software-pipelined kPrefetch
 // groups ahead so the L2 latency of the step's key block overlaps the arithmetic.
-constexpr int kPrefetch = 1;
+template <int DG>
+struct Prefetch { static constexpr int value = DG <= 3 ? 1 : 0; };
 struct KeyGroup {
     u32x4 k1, k2, ks, pk;
 };
@@ -183,6 +185,7 @@ __device__ __forceinline__ void mac_digit(const uint32_t (&g)[kRegs], int i, uin
     const uint32_t polyB = kN * 4u;
     const uint32_t koff = (uint32_t)(2 * i) * polyB;
     const uint32_t poff = (u * DG + (uint32_t)i) * polyB;
+    constexpr int kPrefetch = Prefetch<DG>::value;
     KeyGroup kg[kPrefetch + 1];
     auto issue = [&](KeyGroup& t, int gq) {
         const uint32_t go = gq * 1024u;
@@ -209,13 +212,14 @@ __device__ __forceinline__ void mac_digit(const uint32_t (&g)[kRegs], int i, uin
 }
 
 // w += h * f_i                                  (xzw.cpp:281-288)
-template <int METHOD, bool FIRST>
+template <int DG, int METHOD, bool FIRST>
 __device__ __forceinline__ void mac_index(const uint32_t (&h)[kRegs], int i, uint64_t (&w)[kRegs],
                                           __amdgpu_buffer_rsrc_t rk1, __amdgpu_buffer_rsrc_t rk2,
                                           __amdgpu_buffer_rsrc_t rks, const uint2* psi, const Mono& mp,
                                           const Mono& mn, uint32_t vo, uint32_t Q) {
     const uint32_t polyB = kN * 4u;
     const uint32_t koff = (uint32_t)(2 * i + 1) * polyB;
+    constexpr int kPrefetch = Prefetch<DG>::value;
     KeyGroup kg[kPrefetch + 1];
     auto issue = [&](KeyGroup& t, int gq) {
         const uint32_t go = gq * 1024u;
@@ -361,7 +365,7 @@ __global__ __launch_bounds__(kThreads, 2) void mk_step_kernel(StepArgs a) {
         }
         ntt_fwd(x, lds, a.tw_fwd, tb.twf, l, Q);
         digit_range<DG>(x, Q);
-        mac_index<METHOD, FIRST>(x, i, w, rk1, rk2, rks, tb.psi, mp, mn, vo, Q);
+        mac_index<DG, METHOD, FIRST>(x, i, w, rk1, rk2, rks, tb.psi, mp, mn, vo, Q);
     }
     const uint32_t ioff = a.index * polyB;
 #pragma unroll
@@ -723,8 +727,9 @@ int mkacc_create(const mkacc_params* pin, int device, mkacc_ctx** out) {
     if (dg < 2 || dg > 5) return fail(MKACC_E_UNSUPPORTED, "engine supports 2..5 used gadget digits");
     if ((uint32_t)__builtin_ctz(p.baseG) * p.digitsG > 32)
         return fail(MKACC_E_UNSUPPORTED, "engine supports log2(baseG) * digitsG <= 32");
-    if (dg <= 3 && ((uint32_t)__builtin_ctz(p.baseG) * (dg - 1) > 16))
-        return fail(MKACC_E_UNSUPPORTED, "engine packs digits 2..dg into 16 bits");
+    if ((uint32_t)__builtin_ctz(p.baseG) * (dg - 1) > (dg <= 3 ? 16u : 20u) ||
+        (dg > 3 && 2u * __builtin_ctz(p.baseG) + 20u > 32u))
+        return fail(MKACC_E_UNSUPPORTED, "engine packs gadget digits 2..dg into 16 (dg <= 3) or 20 bits");
     if (!is_primitive_root(p.root, 2ull * p.N, p.Q)) return fail(MKACC_E_ARG, "root is not a primitive 2N-th root");
 
     auto c = std::make_unique<mkacc_ctx>();
