@@ -1,0 +1,204 @@
+// C++ tests of the host mirror (include/mkfhe_amd_binfhe.hpp) written the way
+// the reference's own binfhe unit tests read: build params, keys and an
+// accumulator, call EvalAcc, compare.  The expected values come from the CPU
+// oracle (oracle/mkfhe_oracle.c), which only tests may link.
+//
+//   ./test_binfhe_mirror cpu   -- host logic only (no GPU calls)
+//   ./test_binfhe_mirror gpu   -- bit-exact parity through the HIP engine
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "mkfhe_amd_binfhe.hpp"
+#include "mkfhe_oracle.h"
+
+using namespace mkfhe_amd;
+
+static int g_fail = 0;
+#define EXPECT(cond)                                                               \
+    do {                                                                           \
+        if (!(cond)) {                                                             \
+            std::fprintf(stderr, "FAIL %s:%d: %s\n", __FILE__, __LINE__, #cond);   \
+            ++g_fail;                                                              \
+        }                                                                          \
+    } while (0)
+template <class E, class F>
+static bool throws(F f) {
+    try {
+        f();
+    } catch (const E&) {
+        return true;
+    } catch (...) {
+        return false;
+    }
+    return false;
+}
+
+static const uint64_t kQ = 134176769;
+
+// ---- host-only checks ---------------------------------------------------------
+static void test_cpu() {
+    auto p = UniEncCryptoParams::FromParamSet("STD128_MKNTRU", MKNTRU);
+    EXPECT(p->Getk() == 2 && p->GetLatticeParam() == 765 && p->GetN() == 2048);
+    EXPECT(p->GetQ() == kQ && p->Getq() == 45181 && p->GetBaseG() == 128 && p->GetDigitsG() == 4);
+    auto pl = UniEncCryptoParams::FromParamSet("STD100_MKNTRU_LWE_2", MKNTRU_LWE);
+    EXPECT(pl->Getk() == 4 && pl->GetLatticeParam() == 500 && pl->Getq() == 32749 && pl->GetDigitsG() == 3);
+    // reference error behaviour: config_error on a non-power-of-two gadget base
+    // (mk-cryptoparameters.h:146-147) and on an invalid method
+    EXPECT(throws<config_error>([] { UniEncCryptoParams(2, 2048, kQ, 45181, 100, MKNTRU, 10); }));
+    EXPECT(throws<config_error>([] { UniEncCryptoParams(2, 2048, kQ, 45181, 512, GINX, 10); }));
+    EXPECT(throws<config_error>([] { UniEncCryptoParams::FromParamSet("STD128", MKNTRU); }));
+    EXPECT(throws<config_error>([] { MakeUniEncAccumulator(LMKCDEY); }));
+    EXPECT(dynamic_cast<UniEncAccumulatorXZW*>(MakeUniEncAccumulator(MKNTRU).get()) != nullptr);
+    EXPECT(dynamic_cast<UniEncAccumulatorXZW_B*>(MakeUniEncAccumulator(MKNTRU_LWE).get()) != nullptr);
+    // EvalAcc without keys: config_error before any device work (binfhe-base-scheme.cpp:1075-1080)
+    auto acc = MakeUniEncAccumulator(MKNTRU);
+    ConstUniEncACCKey none;
+    MKACCCiphertext a = std::make_shared<MKACCCiphertextImpl>();
+    EXPECT(throws<config_error>([&] { acc->EvalAcc(p, none, {}, {}, a, {}); }));
+    // the method check is per accumulator class
+    auto accB = MakeUniEncAccumulator(MKNTRU_B);
+    ConstUniEncACCKey some = std::make_shared<const UniEncACCKeyImpl>();
+    EXPECT(throws<config_error>([&] { accB->EvalAcc(p, some, {}, {}, a, {}); }));
+}
+
+// ---- GPU parity ------------------------------------------------------------------
+struct Case {
+    BINFHE_METHOD method;
+    uint32_t k, n;
+    uint64_t q;
+    uint32_t baseG;
+    uint32_t B;
+};
+
+static std::vector<uint64_t> uniform(size_t n, uint64_t bound, uint64_t seed) {
+    std::vector<uint64_t> v(n);
+    orc_fill_uniform(v.data(), n, bound, seed);
+    return v;
+}
+
+static void run_case(const Case& cs, uint64_t seed) {
+    const uint32_t N = 2048;
+    auto params = std::make_shared<UniEncCryptoParams>(cs.k, N, kQ, cs.q, cs.baseG, cs.method, cs.n);
+    auto acc = MakeUniEncAccumulator(cs.method);
+    const mkacc_params eff = acc->Params(*params);
+    const uint32_t dg = eff.digitsG - 1, nk = cs.method == MKNTRU ? 2 : 1;
+
+    orc_params op{};
+    op.method = cs.method == MKNTRU ? ORC_XZW : ORC_XZW_B;
+    op.k = cs.k; op.n = cs.n; op.N = N; op.Q = kQ; op.q = cs.q; op.baseG = cs.baseG;
+    op.digitsG = eff.digitsG; op.psi = eff.root;
+    orc_ctx* oc = orc_ctx_create(&op);
+    EXPECT(oc != nullptr);
+
+    // keys: the reference containers, filled with seed-derived residues
+    auto evk = uniform(orc_evk_words(&op), kQ, seed * 10 + 1);
+    auto pk = uniform((size_t)cs.k * dg * N, kQ, seed * 10 + 2);
+    auto ek = std::make_shared<UniEncACCKeyImpl>(cs.k, nk, cs.n + 1);
+    size_t o = 0;
+    for (uint32_t u = 0; u < cs.k; ++u)
+        for (uint32_t j = 0; j < nk; ++j)
+            for (uint32_t i = 0; i <= cs.n; ++i) {
+                auto key = std::make_shared<UniEncEvalKeyImpl>(dg, 2);
+                for (uint32_t d = 0; d < dg; ++d)
+                    for (uint32_t c = 0; c < 2; ++c, o += N)
+                        key->GetElements()[d][c] =
+                            NativePoly(NativeVector(evk.begin() + o, evk.begin() + o + N), EVALUATION);
+                (*ek)[u][j][i] = key;
+            }
+    std::vector<std::vector<NativePoly>> Pkey(cs.k);
+    for (uint32_t u = 0; u < cs.k; ++u)
+        for (uint32_t d = 0; d < dg; ++d) {
+            const size_t b = ((size_t)u * dg + d) * N;
+            Pkey[u].emplace_back(NativeVector(pk.begin() + b, pk.begin() + b + N), EVALUATION);
+        }
+    ConstUniEncACCKey cek = ek;
+
+    const uint64_t bound = cs.method == MKNTRU ? cs.q : 2 * N;
+    auto ct = uniform((size_t)cs.B * cs.k * cs.n, bound, seed * 10 + 3);
+    auto acc0 = uniform((size_t)cs.B * cs.k * N, kQ, seed * 10 + 4);
+    ct[0] = 0;                                            // monomial edge c = 0
+    ct[(size_t)cs.k * cs.n - 1] = bound - 1;              // and c = 2N - 1
+    auto expect = acc0;
+    EXPECT(orc_evalacc_batch(oc, evk.data(), pk.data(), ct.data(), expect.data(), cs.B, 8) == 0);
+
+    std::vector<MKACCCiphertext> accs;
+    std::vector<std::vector<NativeVector>> cts;
+    for (uint32_t b = 0; b < cs.B; ++b) {
+        std::vector<NativePoly> el;
+        std::vector<NativeVector> c;
+        for (uint32_t u = 0; u < cs.k; ++u) {
+            const size_t ao = ((size_t)b * cs.k + u) * N, co = ((size_t)b * cs.k + u) * cs.n;
+            el.emplace_back(NativeVector(acc0.begin() + ao, acc0.begin() + ao + N), EVALUATION);
+            c.emplace_back(ct.begin() + co, ct.begin() + co + cs.n);
+        }
+        accs.push_back(std::make_shared<MKACCCiphertextImpl>(el));
+        cts.push_back(c);
+    }
+    // gate 0 through the reference-shaped EvalAcc, the rest as a batch
+    MKACCCiphertext a0 = accs[0];
+    acc->EvalAcc(params, cek, Pkey, {}, a0, cts[0]);
+    std::vector<MKACCCiphertext> rest(accs.begin() + 1, accs.end());
+    std::vector<std::vector<NativeVector>> rcts(cts.begin() + 1, cts.end());
+    acc->EvalAccBatch(params, cek, Pkey, rest, rcts);
+    size_t bad = 0;
+    for (uint32_t b = 0; b < cs.B; ++b)
+        for (uint32_t u = 0; u < cs.k; ++u)
+            for (uint32_t j = 0; j < N; ++j)
+                bad += accs[b]->GetElements()[u][j] != expect[((size_t)b * cs.k + u) * N + j];
+    if (bad) std::fprintf(stderr, "case method=%d k=%u n=%u: %zu coefficients differ\n", cs.method, cs.k, cs.n, bad);
+    EXPECT(bad == 0);
+
+    // primitives: SetFormat (NTT) and SignedDigitDecompose against the oracle
+    NativePoly x(uniform(N, kQ, seed * 10 + 5), COEFFICIENT);
+    NativePoly y = x;
+    acc->SetFormat(params, y, EVALUATION);
+    std::vector<uint64_t> ref = x.values;
+    orc_ntt_forward(ref.data(), N, kQ, eff.root);
+    EXPECT(y.values == ref && y.format == EVALUATION);
+    acc->SetFormat(params, y, COEFFICIENT);
+    EXPECT(y == x);
+    std::vector<NativePoly> digits;
+    acc->SignedDigitDecompose(params, x, digits);
+    std::vector<uint64_t> rd((size_t)dg * N);
+    orc_sdd(x.values.data(), rd.data(), N, kQ, cs.baseG, dg);
+    EXPECT(digits.size() == dg);
+    for (uint32_t d = 0; d < dg && d < digits.size(); ++d)
+        EXPECT(std::memcmp(digits[d].values.data(), rd.data() + (size_t)d * N, N * 8) == 0);
+
+    // range errors keep the reference's exception class (math_error)
+    auto badacc = std::make_shared<MKACCCiphertextImpl>(accs[0]->GetElements());
+    badacc->GetElements()[0][5] = kQ;
+    EXPECT(throws<math_error>([&] { acc->EvalAcc(params, cek, Pkey, {}, badacc, cts[0]); }));
+    orc_ctx_destroy(oc);
+}
+
+static void test_gpu() {
+    const Case cases[] = {
+        {MKNTRU, 2, 4, 45181, 1 << 9, 3},      // STD100_MKNTRU shape
+        {MKNTRU, 2, 3, 45181, 1 << 7, 2},      // STD128_MKNTRU shape (dg = 3)
+        {MKNTRU_LWE, 4, 3, 32749, 1 << 9, 2},  // STD100_MKNTRU_LWE_2 shape
+        {MKNTRU, 3, 2, 45181, 1 << 6, 2},      // dg = 4
+    };
+    uint64_t seed = 1;
+    for (const Case& c : cases) run_case(c, seed++);
+}
+
+int main(int argc, char** argv) {
+    const std::string mode = argc > 1 ? argv[1] : "cpu";
+    try {
+        if (mode == "cpu") test_cpu();
+        else test_gpu();
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "unexpected exception: %s\n", e.what());
+        return 2;
+    }
+    if (g_fail) {
+        std::fprintf(stderr, "%d check(s) failed\n", g_fail);
+        return 1;
+    }
+    std::printf("ok (%s)\n", mode.c_str());
+    return 0;
+}
