@@ -46,6 +46,16 @@ def algorithmic_counts(k: int, n: int, dg: int, N: int = 2048, B: int = 1):
     return mulmods, bytes_
 
 
+def measured_traffic(paramset: str):
+    """Per-launch HBM bytes of the step kernel from the committed PMC record
+    (profiles/traffic_<paramset>.json, written by tools/pmc_summary.py from
+    separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes), or None."""
+    f = os.path.join(ROOT, "profiles", f"traffic_{paramset}.json")
+    if not os.path.exists(f):
+        return None
+    return json.load(open(f))["traffic_bytes"]
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -172,7 +182,8 @@ def main():
                    "paramset": args.paramset, "batch_per_gpu": B, "global_batch": world * B,
                    "parallelism": f"gate-sharded x{world}"},
         "roofline": {"bound": "hbm", "achieved": by / per_launch_s / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                     "frac": by / per_launch_s / 1e9 / PEAK_HBM_GBS, "traffic": None,
+                     "frac": by / per_launch_s / 1e9 / PEAK_HBM_GBS,
+                     "traffic": measured_traffic(args.paramset) if not args.n_override else None,
                      "kernel": "mk_step_kernel", "per_launch_us": per_launch_s * 1e6,
                      "bytes_per_launch": by},
         "roofline_valu": {"bound": "valu-int", "achieved": mm / per_launch_s / 1e12, "peak": PEAK_SHOUP_MULMOD_TPS / 1e12,
