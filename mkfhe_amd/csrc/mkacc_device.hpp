@@ -179,11 +179,11 @@ __device__ __forceinline__ const uint2* opaque(const uint2* p) {
     return (const uint2*)v;
 }
 
-// ---- per-lane twiddles, staged in LDS ------------------------------------------
+// ---- per-lane twiddles ----------------------------------------------------------
 // Pass B (stages 5..9) and pass C (stage 10) need per-lane twiddles.  They are
-// copied once per workgroup into LDS in an interleaved order so that a wave's
-// read of "twiddle m" is one conflict-free ds_read_b64 at a lane-dependent
-// base plus an immediate offset:
+// stored in an interleaved order so that a wave's read of "twiddle m" is one
+// fully coalesced 512-byte dwordx2 load (or, from LDS, one conflict-free
+// ds_read_b64) at a lane-dependent base plus an immediate offset:
 //   stage s in 5..9 : pair (m, lhi) at  twl_off(s) + 32*m + lhi   (lhi = lane >> 1)
 //   stage 10        : pair (m, lane) at kTwlC + 64*m + lane
 // Entry (m, lhi) of stage s is reference table index 2^s + lhi*2^(s-5) + m, and

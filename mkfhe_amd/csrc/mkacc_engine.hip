@@ -46,20 +46,29 @@ int fail(int code, const std::string& msg) {
             return fail(MKACC_E_DEVICE, std::string(#expr) + ": " + hipGetErrorString(_e));    \
     } while (0)
 
-constexpr int kWavesPerBlock = 8;                 // one 512-thread workgroup per CU (2 waves / SIMD)
+// 256-thread workgroups, two per CU (2 waves / SIMD, LDS 65.8 KB each).
+// 512-thread workgroups sharing one LDS table image (one per CU) were tried
+// and rejected: waves 4-7 of such a workgroup produced rare, run-to-run
+// varying wrong results on MI355X (tools/dbg/stress.py; root cause not
+// identified -- isolated transposes and LDS fills were clean), while two
+// 4-wave workgroups per CU are deterministic and measured faster.
+constexpr int kWavesPerBlock = 4;
 constexpr int kThreads = 64 * kWavesPerBlock;
 
-// LDS image shared by a workgroup (built once per context, copied in at kernel start):
+// Table image (built once per context, HBM):
 //   [0, kTwlPairs)                forward per-lane twiddles (mkacc_device.hpp layout)
 //   [kTwlPairs, 2 kTwlPairs)      inverse per-lane twiddles
 //   [2 kTwlPairs, + 2N)           psi^e (e in [0, 2N)) with Shoup companion, at psi_pos(e)
+// The NTTs read the twiddle runs from HBM/L2 (L1-resident, coalesced); the psi
+// table, gathered at data-dependent slots, is copied into LDS at kernel start,
 // followed by one transpose scratch of kLdsWords per wave.
 constexpr int kPsiPairs = 2 * kN;
 constexpr int kImgPairs = 2 * kTwlPairs + kPsiPairs;
 constexpr int kImgWords = 2 * kImgPairs;
-constexpr size_t kStepLdsBytes = (size_t)(kImgWords + kWavesPerBlock * kLdsWords) * 4;
-static_assert(kImgWords % 4 == 0, "LDS image is copied with dwordx4");
-static_assert(kStepLdsBytes <= 160 * 1024, "LDS budget");
+constexpr int kLdsPsiWords = 2 * kPsiPairs;
+constexpr size_t kStepLdsBytes = (size_t)(kLdsPsiWords + kWavesPerBlock * kLdsWords) * 4;
+static_assert(kLdsPsiWords % 4 == 0, "psi table is copied with dwordx4");
+static_assert(2 * kStepLdsBytes <= 160 * 1024, "two workgroups per CU");
 
 // Bank-spreading position of psi^e in the LDS table: the exponents a wave
 // gathers (c * (2 brv(j) + 1) mod 2N) repeat in their low 5 bits across lanes;
@@ -76,7 +85,7 @@ struct StepArgs {
     const uint32_t* key2;      // ev2 = (*ek)[u][1][i] (XZW)
     const uint32_t* keys;      // evs = (*ek)[0][0][n] (first step)
     const uint32_t* pkey;      // [k][dg][N]
-    const uint32_t* img;       // LDS image [kImgWords]
+    const uint32_t* img;       // table image [kImgWords]
     const uint2* tw_fwd;       // [N] reference forward table (pass A, scalar reads)
     const uint2* tw_inv;       // [N]
     uint32_t B, k, index;
@@ -84,22 +93,23 @@ struct StepArgs {
     SddConsts sd;
 };
 
-// Copy the LDS image (twiddles + psi table) into this workgroup's LDS.
+// Copy the psi table of the image into this workgroup's LDS.
 __device__ __forceinline__ void load_image(uint32_t* smem, const uint32_t* img) {
+    // psi starts at pair 2 kTwlPairs = uint4 index kTwlPairs
     const uint4* src = reinterpret_cast<const uint4*>(img);
     uint4* dst = reinterpret_cast<uint4*>(smem);
-    for (int i = threadIdx.x; i < kImgWords / 4; i += blockDim.x) dst[i] = src[i];
+    for (int i = threadIdx.x; i < kLdsPsiWords / 4; i += blockDim.x) dst[i] = src[i + kTwlPairs];
     __syncthreads();
 }
 
 struct Tables {
-    const uint2* twf;   // LDS
-    const uint2* twi;   // LDS
+    const uint2* twf;   // HBM image: forward per-lane twiddles
+    const uint2* twi;   // HBM image: inverse per-lane twiddles
     const uint2* psi;   // LDS
 };
-__device__ __forceinline__ Tables tables(uint32_t* smem) {
-    const uint2* b = reinterpret_cast<const uint2*>(smem);
-    return Tables{b, b + kTwlPairs, b + 2 * kTwlPairs};
+__device__ __forceinline__ Tables tables(uint32_t* smem, const uint32_t* img) {
+    const uint2* g = reinterpret_cast<const uint2*>(img);
+    return Tables{g, g + kTwlPairs, reinterpret_cast<const uint2*>(smem)};
 }
 
 // Monomial X^e at EVAL slot j = (lane << 5) | r: the reference stores
@@ -114,7 +124,11 @@ struct Mono {
                                        1, 17, 9, 25, 5, 21, 13, 29, 3, 19, 11, 27, 7, 23, 15, 31};
         // opaque: keeps the 32 per-slot exponents from being hoisted out of the
         // party / digit loops (they would stay live in VGPRs across the NTTs)
-        const uint32_t e = (opaque_v(co) + c * (128u * kBr5[r])) & (2u * kN - 1u);
+        // the wave-uniform part is recomputed per use (one s_mul) rather than
+        // kept as 32 hoisted SGPR constants per monomial
+        uint32_t cs = c;
+        asm volatile("" : "+s"(cs));
+        const uint32_t e = (opaque_v(co) + cs * (128u * kBr5[r])) & (2u * kN - 1u);
         return psi[psi_pos(e)];
     }
 };
@@ -172,16 +186,19 @@ __device__ __forceinline__ void digit_range(uint32_t (&x)[kRegs], uint32_t Q) {
 template <int DG>
 struct Prefetch { static constexpr int value = DG <= 3 ? 1 : 0; };
 struct KeyGroup {
-    u32x4 k1, k2, ks, pk;
+    u32x4 k1, k2, ks, pk, acc;
 };
 
 // uj_u += g * d_i ; sv += g * P[u][i]          (xzw.cpp:263-269)
-template <int DG, int METHOD, bool FIRST>
+// START (digit 0): uj_u starts from acc_u (AddToAccXZW's acc + acctemp,
+// xzw.cpp:342-344), streamed in with the keys; 0 in the FIRST step, where
+// AddToAccXZW0 overwrites acc (xzw.cpp:380).
+template <int DG, int METHOD, bool FIRST, bool START>
 __device__ __forceinline__ void mac_digit(const uint32_t (&g)[kRegs], int i, uint32_t u, uint64_t (&uj)[kRegs],
                                           uint64_t (&sv)[kRegs], __amdgpu_buffer_rsrc_t rk1,
                                           __amdgpu_buffer_rsrc_t rk2, __amdgpu_buffer_rsrc_t rks,
-                                          __amdgpu_buffer_rsrc_t rpk, const uint2* psi, const Mono& mp,
-                                          const Mono& mn, uint32_t vo, uint32_t Q) {
+                                          __amdgpu_buffer_rsrc_t rpk, __amdgpu_buffer_rsrc_t rin, const uint2* psi,
+                                          const Mono& mp, const Mono& mn, uint32_t vo, uint32_t Q) {
     const uint32_t polyB = kN * 4u;
     const uint32_t koff = (uint32_t)(2 * i) * polyB;
     const uint32_t poff = (u * DG + (uint32_t)i) * polyB;
@@ -193,6 +210,7 @@ __device__ __forceinline__ void mac_digit(const uint32_t (&g)[kRegs], int i, uin
         t.pk = bload4(rpk, vo, poff + go);
         if (METHOD == XZW) t.k2 = bload4(rk2, vo, koff + go);
         if (FIRST) t.ks = bload4(rks, vo, koff + go);
+        if (START && !FIRST) t.acc = bload4(rin, vo, u * polyB + go);
     };
 #pragma unroll
     for (int j = 0; j < kPrefetch; ++j) issue(kg[j], j);
@@ -204,7 +222,7 @@ __device__ __forceinline__ void mac_digit(const uint32_t (&g)[kRegs], int i, uin
         for (int e = 0; e < 4; ++e) {
             const int r = 4 * gq + e;
             const uint32_t deff = key_eff<METHOD, FIRST>(t.k1[e], t.k2[e], t.ks[e], psi, mp, mn, r, Q);
-            uj[r] = mad64(g[r], deff, uj[r]);
+            uj[r] = mad64(g[r], deff, START ? (uint64_t)(FIRST ? 0u : t.acc[e]) : uj[r]);
             sv[r] = mad64(g[r], t.pk[e], sv[r]);
         }
         sched_fence();
@@ -251,129 +269,167 @@ __device__ __forceinline__ void mac_index(const uint32_t (&h)[kRegs], int i, uin
 // uj_u = sum_i g_i d_i, sumV = sum_u sum_i g_i P[u][i] and w = sum_i h_i f_i are
 // lazy 64-bit accumulators (v_mad_u64_u32) reduced once; all sums are exact
 // mod Q, so the reordering is bit-exact.
+// Per-wave state shared by the passes of one step.
+struct StepCtx {
+    const Tables tb;
+    uint32_t* lds;
+    const StepArgs* a;
+    Mod m;
+    SddConsts sd;
+    Mono mp, mn;
+    uint32_t l, vo;
+    __amdgpu_buffer_rsrc_t rin, rout, rk1, rk2, rks, rpk;
+};
+
+// One party u of HbProd (mk-acc-xzw.cpp:245-270) fused with AddToAccXZW's
+// rotation and final add (xzw.cpp:336-344):
+//   uj_u = (FIRST ? 0 : acc_u) + sum_i NTT(g_i) * d_i,   g = SDD(iNTT(acc_u * (X^c - 1)))
+//   sv  += sum_i NTT(g_i) * P[u][i]
+// Party `index` is processed last (LAST): its sum stays in registers (`keep`)
+// and receives the f-part of HbProd before the single store.
+template <int DG, int METHOD, bool FIRST, bool LAST>
+__device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_t (&sv)[kRegs],
+                                           uint32_t (&keep)[kRegs]) {
+    constexpr int kDigitUnroll = 1;
+    const uint32_t Q = s.m.Q, polyB = kN * 4u;
+    uint32_t x[kRegs];
+    uint64_t uj[kRegs];
+#pragma unroll
+    for (int gq = 0; gq < 8; ++gq) {
+        const u32x4 t = bload4(s.rin, s.vo, u * polyB + gq * 1024u);
+        x[4 * gq] = t.x; x[4 * gq + 1] = t.y; x[4 * gq + 2] = t.z; x[4 * gq + 3] = t.w;
+    }
+    if (!FIRST) {
+        // acctemp = acc * (X^c - 1)                     (xzw.cpp:336-338)
+        // x canonical -> x*X^c - x + Q in (0, 3Q) -> [0, 2Q)
+#pragma unroll
+        for (int r0 = 0; r0 < kRegs; r0 += 8) {
+#pragma unroll
+            for (int r = r0; r < r0 + 8; ++r) {
+                const uint32_t y = mul_shoup_lazy(x[r], s.mp.at(s.tb.psi, r), Q) + Q - x[r];
+                x[r] = min(y, y - 2u * Q);
+            }
+            sched_fence();
+        }
+    }
+    ntt_inv_noscale(x, s.lds, s.a->tw_inv, s.tb.twi, s.l, Q);
+    // SignedDigitDecompose (mk-acc.cpp:54-80): digit 1 -> x, digits 2.. packed
+    PackedDigits<DG> pd;
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) {
+        x[r] = pd.put(r, sdd_offset(x[r], s.sd), s.sd);
+        if ((r & 7) == 7) sched_fence();
+    }
+    ntt_fwd(x, s.lds, s.a->tw_fwd, s.tb.twf, s.l, Q);
+    digit_range<DG>(x, Q);
+    mac_digit<DG, METHOD, FIRST, true>(x, 0, u, uj, sv, s.rk1, s.rk2, s.rks, s.rpk, s.rin, s.tb.psi, s.mp, s.mn,
+                                       s.vo, Q);
+#pragma unroll kDigitUnroll
+    for (int i = 1; i < DG; ++i) {
+#pragma unroll
+        for (int r = 0; r < kRegs; ++r) x[r] = pd.get(r, i + 1, s.sd);
+        ntt_fwd(x, s.lds, s.a->tw_fwd, s.tb.twf, s.l, Q);
+        digit_range<DG>(x, Q);
+        mac_digit<DG, METHOD, FIRST, false>(x, i, u, uj, sv, s.rk1, s.rk2, s.rks, s.rpk, s.rin, s.tb.psi, s.mp,
+                                            s.mn, s.vo, Q);
+    }
+    // acc_u <- uj_u (canonical); sumV reduced per party
+#pragma unroll
+    for (int gq = 0; gq < 8; ++gq) {
+        u32x4 t;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int r = 4 * gq + e;
+            t[e] = reduce58(uj[r], s.m);
+            sv[r] = reduce58(sv[r], s.m);
+            if (LAST) keep[r] = t[e];
+        }
+        if (!LAST) bstore4(t, s.rout, s.vo, u * polyB + gq * 1024u);
+    }
+}
+
+// One accumulator step for one gate per wavefront.
+//   FIRST:  AddToAccXZW0 (mk-acc-xzw.cpp:347-381 / xzw_B.cpp:333-381): acc <- HbProd(acc)
+//   else:   AddToAccXZW  (mk-acc-xzw.cpp:292-345 / xzw_B.cpp:281-330):
+//           acc <- acc + HbProd(acc * (X^c - 1))
+// HbProd is mk-acc-xzw.cpp:231-290, register resident: the per-slot sums
+// uj_u = sum_i g_i d_i, sumV = sum_u sum_i g_i P[u][i] and w = sum_i h_i f_i are
+// lazy 64-bit accumulators (v_mad_u64_u32) reduced once; all sums are exact
+// mod Q, so the reordering (parties in the order index+1, ..., index) is
+// bit-exact.
 template <int DG, int METHOD, bool FIRST>
 __global__ __launch_bounds__(kThreads, 2) void mk_step_kernel(StepArgs a) {
-    // register allocation fits without spills when the digit loop is unrolled
-    // for DG = 2 and kept rolled for DG >= 3 (measured, hipcc ROCm 7.2)
     constexpr int kDigitUnroll = DG == 2 ? 2 : 1;
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     load_image(smem, a.img);
-    const Tables tb = tables(smem);
     const uint32_t l = threadIdx.x & 63u;
     // wave-uniform (SGPR) gate index: the per-gate buffer descriptors must be
     // scalar, otherwise every load through them becomes a waterfall loop
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t gate = blockIdx.x * kWavesPerBlock + wv;
     if (gate >= a.B) return;
-    uint32_t* lds = smem + kImgWords + wv * kLdsWords;
-    const Mod m = a.m;
-    const uint32_t Q = m.Q;
-    const SddConsts sd = a.sd;
+    const uint32_t Q = a.m.Q;
     const uint32_t c = __builtin_amdgcn_readfirstlane(a.cvals[gate]);
     const uint32_t cneg = (2u * kN - c) & (2u * kN - 1u);
-    const Mono mp = make_mono(c, l), mn = make_mono(cneg, l);
-    const uint32_t k = a.k;
+    const uint32_t k = a.k, index = a.index;
     const uint32_t polyB = kN * 4u;
-    const uint32_t vo = l * 16u;   // lane offset of a C4 dwordx4
-
-    const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.acc_in + (size_t)gate * k * kN, k * polyB);
-    const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.acc_out + (size_t)gate * k * kN, k * polyB);
-    const __amdgpu_buffer_rsrc_t rk1 = make_rsrc(a.key1, DG * 2 * polyB);
-    const __amdgpu_buffer_rsrc_t rk2 = make_rsrc(a.key2, DG * 2 * polyB);
-    const __amdgpu_buffer_rsrc_t rks = make_rsrc(a.keys, DG * 2 * polyB);
-    const __amdgpu_buffer_rsrc_t rpk = make_rsrc(a.pkey, k * DG * polyB);
+    const StepCtx s{tables(smem, a.img),
+                    smem + kLdsPsiWords + wv * kLdsWords,
+                    &a,
+                    a.m,
+                    a.sd,
+                    make_mono(c, l),
+                    make_mono(cneg, l),
+                    l,
+                    l * 16u,
+                    make_rsrc(a.acc_in + (size_t)gate * k * kN, k * polyB),
+                    make_rsrc(a.acc_out + (size_t)gate * k * kN, k * polyB),
+                    make_rsrc(a.key1, DG * 2 * polyB),
+                    make_rsrc(a.key2, DG * 2 * polyB),
+                    make_rsrc(a.keys, DG * 2 * polyB),
+                    make_rsrc(a.pkey, k * DG * polyB)};
 
     uint64_t sv[kRegs];
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) sv[r] = 0;
-
-    for (uint32_t u = 0; u < k; ++u) {
-        uint32_t x[kRegs];
-#pragma unroll
-        for (int gq = 0; gq < 8; ++gq) {
-            const u32x4 t = bload4(rin, vo, u * polyB + gq * 1024u);
-            x[4 * gq] = t.x; x[4 * gq + 1] = t.y; x[4 * gq + 2] = t.z; x[4 * gq + 3] = t.w;
-        }
-        if (!FIRST) {
-            // acctemp = acc * (X^c - 1)                     (xzw.cpp:336-338)
-            // x canonical -> x*X^c - x + Q in (0, 3Q) -> [0, 2Q)
-#pragma unroll
-            for (int r0 = 0; r0 < kRegs; r0 += 8) {
-#pragma unroll
-                for (int r = r0; r < r0 + 8; ++r) {
-                    const uint32_t y = mul_shoup_lazy(x[r], mp.at(tb.psi, r), Q) + Q - x[r];
-                    x[r] = min(y, y - 2u * Q);
-                }
-                sched_fence();
-            }
-        }
-        ntt_inv_noscale(x, lds, a.tw_inv, tb.twi, l, Q);
-        // SignedDigitDecompose (mk-acc.cpp:54-80): digit 1 -> x, digits 2.. packed
-        PackedDigits<DG> pd;
-#pragma unroll
-        for (int r = 0; r < kRegs; ++r) {
-            x[r] = pd.put(r, sdd_offset(x[r], sd), sd);
-            if ((r & 7) == 7) sched_fence();
-        }
-        uint64_t uj[kRegs];
-#pragma unroll
-        for (int r = 0; r < kRegs; ++r) uj[r] = 0;
-#pragma unroll kDigitUnroll
-        for (int i = 0; i < DG; ++i) {
-            if (i > 0) {
-#pragma unroll
-                for (int r = 0; r < kRegs; ++r) x[r] = pd.get(r, i + 1, sd);
-            }
-            ntt_fwd(x, lds, a.tw_fwd, tb.twf, l, Q);
-            digit_range<DG>(x, Q);
-            mac_digit<DG, METHOD, FIRST>(x, i, u, uj, sv, rk1, rk2, rks, rpk, tb.psi, mp, mn, vo, Q);
-        }
-        // acc_u <- (FIRST ? 0 : acc_u) + uj_u   (xzw.cpp:270, 342-344); sumV reduced per party
-#pragma unroll
-        for (int gq = 0; gq < 8; ++gq) {
-            u32x4 t = {0, 0, 0, 0};
-            if (!FIRST) t = bload4(rin, vo, u * polyB + gq * 1024u);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int r = 4 * gq + e;
-                t[e] = reduce58(uj[r] + t[e], m);
-                sv[r] = reduce58(sv[r], m);
-            }
-            bstore4(t, rout, vo, u * polyB + gq * 1024u);
-        }
+    uint32_t keep[kRegs];
+    for (uint32_t t = 1; t < k; ++t) {
+        const uint32_t u = index + t < k ? index + t : index + t - k;
+        party_pass<DG, METHOD, FIRST, false>(s, u, sv, keep);
     }
+    party_pass<DG, METHOD, FIRST, true>(s, index, sv, keep);
 
     // second half of HbProd: iNTT(sumV) -> SDD -> NTT -> acc[index] += <., f>
     uint32_t x[kRegs];
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) x[r] = (uint32_t)sv[r];
-    ntt_inv_noscale(x, lds, a.tw_inv, tb.twi, l, Q);
+    ntt_inv_noscale(x, s.lds, a.tw_inv, s.tb.twi, l, Q);
     PackedDigits<DG> pd;
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) {
-        x[r] = pd.put(r, sdd_offset(x[r], sd), sd);
+        x[r] = pd.put(r, sdd_offset(x[r], s.sd), s.sd);
         if ((r & 7) == 7) sched_fence();
     }
     uint64_t w[kRegs];
 #pragma unroll
-    for (int r = 0; r < kRegs; ++r) w[r] = 0;
+    for (int r = 0; r < kRegs; ++r) w[r] = keep[r];
 #pragma unroll kDigitUnroll
     for (int i = 0; i < DG; ++i) {
         if (i > 0) {
 #pragma unroll
-            for (int r = 0; r < kRegs; ++r) x[r] = pd.get(r, i + 1, sd);
+            for (int r = 0; r < kRegs; ++r) x[r] = pd.get(r, i + 1, s.sd);
         }
-        ntt_fwd(x, lds, a.tw_fwd, tb.twf, l, Q);
+        ntt_fwd(x, s.lds, a.tw_fwd, s.tb.twf, l, Q);
         digit_range<DG>(x, Q);
-        mac_index<DG, METHOD, FIRST>(x, i, w, rk1, rk2, rks, tb.psi, mp, mn, vo, Q);
+        mac_index<DG, METHOD, FIRST>(x, i, w, s.rk1, s.rk2, s.rks, s.tb.psi, s.mp, s.mn, s.vo, Q);
     }
-    const uint32_t ioff = a.index * polyB;
+    const uint32_t ioff = index * polyB;
 #pragma unroll
     for (int gq = 0; gq < 8; ++gq) {
-        u32x4 t = bload4(rout, vo, ioff + gq * 1024u);
+        u32x4 t;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) t[e] = reduce58(w[4 * gq + e] + t[e], m);
-        bstore4(t, rout, vo, ioff + gq * 1024u);
+        for (int e = 0; e < 4; ++e) t[e] = reduce58(w[4 * gq + e], s.m);
+        bstore4(t, s.rout, s.vo, ioff + gq * 1024u);
     }
 }
 
@@ -417,7 +473,7 @@ __global__ __launch_bounds__(kThreads) void ntt_fwd_kernel(const uint32_t* __res
                                                             uint32_t Q) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     load_image(smem, img);
-    const Tables tb = tables(smem);
+    const Tables tb = tables(smem, img);
     const uint32_t l = threadIdx.x & 63u, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t p = blockIdx.x * kWavesPerBlock + wv;
     if (p >= count) return;
@@ -425,7 +481,7 @@ __global__ __launch_bounds__(kThreads) void ntt_fwd_kernel(const uint32_t* __res
     uint32_t x[kRegs];
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) x[r] = src[jA(l, r)];
-    ntt_fwd(x, smem + kImgWords + wv * kLdsWords, twf, tb.twf, l, Q);
+    ntt_fwd(x, smem + kLdsPsiWords + wv * kLdsWords, twf, tb.twf, l, Q);
     uint32_t* dst = out + (size_t)p * kN;
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) dst[jC(l, r)] = canon4(x[r], Q);
@@ -436,7 +492,7 @@ __global__ __launch_bounds__(kThreads) void ntt_inv_kernel(const uint32_t* __res
                                                             uint32_t Q, uint32_t ninv, uint32_t ninvp) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     load_image(smem, img);
-    const Tables tb = tables(smem);
+    const Tables tb = tables(smem, img);
     const uint32_t l = threadIdx.x & 63u, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t p = blockIdx.x * kWavesPerBlock + wv;
     if (p >= count) return;
@@ -444,7 +500,7 @@ __global__ __launch_bounds__(kThreads) void ntt_inv_kernel(const uint32_t* __res
     uint32_t x[kRegs];
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) x[r] = src[jC(l, r)];
-    ntt_inv_noscale(x, smem + kImgWords + wv * kLdsWords, twi, tb.twi, l, Q);
+    ntt_inv_noscale(x, smem + kLdsPsiWords + wv * kLdsWords, twi, tb.twi, l, Q);
     uint32_t* dst = out + (size_t)p * kN;
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) dst[jA(l, r)] = mul_shoup(x[r], ninv, ninvp, Q);

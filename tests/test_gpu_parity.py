@@ -78,7 +78,7 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("case", CASES, ids=[f"{c[0]}-k{c[1]}-n{c[2]}-B{c[4]}" for c in CASES])
+@pytest.mark.parametrize("case", CASES, ids=[f"{c[0]}-k{c[1]}-n{c[2]}-logB{c[4].bit_length() - 1}-B{c[5]}" for c in CASES])
 def test_evalacc_small_parity(mk, oracle, case):
     meth, k, n, q, baseG, B = case
     om = oracle.XZW if meth == "XZW" else oracle.XZW_B
@@ -160,3 +160,18 @@ def test_errors(mk, oracle):
     with pytest.raises(mk.MkaccError):
         eng.upload_keys(bad, pkey)
     assert eng.eval_batch(ct[:0], acc[:0]).shape == (0, 2, 2048)
+
+
+def test_evalacc_many_gates_every_wave_slot(mk, oracle):
+    """512 gates (every wave slot of every workgroup, all CUs partly busy),
+    three repeated runs: bit-exact and run-to-run identical.  Guards against
+    the nondeterminism seen with 512-thread workgroups."""
+    B = 512
+    orc, evk, pkey, ct, acc = make_case(oracle, oracle.XZW, 2, 2, 45181, 1 << 7, B, seed=77)
+    exp = orc.evalacc_batch(evk, pkey, ct, acc, 16).astype(np.uint32)
+    eng = _engine(mk, mk.MKNTRU, 2, 2, 45181, 1 << 7)
+    eng.upload_keys(evk.astype(np.uint32), pkey.astype(np.uint32))
+    for _ in range(3):
+        got = eng.eval_batch(ct.astype(np.uint32), acc.astype(np.uint32))
+        bad = [g for g in range(B) if not np.array_equal(got[g], exp[g])]
+        assert not bad, f"gates differing from the oracle: {bad[:16]}"
