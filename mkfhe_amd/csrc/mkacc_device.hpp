@@ -241,8 +241,10 @@ __device__ __forceinline__ void inv_stage_b(uint32_t (&x)[kRegs], const uint2* t
 //          with scalar loads (wave-uniform indices 1..31)
 //   twl  : this direction's per-lane LDS table (layout above)
 // Input residues in [0, 4Q); output EVAL values in [0, 4Q) (not canonical).
+//   tw10 : stage-10 twiddles (pairs (m, lane) at tw10 + 64*m + lane); twl + kTwlC
+//          or a copy of that block in LDS
 __device__ __forceinline__ void ntt_fwd(uint32_t (&x)[kRegs], uint32_t* lds, const uint2* tw_g, const uint2* twl,
-                                        uint32_t l, uint32_t Q) {
+                                        const uint2* tw10, uint32_t l, uint32_t Q) {
     // pass A: stages 0..4 (bits 10..6); twiddle index uniform across the wave
     const ConstTable twc{(const_u64*)opaque(tw_g)};
 #pragma unroll
@@ -267,7 +269,7 @@ __device__ __forceinline__ void ntt_fwd(uint32_t (&x)[kRegs], uint32_t* lds, con
     fwd_stage_b<9>(x, twl, lhi, Q);
     transpose<1, 2>(x, lds, l);
     // pass C: stage 10 (bit 0), in two halves of 8 twiddles
-    const uint2* tc = twl + kTwlC + lo;
+    const uint2* tc = tw10 + lo;
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
         uint2 w[8];

@@ -65,9 +65,10 @@ constexpr int kThreads = 64 * kWavesPerBlock;
 constexpr int kPsiPairs = 2 * kN;
 constexpr int kImgPairs = 2 * kTwlPairs + kPsiPairs;
 constexpr int kImgWords = 2 * kImgPairs;
-constexpr int kLdsPsiWords = 2 * kPsiPairs;
-constexpr size_t kStepLdsBytes = (size_t)(kLdsPsiWords + kWavesPerBlock * kLdsWords) * 4;
-static_assert(kLdsPsiWords % 4 == 0, "psi table is copied with dwordx4");
+// LDS: [forward stage-10 twiddles, 1024 pairs][psi table, 2N pairs][scratch]
+constexpr int kLdsTabWords = 2 * (1024 + kPsiPairs);
+constexpr size_t kStepLdsBytes = (size_t)(kLdsTabWords + kWavesPerBlock * kLdsWords) * 4;
+static_assert(kLdsTabWords % 4 == 0, "LDS tables are copied with dwordx4");
 static_assert(2 * kStepLdsBytes <= 160 * 1024, "two workgroups per CU");
 
 // Bank-spreading position of psi^e in the LDS table: the exponents a wave
@@ -93,23 +94,28 @@ struct StepArgs {
     SddConsts sd;
 };
 
-// Copy the psi table of the image into this workgroup's LDS.
+// Copy the forward stage-10 twiddles (the largest per-lane run, used by 3/4
+// of the NTTs) and the psi table of the image into this workgroup's LDS.
 __device__ __forceinline__ void load_image(uint32_t* smem, const uint32_t* img) {
-    // psi starts at pair 2 kTwlPairs = uint4 index kTwlPairs
     const uint4* src = reinterpret_cast<const uint4*>(img);
     uint4* dst = reinterpret_cast<uint4*>(smem);
-    for (int i = threadIdx.x; i < kLdsPsiWords / 4; i += blockDim.x) dst[i] = src[i + kTwlPairs];
+    // stage 10 of the forward table: pairs [kTwlC, kTwlC + 1024) = uint4 [kTwlC/2, +512)
+    for (int i = threadIdx.x; i < 512; i += blockDim.x) dst[i] = src[kTwlC / 2 + i];
+    // psi: pairs [2 kTwlPairs, + 2N) = uint4 [kTwlPairs, + N)
+    for (int i = threadIdx.x; i < kN; i += blockDim.x) dst[512 + i] = src[kTwlPairs + i];
     __syncthreads();
 }
 
 struct Tables {
-    const uint2* twf;   // HBM image: forward per-lane twiddles
-    const uint2* twi;   // HBM image: inverse per-lane twiddles
-    const uint2* psi;   // LDS
+    const uint2* twf;    // HBM image: forward per-lane twiddles
+    const uint2* twi;    // HBM image: inverse per-lane twiddles
+    const uint2* twfc;   // LDS: forward stage-10 twiddles
+    const uint2* psi;    // LDS
 };
 __device__ __forceinline__ Tables tables(uint32_t* smem, const uint32_t* img) {
     const uint2* g = reinterpret_cast<const uint2*>(img);
-    return Tables{g, g + kTwlPairs, reinterpret_cast<const uint2*>(smem)};
+    const uint2* t = reinterpret_cast<const uint2*>(smem);
+    return Tables{g, g + kTwlPairs, t, t + 1024};
 }
 
 // Monomial X^e at EVAL slot j = (lane << 5) | r: the reference stores
@@ -273,7 +279,8 @@ __device__ __forceinline__ void mac_index(const uint32_t (&h)[kRegs], int i, uin
 struct StepCtx {
     const Tables tb;
     uint32_t* lds;
-    const StepArgs* a;
+    const uint2* tw_fwd;
+    const uint2* tw_inv;
     Mod m;
     SddConsts sd;
     Mono mp, mn;
@@ -312,7 +319,7 @@ __device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_
             sched_fence();
         }
     }
-    ntt_inv_noscale(x, s.lds, s.a->tw_inv, s.tb.twi, s.l, Q);
+    ntt_inv_noscale(x, s.lds, s.tw_inv, s.tb.twi, s.l, Q);
     // SignedDigitDecompose (mk-acc.cpp:54-80): digit 1 -> x, digits 2.. packed
     PackedDigits<DG> pd;
 #pragma unroll
@@ -320,7 +327,7 @@ __device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_
         x[r] = pd.put(r, sdd_offset(x[r], s.sd), s.sd);
         if ((r & 7) == 7) sched_fence();
     }
-    ntt_fwd(x, s.lds, s.a->tw_fwd, s.tb.twf, s.l, Q);
+    ntt_fwd(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, s.l, Q);
     digit_range<DG>(x, Q);
     mac_digit<DG, METHOD, FIRST, true>(x, 0, u, uj, sv, s.rk1, s.rk2, s.rks, s.rpk, s.rin, s.tb.psi, s.mp, s.mn,
                                        s.vo, Q);
@@ -328,7 +335,7 @@ __device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_
     for (int i = 1; i < DG; ++i) {
 #pragma unroll
         for (int r = 0; r < kRegs; ++r) x[r] = pd.get(r, i + 1, s.sd);
-        ntt_fwd(x, s.lds, s.a->tw_fwd, s.tb.twf, s.l, Q);
+        ntt_fwd(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, s.l, Q);
         digit_range<DG>(x, Q);
         mac_digit<DG, METHOD, FIRST, false>(x, i, u, uj, sv, s.rk1, s.rk2, s.rks, s.rpk, s.rin, s.tb.psi, s.mp,
                                             s.mn, s.vo, Q);
@@ -374,8 +381,9 @@ __global__ __launch_bounds__(kThreads, 2) void mk_step_kernel(StepArgs a) {
     const uint32_t k = a.k, index = a.index;
     const uint32_t polyB = kN * 4u;
     const StepCtx s{tables(smem, a.img),
-                    smem + kLdsPsiWords + wv * kLdsWords,
-                    &a,
+                    smem + kLdsTabWords + wv * kLdsWords,
+                    a.tw_fwd,
+                    a.tw_inv,
                     a.m,
                     a.sd,
                     make_mono(c, l),
@@ -403,7 +411,7 @@ __global__ __launch_bounds__(kThreads, 2) void mk_step_kernel(StepArgs a) {
     uint32_t x[kRegs];
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) x[r] = (uint32_t)sv[r];
-    ntt_inv_noscale(x, s.lds, a.tw_inv, s.tb.twi, l, Q);
+    ntt_inv_noscale(x, s.lds, s.tw_inv, s.tb.twi, l, Q);
     PackedDigits<DG> pd;
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) {
@@ -419,7 +427,7 @@ __global__ __launch_bounds__(kThreads, 2) void mk_step_kernel(StepArgs a) {
 #pragma unroll
             for (int r = 0; r < kRegs; ++r) x[r] = pd.get(r, i + 1, s.sd);
         }
-        ntt_fwd(x, s.lds, a.tw_fwd, s.tb.twf, l, Q);
+        ntt_fwd(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, l, Q);
         digit_range<DG>(x, Q);
         mac_index<DG, METHOD, FIRST>(x, i, w, s.rk1, s.rk2, s.rks, s.tb.psi, s.mp, s.mn, s.vo, Q);
     }
@@ -481,7 +489,7 @@ __global__ __launch_bounds__(kThreads) void ntt_fwd_kernel(const uint32_t* __res
     uint32_t x[kRegs];
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) x[r] = src[jA(l, r)];
-    ntt_fwd(x, smem + kLdsPsiWords + wv * kLdsWords, twf, tb.twf, l, Q);
+    ntt_fwd(x, smem + kLdsTabWords + wv * kLdsWords, twf, tb.twf, tb.twfc, l, Q);
     uint32_t* dst = out + (size_t)p * kN;
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) dst[jC(l, r)] = canon4(x[r], Q);
@@ -500,7 +508,7 @@ __global__ __launch_bounds__(kThreads) void ntt_inv_kernel(const uint32_t* __res
     uint32_t x[kRegs];
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) x[r] = src[jC(l, r)];
-    ntt_inv_noscale(x, smem + kLdsPsiWords + wv * kLdsWords, twi, tb.twi, l, Q);
+    ntt_inv_noscale(x, smem + kLdsTabWords + wv * kLdsWords, twi, tb.twi, l, Q);
     uint32_t* dst = out + (size_t)p * kN;
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) dst[jA(l, r)] = mul_shoup(x[r], ninv, ninvp, Q);

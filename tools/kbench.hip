@@ -24,11 +24,11 @@ __global__ __launch_bounds__(256, 4) void chain(uint32_t* data, const uint2* twf
     load_c4(x, data + (size_t)p * kN, l);
     for (int it = 0; it < iters; ++it) {
         if (MODE == 0) {
-            ntt_fwd(x, lds, twf, l, Q);
+            ntt_fwd(x, lds, twf, twf, twf + kTwlC, l, Q);
 #pragma unroll
             for (int r = 0; r < kRegs; ++r) x[r] = min(x[r], x[r] - 2 * Q);
         } else if (MODE == 1) {
-            ntt_inv_noscale(x, lds, twi, l, Q);
+            ntt_inv_noscale(x, lds, twi, twi, l, Q);
         } else {
             transpose<0, 1>(x, lds, l);
             transpose<1, 2>(x, lds, l);
