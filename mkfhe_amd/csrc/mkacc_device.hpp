@@ -131,9 +131,31 @@ __device__ __forceinline__ void transpose(uint32_t (&x)[kRegs], uint32_t* lds, u
 
 // ---- forward NTT (Cooley-Tukey, reference table indexing) -------------------
 // tw[i] = { psi^brv(i), companion }, i in [0, N): reference rootOfUnityTable.
-// Lazy (Harvey) butterflies: the forward NTT keeps values in [0, 4Q), the
-// inverse in [0, 2Q) (4Q < 2^29, so nothing overflows 32 bits).  Shoup's
-// product q*Q - x*w is formed negated so both outputs take one instruction.
+// Lazy butterflies.  Shoup's product T = b*w - q*Q lies in [0, 2Q) for ANY
+// 32-bit b, so the forward transform never reduces b, and it reduces a only
+// once, at the last stage: a stage maps values below A to values below A + 2Q
+// (a + T, a - T + 2Q), so inputs below 4Q stay below 4Q + 10*2Q = 24Q < 2^32
+// (Q < 2^27) through stages 0..9; stage 10 brings a back under 2Q and emits
+// [0, 4Q).  Shoup's product is formed negated so both outputs take one
+// instruction.  The inverse (GS) keeps values in [0, 2Q).
+__device__ __forceinline__ void ct_bfly_lazy(uint32_t& a, uint32_t& b, uint2 w, uint32_t Q) {
+    const uint32_t X = a;
+    const uint32_t q = __umulhi(b, w.y);
+    const uint32_t Tn = q * Q - b * w.x;                         // -T, T in [0, 2Q)
+    a = X - Tn;                                                  // X + T
+    b = X + Tn + 2u * Q;                                         // X - T + 2Q
+}
+// last stage: a in [0, 24Q) -> X in [0, 2Q); outputs in [0, 4Q)
+__device__ __forceinline__ void ct_bfly_last(uint32_t& a, uint32_t& b, uint2 w, uint32_t Q) {
+    uint32_t X = min(a, a - 16u * Q);
+    X = min(X, X - 8u * Q);
+    X = min(X, X - 4u * Q);
+    X = min(X, X - 2u * Q);                                      // [0, 2Q)
+    const uint32_t q = __umulhi(b, w.y);
+    const uint32_t Tn = q * Q - b * w.x;
+    a = X - Tn;                                                  // [0, 4Q)
+    b = X + Tn + 2u * Q;                                         // (0, 4Q)
+}
 __device__ __forceinline__ void ct_bfly(uint32_t& a, uint32_t& b, uint2 w, uint32_t Q) {
     const uint32_t X = min(a, a - 2u * Q);                      // [0, 2Q)
     const uint32_t q = __umulhi(b, w.y);
@@ -210,7 +232,7 @@ __device__ __forceinline__ void fwd_stage_b(uint32_t (&x)[kRegs], const uint2* t
             if (r & H) continue;
             const int m = r >> SH;
             if (m < c0 || m >= c0 + CH) continue;
-            ct_bfly(x[r], x[r + H], w[m - c0], Q);
+            ct_bfly_lazy(x[r], x[r + H], w[m - c0], Q);
         }
         sched_fence();
     }
@@ -254,7 +276,7 @@ __device__ __forceinline__ void ntt_fwd(uint32_t (&x)[kRegs], uint32_t* lds, con
         for (int r = 0; r < kRegs; ++r) {
             if (r & h) continue;
             const uint2 w = twc[(1 << s) + (r >> (5 - s))];
-            ct_bfly(x[r], x[r + h], w, Q);
+            ct_bfly_lazy(x[r], x[r + h], w, Q);
         }
         sched_fence();
     }
@@ -276,7 +298,7 @@ __device__ __forceinline__ void ntt_fwd(uint32_t (&x)[kRegs], uint32_t* lds, con
 #pragma unroll
         for (int m = 0; m < 8; ++m) w[m] = tc[64 * (8 * hf + m)];
 #pragma unroll
-        for (int m = 0; m < 8; ++m) ct_bfly(x[16 * hf + 2 * m], x[16 * hf + 2 * m + 1], w[m], Q);
+        for (int m = 0; m < 8; ++m) ct_bfly_last(x[16 * hf + 2 * m], x[16 * hf + 2 * m + 1], w[m], Q);
         sched_fence();
     }
 }
