@@ -110,6 +110,48 @@ int mkacc_sync(mkacc_ctx* ctx);
 /* The context's HIP stream (hipStream_t as void*), for event timing. */
 void* mkacc_stream(mkacc_ctx* ctx);
 
+/* ---- gate level: head + EvalAcc + tail -------------------------------------
+ * BinFHEScheme::EvalBinGate for MK-NTRU (binfhe-base-scheme.cpp:467-515) and
+ * MK-LWE (binfhe-base-scheme.cpp:380-463): gate head, BootstrapGateCore
+ * (test vector + EvalAcc, :1004-1130), extraction (Transpose + iNTT,
+ * :498-506 / :441-449), ModSwitch to qKS (RoundqQ in double,
+ * mntru-pke.cpp:11-16, 359-374) and the key switch (KeySwitch2,
+ * mntru-pke.cpp:763-823 / KeySwitch, mklwe-pke.cpp:260-298).
+ * Only NAND is supported, as in the reference (ctGateGen, :340-376). */
+typedef struct mkacc_ks_params {
+    uint64_t qKS;      /* key-switching modulus (modKS; 45181 / 32749 in every MK set) */
+    uint32_t baseKS;   /* key-switching digit base (baseKS = 32); at most 256 */
+    uint32_t n_out;    /* dimension of the output ciphertext (latticeParam n) */
+} mkacc_ks_params;
+
+/* Digits per coefficient: ceil(log qKS / log baseKS) (mntru-pke.cpp:771). */
+uint32_t mkacc_ks_digits(const mkacc_ks_params* ks);
+
+/* MK-NTRU KeySwitch2 key.  ksk [k][N*dks][n_out] = KSK2[u][1] of
+ * KeySwitchGen2 (mntru-pke.cpp:744-755); the engine relies on
+ * KSK2[u][j] = j * KSK2[u][1] mod qKS, which KeySwitchGen2 guarantees. */
+int mkacc_upload_ksk_mntru(mkacc_ctx* ctx, const mkacc_ks_params* ks, const uint32_t* ksk);
+/* MK-LWE KeySwitch key (mklwe-pke.cpp:176-258): A [k][N][baseKS][dks][n_out],
+ * B [k][N][baseKS][dks] (GetElementsA / GetElementsB). */
+int mkacc_upload_ksk_mklwe(mkacc_ctx* ctx, const mkacc_ks_params* ks, const uint32_t* A, const uint32_t* B);
+
+/* B NAND gates, MK-NTRU.  ct_nand [k][n] (ctGateGen), ct1/ct2 [B][k][n] mod q
+ * -> out [B][k][n_out] mod qKS.  Host buffers, synchronous. */
+int mkacc_eval_nand_mntru(mkacc_ctx* ctx, const uint32_t* ct_nand, const uint32_t* ct1, const uint32_t* ct2,
+                          uint32_t* out, size_t B);
+/* B NAND gates, MK-LWE.  a1/a2 [B][k][n], b1/b2 [B] mod q
+ * -> out_a [B][k][n_out], out_b [B] mod qKS.  Host buffers, synchronous. */
+int mkacc_eval_nand_mklwe(mkacc_ctx* ctx, const uint32_t* a1, const uint32_t* b1, const uint32_t* a2,
+                          const uint32_t* b2, uint32_t* out_a, uint32_t* out_b, size_t B);
+/* Device-pointer form of both (ct_nand unused for MK-LWE, b1/b2/out_b unused
+ * for MK-NTRU); enqueued on the context stream. */
+int mkacc_eval_nand_device(mkacc_ctx* ctx, const uint32_t* d_ct_nand, const uint32_t* d_a1, const uint32_t* d_b1,
+                           const uint32_t* d_a2, const uint32_t* d_b2, uint32_t* d_out_a, uint32_t* d_out_b,
+                           size_t B);
+/* The tail alone on B accumulators acc [B][k][N] (EVAL, reference order):
+ * extraction + ModSwitch + key switch -> out_a [B][k][n_out] (+ out_b [B]). */
+int mkacc_gate_tail(mkacc_ctx* ctx, const uint32_t* acc, uint32_t* out_a, uint32_t* out_b, size_t B);
+
 /* ---- primitives exposed for parity tests (same layouts as above) ---- */
 /* NativePoly::SetFormat(EVALUATION) on `count` polys: COEFF -> EVAL. */
 int mkacc_ntt_forward(mkacc_ctx* ctx, const uint32_t* in, uint32_t* out, size_t count);

@@ -46,6 +46,12 @@ class MkaccParams(ctypes.Structure):
         return {f: getattr(self, f) for f, _ in self._fields_}
 
 
+class MkaccKsParams(ctypes.Structure):
+    """struct mkacc_ks_params (include/mkfhe_amd.h)."""
+
+    _fields_ = [("qKS", ctypes.c_uint64), ("baseKS", ctypes.c_uint32), ("n_out", ctypes.c_uint32)]
+
+
 # every symbol include/mkfhe_amd.h declares, with (restype, argtypes)
 SIGNATURES = {
     "mkacc_paramset": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_uint32, ctypes.POINTER(MkaccParams)]),
@@ -61,6 +67,14 @@ SIGNATURES = {
                                                ctypes.c_void_p, ctypes.c_size_t]),
     "mkacc_sync": (ctypes.c_int, [ctypes.c_void_p]),
     "mkacc_stream": (ctypes.c_void_p, [ctypes.c_void_p]),
+    "mkacc_ks_digits": (ctypes.c_uint32, [ctypes.POINTER(MkaccKsParams)]),
+    "mkacc_upload_ksk_mntru": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MkaccKsParams), _u32p]),
+    "mkacc_upload_ksk_mklwe": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(MkaccKsParams), _u32p, _u32p]),
+    "mkacc_eval_nand_mntru": (ctypes.c_int, [ctypes.c_void_p, _u32p, _u32p, _u32p, _u32p, ctypes.c_size_t]),
+    "mkacc_eval_nand_mklwe": (ctypes.c_int, [ctypes.c_void_p, _u32p, _u32p, _u32p, _u32p, _u32p, _u32p,
+                                             ctypes.c_size_t]),
+    "mkacc_eval_nand_device": (ctypes.c_int, [ctypes.c_void_p] + [ctypes.c_void_p] * 7 + [ctypes.c_size_t]),
+    "mkacc_gate_tail": (ctypes.c_int, [ctypes.c_void_p, _u32p, _u32p, _u32p, ctypes.c_size_t]),
     "mkacc_ntt_forward": (ctypes.c_int, [ctypes.c_void_p, _u32p, _u32p, ctypes.c_size_t]),
     "mkacc_ntt_inverse": (ctypes.c_int, [ctypes.c_void_p, _u32p, _u32p, ctypes.c_size_t]),
     "mkacc_sdd": (ctypes.c_int, [ctypes.c_void_p, _u32p, _u32p, ctypes.c_size_t]),

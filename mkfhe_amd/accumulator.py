@@ -76,6 +76,7 @@ class MKAccumulatorEngine:
         self.nk = 2 if eff.method == MKNTRU else 1
         self.device = device
         self._key_token = None
+        self.ks = None
 
     def close(self):
         if getattr(self, "_h", None):
@@ -137,6 +138,70 @@ class MKAccumulatorEngine:
 
     def stream_handle(self) -> int:
         return _lib.load().mkacc_stream(self._h) or 0
+
+    # -- gate level (head + EvalAcc + tail) ----------------------------------------
+    def upload_ksk_mntru(self, ksk: np.ndarray, qKS: int, baseKS: int, n_out: int):
+        """KeySwitch2 key: ksk [k][N*dks][n_out] = KSK2[u][1] (mntru-pke.cpp:744-755)."""
+        ks = _lib.MkaccKsParams(qKS, baseKS, n_out)
+        a = np.ascontiguousarray(ksk, dtype=np.uint32)
+        check(_lib.load().mkacc_upload_ksk_mntru(self._h, ctypes.byref(ks), _u32(a)))
+        self.ks = ks
+
+    def upload_ksk_mklwe(self, A: np.ndarray, B: np.ndarray, qKS: int, baseKS: int, n_out: int):
+        """MK-LWE KeySwitch key: A [k][N][Bks][dks][n_out], B [k][N][Bks][dks] (mklwe-pke.cpp:176-258)."""
+        ks = _lib.MkaccKsParams(qKS, baseKS, n_out)
+        a = np.ascontiguousarray(A, dtype=np.uint32)
+        b = np.ascontiguousarray(B, dtype=np.uint32)
+        check(_lib.load().mkacc_upload_ksk_mklwe(self._h, ctypes.byref(ks), _u32(a), _u32(b)))
+        self.ks = ks
+
+    def _need_ksk(self):
+        if self.ks is None:
+            raise MkaccError(_lib.MKACC_E_NOKEYS, "Key-switching keys have not been uploaded")
+
+    def eval_nand_mntru(self, ct_nand: np.ndarray, ct1: np.ndarray, ct2: np.ndarray) -> np.ndarray:
+        """B MK-NTRU NAND gates (EvalBinGate, binfhe-base-scheme.cpp:467-515) -> [B][k][n_out]."""
+        self._need_ksk()
+        c1 = np.ascontiguousarray(ct1, dtype=np.uint32)
+        c2 = np.ascontiguousarray(ct2, dtype=np.uint32)
+        cn = np.ascontiguousarray(ct_nand, dtype=np.uint32)
+        B = c1.shape[0]
+        out = np.empty((B, self.k, self.ks.n_out), dtype=np.uint32)
+        check(_lib.load().mkacc_eval_nand_mntru(self._h, _u32(cn), _u32(c1), _u32(c2), _u32(out), B))
+        return out
+
+    def eval_nand_mklwe(self, a1, b1, a2, b2):
+        """B MK-LWE NAND gates (binfhe-base-scheme.cpp:380-463) -> (a [B][k][n_out], b [B])."""
+        self._need_ksk()
+        a1 = np.ascontiguousarray(a1, dtype=np.uint32)
+        a2 = np.ascontiguousarray(a2, dtype=np.uint32)
+        b1 = np.ascontiguousarray(b1, dtype=np.uint32)
+        b2 = np.ascontiguousarray(b2, dtype=np.uint32)
+        B = a1.shape[0]
+        oa = np.empty((B, self.k, self.ks.n_out), dtype=np.uint32)
+        ob = np.empty(B, dtype=np.uint32)
+        check(_lib.load().mkacc_eval_nand_mklwe(self._h, _u32(a1), _u32(b1), _u32(a2), _u32(b2), _u32(oa),
+                                                _u32(ob), B))
+        return oa, ob
+
+    def eval_nand_device(self, d_nand, d_a1, d_b1, d_a2, d_b2, d_out_a, d_out_b, B: int):
+        """Device-pointer gates (torch tensors or ints; None for unused); asynchronous."""
+        def ptr(t):
+            if t is None:
+                return ctypes.c_void_p(0)
+            return ctypes.c_void_p(t if isinstance(t, int) else t.data_ptr())
+        check(_lib.load().mkacc_eval_nand_device(self._h, ptr(d_nand), ptr(d_a1), ptr(d_b1), ptr(d_a2), ptr(d_b2),
+                                                 ptr(d_out_a), ptr(d_out_b), B))
+
+    def gate_tail(self, acc: np.ndarray):
+        """Extraction + ModSwitch + key switch of B accumulators [B][k][N] (EVAL)."""
+        self._need_ksk()
+        a = np.ascontiguousarray(acc, dtype=np.uint32)
+        B = a.shape[0]
+        oa = np.empty((B, self.k, self.ks.n_out), dtype=np.uint32)
+        ob = np.empty(B, dtype=np.uint32)
+        check(_lib.load().mkacc_gate_tail(self._h, _u32(a), _u32(oa), _u32(ob), B))
+        return oa if self.method == MKNTRU else (oa, ob)
 
     # -- primitives -------------------------------------------------------------
     def _prim(self, fn, a: np.ndarray, out_mul: int):

@@ -538,6 +538,14 @@ StepFn pick_step(int method, bool first) {
     return first ? mk_step_kernel<DG, XZW_B, true> : mk_step_kernel<DG, XZW_B, false>;
 }
 
+StepFn step_fn(int dg, int method, bool first);
+
+}  // namespace
+
+#include "mkacc_gate.hpp"
+
+namespace {
+
 StepFn step_fn(int dg, int method, bool first) {
     switch (dg) {
         case 2: return pick_step<2>(method, first);
@@ -577,6 +585,19 @@ struct mkacc_ctx {
     size_t io_B = 0;
     uint32_t* d_ct = nullptr;
     uint32_t* d_io = nullptr;
+    // gate head / tail (mkacc_gate.hpp)
+    mkacc_ks_params ks{};
+    uint32_t dks = 0, n_pad = 0;
+    bool have_ksk = false;
+    uint16_t* d_ksk = nullptr;     // MNTRU: [k][dks*N][n_pad], row l = t*N + j
+    uint16_t* d_lweA = nullptr;    // MK-LWE: [k][N][Bks][dks][n_out]
+    uint16_t* d_lweB = nullptr;    // MK-LWE: [k][N][Bks][dks]
+    uint32_t* d_tv = nullptr;      // test vector NTT(Rx) * N^-1, C4 [N]
+    size_t gate_B = 0;
+    uint8_t* d_digits = nullptr;   // [B][k][dks][N]
+    uint32_t* d_bh = nullptr;      // [B] MK-LWE rotation b
+    uint32_t* d_gin = nullptr;     // host API staging of gate inputs
+    uint32_t* d_gout = nullptr;
     std::mutex mu;
 };
 
@@ -606,22 +627,11 @@ int ensure_ws(mkacc_ctx* c, size_t B) {
     return MKACC_OK;
 }
 
-int launch_batch(mkacc_ctx* c, const uint32_t* d_ct, const uint32_t* d_in, uint32_t* d_out, size_t B) {
-    if (!c->have_keys) return fail(MKACC_E_NOKEYS, "Bootstrapping keys have not been generated/uploaded");
-    if (B == 0) return MKACC_OK;
-    int rc = ensure_ws(c, B);
-    if (rc) return rc;
+// The k*n accumulator steps over a batch whose monomial exponents are in
+// d_cvals and whose C4 accumulators are in d_acc0; returns the buffer holding
+// the result.
+uint32_t* launch_steps(mkacc_ctx* c, size_t B) {
     const uint32_t k = c->p.k, n = c->p.n;
-    const size_t npoly = B * k;
-    const int tpb = 256;
-    {
-        const size_t tot = B * (size_t)k * n;
-        hipLaunchKernelGGL(prep_c_kernel, dim3((unsigned)((tot + tpb - 1) / tpb)), dim3(tpb), 0, c->stream, d_ct,
-                           c->d_cvals, (uint32_t)B, k * n, (uint32_t)c->method_class, (uint32_t)c->p.q);
-        const size_t tw = npoly * kN;
-        hipLaunchKernelGGL(eval_to_c4_kernel, dim3((unsigned)((tw + tpb - 1) / tpb)), dim3(tpb), 0, c->stream, d_in,
-                           c->d_acc0, npoly, c->ninv, c->ninvp, c->mod.Q);
-    }
     uint32_t* cur = c->d_acc0;
     uint32_t* nxt = c->d_acc1;
     const dim3 grid((unsigned)((B + kWavesPerBlock - 1) / kWavesPerBlock)), block(kThreads);
@@ -650,11 +660,142 @@ int launch_batch(mkacc_ctx* c, const uint32_t* d_ct, const uint32_t* d_in, uint3
             std::swap(cur, nxt);
         }
     }
+    return cur;
+}
+
+void launch_prep_c(mkacc_ctx* c, const uint32_t* d_ct, size_t B) {
+    const size_t tot = B * (size_t)c->p.k * c->p.n;
+    hipLaunchKernelGGL(prep_c_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, c->stream, d_ct,
+                       c->d_cvals, (uint32_t)B, c->p.k * c->p.n, (uint32_t)c->method_class, (uint32_t)c->p.q);
+}
+
+int launch_batch(mkacc_ctx* c, const uint32_t* d_ct, const uint32_t* d_in, uint32_t* d_out, size_t B) {
+    if (!c->have_keys) return fail(MKACC_E_NOKEYS, "Bootstrapping keys have not been generated/uploaded");
+    if (B == 0) return MKACC_OK;
+    int rc = ensure_ws(c, B);
+    if (rc) return rc;
+    const size_t npoly = B * c->p.k;
+    const int tpb = 256;
+    launch_prep_c(c, d_ct, B);
+    {
+        const size_t tw = npoly * kN;
+        hipLaunchKernelGGL(eval_to_c4_kernel, dim3((unsigned)((tw + tpb - 1) / tpb)), dim3(tpb), 0, c->stream, d_in,
+                           c->d_acc0, npoly, c->ninv, c->ninvp, c->mod.Q);
+    }
+    uint32_t* cur = launch_steps(c, B);
     {
         const size_t tw = npoly * kN;
         hipLaunchKernelGGL(c4_to_eval_kernel, dim3((unsigned)((tw + tpb - 1) / tpb)), dim3(tpb), 0, c->stream, cur,
                            d_out, npoly, c->nval, c->nvalp, c->mod.Q);
     }
+    HIP_TRY(hipGetLastError());
+    return MKACC_OK;
+}
+
+// ---- gate level (head + EvalAcc + tail) -------------------------------------------
+
+int ensure_gate_ws(mkacc_ctx* c, size_t B) {
+    int rc = ensure_ws(c, B);
+    if (rc) return rc;
+    if (B <= c->gate_B) return MKACC_OK;
+    if (c->d_digits) HIP_TRY(hipFree(c->d_digits));
+    if (c->d_bh) HIP_TRY(hipFree(c->d_bh));
+    c->d_digits = nullptr;
+    c->d_bh = nullptr;
+    c->gate_B = 0;
+    HIP_TRY(hipMalloc(&c->d_digits, B * c->p.k * (size_t)c->dks * kN));
+    HIP_TRY(hipMalloc(&c->d_bh, B * 4));
+    c->gate_B = B;
+    return MKACC_OK;
+}
+
+// Test vector of BootstrapGateCore (binfhe-base-scheme.cpp:1093-1115 MNTRU,
+// :1017-1021 MK-LWE; plaintext modulus p = 4, mntru-ciphertext.h:30), NTT'd on
+// the device and stored C4 * N^-1.
+int ensure_test_vector(mkacc_ctx* c) {
+    if (c->d_tv) return MKACC_OK;
+    const uint64_t Q = c->p.Q, p = 4, Q2p = Q / (2 * p) + 1, Q2pNeg = Q - Q2p;
+    std::vector<uint32_t> rx(kN);
+    for (uint32_t j = 0; j < (uint32_t)kN; ++j) {
+        const bool lo = j < (uint32_t)kN / 2;
+        rx[j] = (uint32_t)(c->method_class == XZW ? (lo ? Q2pNeg : Q2p) : (lo ? Q2p : Q2pNeg));
+    }
+    uint32_t *din = nullptr, *dev = nullptr;
+    HIP_TRY(hipMalloc(&din, kN * 4));
+    HIP_TRY(hipMalloc(&dev, kN * 4));
+    HIP_TRY(hipMalloc(&c->d_tv, kN * 4));
+    HIP_TRY(hipMemcpyAsync(din, rx.data(), kN * 4, hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(ntt_fwd_kernel, dim3(1), dim3(kThreads), kStepLdsBytes, c->stream, din, dev, 1u, c->d_img,
+                       c->d_twf, c->mod.Q);
+    hipLaunchKernelGGL(eval_to_c4_kernel, dim3(kN / 256), dim3(256), 0, c->stream, dev, c->d_tv, (size_t)1, c->ninv,
+                       c->ninvp, c->mod.Q);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipFree(din));
+    HIP_TRY(hipFree(dev));
+    return MKACC_OK;
+}
+
+TailConsts tail_consts(const mkacc_ctx* c) {
+    return TailConsts{c->mod.Q, (uint32_t)c->ks.qKS, c->ks.baseKS, c->dks};
+}
+
+const uint2* psi_image(const mkacc_ctx* c) { return reinterpret_cast<const uint2*>(c->d_img) + 2 * kTwlPairs; }
+
+// tail on the C4 accumulators `acc`: extraction + ModSwitch + digits, then the
+// method's key switch into out_a (and out_b for MK-LWE)
+void launch_tail(mkacc_ctx* c, const uint32_t* acc, uint32_t* out_a, uint32_t* out_b, size_t B) {
+    const uint32_t k = c->p.k;
+    const uint32_t npoly = (uint32_t)(B * k);
+    const uint2* twl_inv = reinterpret_cast<const uint2*>(c->d_img) + kTwlPairs;
+    hipLaunchKernelGGL(extract_kernel, dim3((npoly + 3) / 4), dim3(256), 0, c->stream, acc, c->d_digits, npoly,
+                       c->d_twi, twl_inv, tail_consts(c));
+    const uint32_t L = c->dks * kN;
+    if (c->method_class == XZW) {
+        const uint32_t qinv = (uint32_t)((1ull << 32) / c->ks.qKS);
+        const dim3 grid(c->n_pad / kKsTile, (unsigned)((B + kKsTile - 1) / kKsTile), k);
+        hipLaunchKernelGGL(ks_mntru_kernel, grid, dim3(256), 0, c->stream, c->d_digits, c->d_ksk, out_a,
+                           (uint32_t)B, k, L, c->ks.n_out, c->n_pad, (uint32_t)c->ks.qKS, qinv);
+    } else {
+        const uint32_t b0 = round_qQ_host((c->p.Q >> 3) + 1, c->ks.qKS, c->p.Q);
+        hipLaunchKernelGGL(ks_mklwe_kernel, dim3((unsigned)B), dim3(256), 0, c->stream, c->d_digits, c->d_lweA,
+                           c->d_lweB, out_a, out_b, k, c->ks.n_out, c->ks.baseKS, c->dks, (uint32_t)c->ks.qKS, b0);
+    }
+}
+
+// full NAND gates on device buffers
+int launch_gates(mkacc_ctx* c, const uint32_t* d_nand, const uint32_t* d_a1, const uint32_t* d_b1,
+                 const uint32_t* d_a2, const uint32_t* d_b2, uint32_t* d_out_a, uint32_t* d_out_b, size_t B) {
+    if (!c->have_keys) return fail(MKACC_E_NOKEYS, "Bootstrapping keys have not been generated. Please call MKBTKeyGen before calling bootstrapping.");
+    if (!c->have_ksk) return fail(MKACC_E_NOKEYS, "Key-switching keys have not been uploaded");
+    if (B == 0) return MKACC_OK;
+    int rc = ensure_gate_ws(c, B);
+    if (!rc) rc = ensure_test_vector(c);
+    if (rc) return rc;
+    const uint32_t k = c->p.k, kn = k * c->p.n;
+    const size_t tot = B * (size_t)kn;
+    // head: the raw accumulator exponents go through d_ct
+    if (B > c->io_B) {
+        if (c->d_ct) HIP_TRY(hipFree(c->d_ct));
+        if (c->d_io) HIP_TRY(hipFree(c->d_io));
+        c->d_ct = c->d_io = nullptr;
+        c->io_B = 0;
+        HIP_TRY(hipMalloc(&c->d_ct, tot * 4));
+        HIP_TRY(hipMalloc(&c->d_io, B * k * (size_t)kN * 4));
+        c->io_B = B;
+    }
+    const unsigned g1 = (unsigned)((tot + 255) / 256);
+    if (c->method_class == XZW)
+        hipLaunchKernelGGL(mntru_head_kernel, dim3(g1), dim3(256), 0, c->stream, d_nand, d_a1, d_a2, c->d_ct,
+                           (uint32_t)B, kn, (uint32_t)c->p.q);
+    else
+        hipLaunchKernelGGL(mklwe_head_kernel, dim3(g1), dim3(256), 0, c->stream, d_a1, d_b1, d_a2, d_b2, c->d_ct,
+                           c->d_bh, (uint32_t)B, kn, (uint32_t)c->p.q);
+    launch_prep_c(c, c->d_ct, B);
+    const size_t tw = B * k * (size_t)kN;
+    hipLaunchKernelGGL(acc_init_kernel, dim3((unsigned)((tw + 255) / 256)), dim3(256), 0, c->stream, c->d_acc0,
+                       c->d_tv, c->method_class == XZW ? nullptr : c->d_bh, psi_image(c), (uint32_t)B, k, c->mod.Q);
+    uint32_t* cur = launch_steps(c, B);
+    launch_tail(c, cur, d_out_a, d_out_b, B);
     HIP_TRY(hipGetLastError());
     return MKACC_OK;
 }
@@ -868,7 +1009,9 @@ void mkacc_destroy(mkacc_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (void* p : {(void*)c->d_twf, (void*)c->d_twi, (void*)c->d_img, (void*)c->d_keys, (void*)c->d_pkey,
-                    (void*)c->d_acc0, (void*)c->d_acc1, (void*)c->d_cvals, (void*)c->d_sumv, (void*)c->d_ct, (void*)c->d_io})
+                    (void*)c->d_acc0, (void*)c->d_acc1, (void*)c->d_cvals, (void*)c->d_sumv, (void*)c->d_ct,
+                    (void*)c->d_io, (void*)c->d_ksk, (void*)c->d_lweA, (void*)c->d_lweB, (void*)c->d_tv,
+                    (void*)c->d_digits, (void*)c->d_bh, (void*)c->d_gin, (void*)c->d_gout})
         if (p) (void)hipFree(p);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -931,6 +1074,183 @@ int mkacc_eval_batch_device(mkacc_ctx* c, const uint32_t* d_ct, const uint32_t* 
     std::lock_guard<std::mutex> g(c->mu);
     HIP_TRY(hipSetDevice(c->device));
     return launch_batch(c, d_ct, d_in, d_out, B);
+}
+
+uint32_t mkacc_ks_digits(const mkacc_ks_params* ks) {
+    if (!ks || ks->qKS < 2 || ks->baseKS < 2) return 0;
+    return ks_digit_count(ks->qKS, ks->baseKS);
+}
+
+namespace {
+int check_ks(mkacc_ctx* c, const mkacc_ks_params* ks) {
+    if (!ks) return fail(MKACC_E_ARG, "null key-switching parameters");
+    if (ks->qKS < 2 || ks->qKS > 65535) return fail(MKACC_E_UNSUPPORTED, "engine supports qKS < 2^16");
+    if (ks->baseKS < 2 || ks->baseKS > 256) return fail(MKACC_E_UNSUPPORTED, "engine supports baseKS <= 256");
+    if (ks->n_out == 0 || ks->n_out > 4096) return fail(MKACC_E_ARG, "bad output dimension");
+    c->ks = *ks;
+    c->dks = ks_digit_count(ks->qKS, ks->baseKS);
+    c->n_pad = (ks->n_out + kKsTile - 1) / kKsTile * kKsTile;
+    return MKACC_OK;
+}
+}  // namespace
+
+int mkacc_upload_ksk_mntru(mkacc_ctx* c, const mkacc_ks_params* ks, const uint32_t* ksk) {
+    if (!c || !ksk) return fail(MKACC_E_ARG, "null argument");
+    std::lock_guard<std::mutex> g(c->mu);
+    if (c->method_class != XZW) return fail(MKACC_E_ARG, "KeySwitch2 keys belong to the MKNTRU method");
+    int rc = check_ks(c, ks);
+    if (rc) return rc;
+    const uint32_t k = c->p.k, dks = c->dks, n = ks->n_out, npad = c->n_pad;
+    const size_t L = (size_t)dks * kN;
+    // reference row l = j*dks + t  ->  device row t*N + j, columns padded to n_pad
+    std::vector<uint16_t> h((size_t)k * L * npad, 0);
+    for (uint32_t u = 0; u < k; ++u)
+        for (uint32_t j = 0; j < (uint32_t)kN; ++j)
+            for (uint32_t t = 0; t < dks; ++t) {
+                const uint32_t* src = ksk + (((size_t)u * kN + j) * dks + t) * n;
+                uint16_t* dst = h.data() + ((size_t)u * L + (size_t)t * kN + j) * npad;
+                for (uint32_t i = 0; i < n; ++i) {
+                    if (src[i] >= ks->qKS) return fail(MKACC_E_RANGE, "ksk word not a canonical residue mod qKS");
+                    dst[i] = (uint16_t)src[i];
+                }
+            }
+    HIP_TRY(hipSetDevice(c->device));
+    if (c->d_ksk) HIP_TRY(hipFree(c->d_ksk));
+    c->d_ksk = nullptr;
+    HIP_TRY(hipMalloc(&c->d_ksk, h.size() * 2));
+    HIP_TRY(hipMemcpy(c->d_ksk, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+    c->have_ksk = true;
+    return MKACC_OK;
+}
+
+int mkacc_upload_ksk_mklwe(mkacc_ctx* c, const mkacc_ks_params* ks, const uint32_t* A, const uint32_t* B) {
+    if (!c || !A || !B) return fail(MKACC_E_ARG, "null argument");
+    std::lock_guard<std::mutex> g(c->mu);
+    if (c->method_class != XZW_B) return fail(MKACC_E_ARG, "MK-LWE KeySwitch keys belong to the MKNTRU_LWE method");
+    int rc = check_ks(c, ks);
+    if (rc) return rc;
+    const size_t rows = (size_t)c->p.k * kN * ks->baseKS * c->dks;
+    std::vector<uint16_t> ha(rows * ks->n_out), hb(rows);
+    for (size_t i = 0; i < ha.size(); ++i) {
+        if (A[i] >= ks->qKS) return fail(MKACC_E_RANGE, "A word not a canonical residue mod qKS");
+        ha[i] = (uint16_t)A[i];
+    }
+    for (size_t i = 0; i < rows; ++i) {
+        if (B[i] >= ks->qKS) return fail(MKACC_E_RANGE, "B word not a canonical residue mod qKS");
+        hb[i] = (uint16_t)B[i];
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    if (c->d_lweA) HIP_TRY(hipFree(c->d_lweA));
+    if (c->d_lweB) HIP_TRY(hipFree(c->d_lweB));
+    c->d_lweA = nullptr;
+    c->d_lweB = nullptr;
+    HIP_TRY(hipMalloc(&c->d_lweA, ha.size() * 2));
+    HIP_TRY(hipMalloc(&c->d_lweB, hb.size() * 2));
+    HIP_TRY(hipMemcpy(c->d_lweA, ha.data(), ha.size() * 2, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c->d_lweB, hb.data(), hb.size() * 2, hipMemcpyHostToDevice));
+    c->have_ksk = true;
+    return MKACC_OK;
+}
+
+namespace {
+// host-buffer gate staging: [ct_nand | a1 | a2 | b1 | b2] in, [out_a | out_b] out
+int gate_host(mkacc_ctx* c, const uint32_t* nand, const uint32_t* a1, const uint32_t* b1, const uint32_t* a2,
+              const uint32_t* b2, uint32_t* out_a, uint32_t* out_b, size_t B) {
+    const bool lwe = c->method_class == XZW_B;
+    const size_t kn = (size_t)c->p.k * c->p.n, kno = (size_t)c->p.k * c->ks.n_out;
+    const uint64_t q = c->p.q;
+    for (size_t i = 0; i < B * kn; ++i)
+        if (a1[i] >= q || a2[i] >= q) return fail(MKACC_E_RANGE, "ciphertext word not a canonical residue mod q");
+    if (!lwe)
+        for (size_t i = 0; i < kn; ++i)
+            if (nand[i] >= q) return fail(MKACC_E_RANGE, "ctNAND word not a canonical residue mod q");
+    if (lwe)
+        for (size_t i = 0; i < B; ++i)
+            if (b1[i] >= q || b2[i] >= q) return fail(MKACC_E_RANGE, "ciphertext b not a canonical residue mod q");
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t in_words = kn + 2 * B * kn + 2 * B, out_words = B * kno + B;
+    if (c->d_gin) HIP_TRY(hipFree(c->d_gin));
+    if (c->d_gout) HIP_TRY(hipFree(c->d_gout));
+    c->d_gin = c->d_gout = nullptr;
+    HIP_TRY(hipMalloc(&c->d_gin, in_words * 4));
+    HIP_TRY(hipMalloc(&c->d_gout, out_words * 4));
+    uint32_t* dn = c->d_gin;
+    uint32_t* d1 = dn + kn;
+    uint32_t* d2 = d1 + B * kn;
+    uint32_t* db1 = d2 + B * kn;
+    uint32_t* db2 = db1 + B;
+    if (!lwe) HIP_TRY(hipMemcpyAsync(dn, nand, kn * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(d1, a1, B * kn * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(d2, a2, B * kn * 4, hipMemcpyHostToDevice, c->stream));
+    if (lwe) {
+        HIP_TRY(hipMemcpyAsync(db1, b1, B * 4, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(db2, b2, B * 4, hipMemcpyHostToDevice, c->stream));
+    }
+    int rc = launch_gates(c, dn, d1, db1, d2, db2, c->d_gout, c->d_gout + B * kno, B);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(out_a, c->d_gout, B * kno * 4, hipMemcpyDeviceToHost, c->stream));
+    if (lwe) HIP_TRY(hipMemcpyAsync(out_b, c->d_gout + B * kno, B * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return MKACC_OK;
+}
+}  // namespace
+
+int mkacc_eval_nand_mntru(mkacc_ctx* c, const uint32_t* ct_nand, const uint32_t* ct1, const uint32_t* ct2,
+                          uint32_t* out, size_t B) {
+    if (!c || !ct_nand || !ct1 || !ct2 || !out) return fail(MKACC_E_ARG, "null argument");
+    std::lock_guard<std::mutex> g(c->mu);
+    if (c->method_class != XZW) return fail(MKACC_E_ARG, "method is not MKNTRU");
+    if (ct1 == ct2) return fail(MKACC_E_ARG, "Input ciphertexts should be independant");
+    if (B == 0) return MKACC_OK;
+    return gate_host(c, ct_nand, ct1, nullptr, ct2, nullptr, out, nullptr, B);
+}
+
+int mkacc_eval_nand_mklwe(mkacc_ctx* c, const uint32_t* a1, const uint32_t* b1, const uint32_t* a2,
+                          const uint32_t* b2, uint32_t* out_a, uint32_t* out_b, size_t B) {
+    if (!c || !a1 || !b1 || !a2 || !b2 || !out_a || !out_b) return fail(MKACC_E_ARG, "null argument");
+    std::lock_guard<std::mutex> g(c->mu);
+    if (c->method_class != XZW_B) return fail(MKACC_E_ARG, "method is not MKNTRU_LWE / MKNTRU_B");
+    if (a1 == a2) return fail(MKACC_E_ARG, "Input ciphertexts should be independant");
+    if (B == 0) return MKACC_OK;
+    return gate_host(c, nullptr, a1, b1, a2, b2, out_a, out_b, B);
+}
+
+int mkacc_eval_nand_device(mkacc_ctx* c, const uint32_t* d_ct_nand, const uint32_t* d_a1, const uint32_t* d_b1,
+                           const uint32_t* d_a2, const uint32_t* d_b2, uint32_t* d_out_a, uint32_t* d_out_b,
+                           size_t B) {
+    if (!c || !d_a1 || !d_a2 || !d_out_a) return fail(MKACC_E_ARG, "null argument");
+    std::lock_guard<std::mutex> g(c->mu);
+    if (c->method_class == XZW && !d_ct_nand) return fail(MKACC_E_ARG, "null ctNAND");
+    if (c->method_class == XZW_B && (!d_b1 || !d_b2 || !d_out_b)) return fail(MKACC_E_ARG, "null b");
+    HIP_TRY(hipSetDevice(c->device));
+    return launch_gates(c, d_ct_nand, d_a1, d_b1, d_a2, d_b2, d_out_a, d_out_b, B);
+}
+
+int mkacc_gate_tail(mkacc_ctx* c, const uint32_t* acc, uint32_t* out_a, uint32_t* out_b, size_t B) {
+    if (!c || !acc || !out_a || (c->method_class == XZW_B && !out_b)) return fail(MKACC_E_ARG, "null argument");
+    std::lock_guard<std::mutex> g(c->mu);
+    if (!c->have_ksk) return fail(MKACC_E_NOKEYS, "Key-switching keys have not been uploaded");
+    if (B == 0) return MKACC_OK;
+    const size_t npoly = B * c->p.k, kno = (size_t)c->p.k * c->ks.n_out;
+    for (size_t i = 0; i < npoly * kN; ++i)
+        if (acc[i] >= c->p.Q) return fail(MKACC_E_RANGE, "accumulator word not a canonical residue mod Q");
+    HIP_TRY(hipSetDevice(c->device));
+    int rc = ensure_gate_ws(c, B);
+    if (rc) return rc;
+    uint32_t *din = nullptr, *dout = nullptr;
+    HIP_TRY(hipMalloc(&din, npoly * kN * 4));
+    HIP_TRY(hipMalloc(&dout, (B * kno + B) * 4));
+    HIP_TRY(hipMemcpyAsync(din, acc, npoly * kN * 4, hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(eval_to_c4_kernel, dim3((unsigned)((npoly * kN + 255) / 256)), dim3(256), 0, c->stream, din,
+                       c->d_acc0, npoly, c->ninv, c->ninvp, c->mod.Q);
+    launch_tail(c, c->d_acc0, dout, dout + B * kno, B);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(out_a, dout, B * kno * 4, hipMemcpyDeviceToHost, c->stream));
+    if (out_b) HIP_TRY(hipMemcpyAsync(out_b, dout + B * kno, B * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipFree(din));
+    HIP_TRY(hipFree(dout));
+    return MKACC_OK;
 }
 
 int mkacc_sync(mkacc_ctx* c) {

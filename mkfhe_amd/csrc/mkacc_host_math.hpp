@@ -31,6 +31,15 @@ inline uint64_t modinv(uint64_t a, uint64_t Q) {
     if (t < 0) t += Q;
     return (uint64_t)t;
 }
+// RoundqQ (mntru-pke.cpp:11-16): floor(0.5 + v*q/Q) in IEEE double, mod q
+inline uint32_t round_qQ_host(uint64_t v, uint64_t q, uint64_t Q) {
+    const double x = std::floor(0.5 + (double)v * (double)q / (double)Q);
+    return (uint32_t)((uint64_t)x % q);
+}
+// digitCount of KeySwitch2 / KeySwitch: ceil(log qKS / log baseKS)  (mntru-pke.cpp:771)
+inline uint32_t ks_digit_count(uint64_t qKS, uint32_t baseKS) {
+    return (uint32_t)std::ceil(std::log((double)qKS) / std::log((double)baseKS));
+}
 inline uint32_t bit_reverse(uint32_t x, uint32_t bits) {
     uint32_t r = 0;
     for (uint32_t i = 0; i < bits; ++i) r |= ((x >> i) & 1u) << (bits - 1 - i);

@@ -517,3 +517,144 @@ void orc_mntru_testvector(const orc_ctx* c, uint64_t p, uint64_t* acc) {
     for (uint32_t j = 0; j < N; ++j) acc[j] = j < N / 2 ? Q2pNeg : Q2p;
     ntt_fwd_tab(acc, N, Q, c->tab);
 }
+
+/* ------------------------------------------------------------------------ */
+/* Gate head and tail                                */
+/* ------------------------------------------------------------------------ */
+
+/* MNTRUEncryptionScheme::RoundqQ (mntru-pke.cpp:11-16) and the identical
+ * MKLWEEncryptionScheme::RoundqQ: floor(0.5 + v * q / Q) in IEEE double,
+ * left to right, then Mod(q). */
+uint64_t orc_round_qQ(uint64_t v, uint64_t q, uint64_t Q) {
+    double x = floor(0.5 + (double)v * (double)q / (double)Q);
+    return ((uint64_t)x) % q;
+}
+
+/* MNTRU gate head, BinFHEScheme::EvalBinGate (binfhe-base-scheme.cpp:478-490):
+ * ct_temp = ctNAND - (ct1 + ct2), element-wise mod q (EvalAddEq / EvalSubEq,
+ * mntru-pke.cpp:826-838).  All arrays [k][n]. */
+void orc_mntru_head(const uint64_t* ctNAND, const uint64_t* ct1, const uint64_t* ct2, uint64_t* out,
+                    uint32_t k, uint32_t n, uint64_t q) {
+    for (size_t i = 0; i < (size_t)k * n; ++i) out[i] = submod(ctNAND[i], addmod(ct1[i], ct2[i], q), q);
+}
+
+/* Extraction (binfhe-base-scheme.cpp:498-506 / :441-449): per party
+ * accVec[u] = accVec[u].Transpose() then SetFormat(COEFFICIENT).
+ * acc [k][N] EVAL -> out [k][N] COEFFICIENT. */
+void orc_extract(const orc_ctx* c, const uint64_t* acc, uint64_t* out) {
+    const uint32_t N = c->p.N;
+    for (uint32_t u = 0; u < c->p.k; ++u) {
+        orc_transpose_eval(acc + (size_t)u * N, out + (size_t)u * N, N);
+        ntt_inv_tab(out + (size_t)u * N, N, c->p.Q, c->tabI, c->Ninv);
+    }
+}
+
+static uint32_t ks_digits(uint64_t qKS, uint32_t baseKS) {
+    /* static_cast<size_t>(std::ceil(log(qKS) / log(baseKS)))  (mntru-pke.cpp:771, mklwe-pke.cpp:266) */
+    return (uint32_t)ceil(log((double)qKS) / log((double)baseKS));
+}
+uint32_t orc_ks_digits(uint64_t qKS, uint32_t baseKS) { return ks_digits(qKS, baseKS); }
+
+/* MNTRUEncryptionScheme::KeySwitch2 (mntru-pke.cpp:763-823).
+ *   ksk2 [k][Bks][N*dks][n] mod qKS (KSK2 of KeySwitchGen2, mntru-pke.cpp:744-755)
+ *   ct   [k][N] mod qKS (ModSwitch output)
+ *   out  [k][n] mod qKS                                                      */
+void orc_keyswitch2(const uint64_t* ksk2, const uint64_t* ct, uint64_t* out, uint32_t k, uint32_t N, uint32_t n,
+                    uint64_t qKS, uint32_t baseKS) {
+    const uint32_t dks = ks_digits(qKS, baseKS);
+    const size_t L = (size_t)N * dks;
+    uint32_t* hat = (uint32_t*)malloc(L * sizeof(uint32_t));
+    for (uint32_t u = 0; u < k; ++u) {
+        for (uint32_t i = 0; i < N; ++i) {
+            uint64_t t = ct[(size_t)u * N + i];
+            for (uint32_t j = 0; j < dks; ++j) {
+                hat[(size_t)i * dks + j] = (uint32_t)(t % baseKS);
+                t /= baseKS;
+            }
+        }
+        uint64_t* c = out + (size_t)u * n;
+        memset(c, 0, n * sizeof(uint64_t));
+        for (size_t l = 0; l < L; ++l) {
+            const uint32_t index = hat[l];
+            if (index == 0) continue;
+            const uint64_t* row = ksk2 + (((size_t)u * baseKS + index) * L + l) * n;
+            for (uint32_t i = 0; i < n; ++i) c[i] = addmod(c[i], row[i], qKS);
+        }
+    }
+    free(hat);
+}
+
+/* Full MNTRU NAND gate after EvalAcc: extraction, ModSwitch(qKS)
+ * (mntru-pke.cpp:359-374), KeySwitch2.  acc [k][N] EVAL -> out [k][n]. */
+void orc_mntru_tail(const orc_ctx* c, const uint64_t* acc, const uint64_t* ksk2, uint64_t qKS, uint32_t baseKS,
+                    uint32_t n_out, uint64_t* out) {
+    const uint32_t N = c->p.N, k = c->p.k;
+    uint64_t* ext = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)k * N);
+    orc_extract(c, acc, ext);
+    for (size_t i = 0; i < (size_t)k * N; ++i) ext[i] = orc_round_qQ(ext[i], qKS, c->p.Q);
+    orc_keyswitch2(ksk2, ext, out, k, N, n_out, qKS, baseKS);
+    free(ext);
+}
+
+/* MK-LWE gate head (binfhe-base-scheme.cpp:380-406, 1004-1065):
+ *   ct_temp = (0, 5q/8) - (ct1 + ct2) mod q; ModSwitch to 2N (mklwe-pke.cpp:160-174);
+ *   acc[0] = NTT(X^b * Rx), Rx[j] = j < N/2 ? Q/8+1 : Q - (Q/8+1)  (:1017-1043);
+ *   c = GetAneg() = -a mod 2N (mklwe-ciphertext.h:86-96).
+ * a1, a2 [k][n] mod q; outputs c [k][n] in [0, 2N], acc [k][N] EVAL. */
+void orc_mklwe_head(const orc_ctx* c, const uint64_t* a1, uint64_t b1, const uint64_t* a2, uint64_t b2, uint64_t q,
+                    uint32_t n, uint64_t p, uint64_t* cout, uint64_t* acc) {
+    const uint32_t N = c->p.N, k = c->p.k;
+    const uint64_t M = 2ull * N, Q = c->p.Q;
+    const uint64_t b_tmp = submod((5 * q / 8) % q, addmod(b1, b2, q), q);
+    const uint64_t bms = orc_round_qQ(b_tmp, M, q);
+    for (size_t i = 0; i < (size_t)k * n; ++i) {
+        const uint64_t at = submod(0, addmod(a1[i], a2[i], q), q);
+        const uint64_t ams = orc_round_qQ(at, M, q);
+        cout[i] = ams == 0 ? 0 : M - ams;              /* zero.ModSub(a) mod 2N */
+    }
+    const uint64_t Q2p = Q / (2 * p) + 1, Q2pNeg = Q - Q2p;
+    const uint64_t bhat = bms * M / M;                 /* b*2N/q with q = 2N (:1026) */
+    memset(acc, 0, sizeof(uint64_t) * (size_t)k * N);
+    for (uint32_t j = 0; j < N; ++j) {
+        const uint64_t rx = j < N / 2 ? Q2p : Q2pNeg;
+        const uint64_t index = bhat + j;
+        if (index >= N && index < 2ull * N) acc[index % N] = Q - rx;
+        else acc[index % N] = rx;
+    }
+    ntt_fwd_tab(acc, N, Q, c->tab);
+}
+
+/* MKLWEEncryptionScheme::KeySwitch (mklwe-pke.cpp:260-298).
+ *   A [k][N][Bks][dks][n], B [k][N][Bks][dks] mod qKS; a [k][N], b mod qKS.
+ *   out_a [k][n], *out_b.                                                    */
+void orc_mklwe_keyswitch(const uint64_t* A, const uint64_t* Bk, const uint64_t* a, uint64_t b, uint64_t* out_a,
+                         uint64_t* out_b, uint32_t k, uint32_t N, uint32_t n, uint64_t qKS, uint32_t baseKS) {
+    const uint32_t dks = ks_digits(qKS, baseKS);
+    memset(out_a, 0, sizeof(uint64_t) * (size_t)k * n);
+    for (uint32_t u = 0; u < k; ++u)
+        for (uint32_t i = 0; i < N; ++i) {
+            uint64_t t = a[(size_t)u * N + i];
+            for (uint32_t j = 0; j < dks; ++j) {
+                const uint64_t a0 = t % baseKS;
+                t /= baseKS;
+                const size_t e = (((size_t)u * N + i) * baseKS + a0) * dks + j;
+                b = submod(b, Bk[e], qKS);
+                const uint64_t* row = A + e * n;
+                for (uint32_t l = 0; l < n; ++l) out_a[(size_t)u * n + l] = submod(out_a[(size_t)u * n + l], row[l], qKS);
+            }
+        }
+    *out_b = b;
+}
+
+/* MK-LWE gate tail: extraction, b = Q/8 + 1 (binfhe-base-scheme.cpp:451),
+ * ModSwitch(qKS), KeySwitch.  acc [k][N] EVAL -> out_a [k][n], *out_b. */
+void orc_mklwe_tail(const orc_ctx* c, const uint64_t* acc, const uint64_t* A, const uint64_t* Bk, uint64_t qKS,
+                    uint32_t baseKS, uint32_t n_out, uint64_t* out_a, uint64_t* out_b) {
+    const uint32_t N = c->p.N, k = c->p.k;
+    uint64_t* ext = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)k * N);
+    orc_extract(c, acc, ext);
+    for (size_t i = 0; i < (size_t)k * N; ++i) ext[i] = orc_round_qQ(ext[i], qKS, c->p.Q);
+    const uint64_t b = orc_round_qQ((c->p.Q >> 3) + 1, qKS, c->p.Q);
+    orc_mklwe_keyswitch(A, Bk, ext, b, out_a, out_b, k, N, n_out, qKS, baseKS);
+    free(ext);
+}

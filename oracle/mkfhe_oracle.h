@@ -96,6 +96,24 @@ void orc_fill_uniform_u32(uint32_t* out, size_t n, uint64_t bound, uint64_t seed
 /* BootstrapGateCore MNTRU test vector (binfhe-base-scheme.cpp:1093-1115): acc[0] = NTT(Rx), acc[u>0] = 0 */
 void orc_mntru_testvector(const orc_ctx* c, uint64_t p, uint64_t* acc);
 
+
+/* ---- gate head / tail (binfhe-base-scheme.cpp:380-515, mntru-pke.cpp, mklwe-pke.cpp) ---- */
+uint64_t orc_round_qQ(uint64_t v, uint64_t q, uint64_t Q);          /* RoundqQ, mntru-pke.cpp:11-16 */
+uint32_t orc_ks_digits(uint64_t qKS, uint32_t baseKS);                 /* ceil(log qKS / log baseKS) */
+void orc_mntru_head(const uint64_t* ctNAND, const uint64_t* ct1, const uint64_t* ct2, uint64_t* out,
+                    uint32_t k, uint32_t n, uint64_t q);
+void orc_extract(const orc_ctx* c, const uint64_t* acc, uint64_t* out);
+void orc_keyswitch2(const uint64_t* ksk2, const uint64_t* ct, uint64_t* out, uint32_t k, uint32_t N, uint32_t n,
+                    uint64_t qKS, uint32_t baseKS);
+void orc_mntru_tail(const orc_ctx* c, const uint64_t* acc, const uint64_t* ksk2, uint64_t qKS, uint32_t baseKS,
+                    uint32_t n_out, uint64_t* out);
+void orc_mklwe_head(const orc_ctx* c, const uint64_t* a1, uint64_t b1, const uint64_t* a2, uint64_t b2, uint64_t q,
+                    uint32_t n, uint64_t p, uint64_t* cout, uint64_t* acc);
+void orc_mklwe_keyswitch(const uint64_t* A, const uint64_t* Bk, const uint64_t* a, uint64_t b, uint64_t* out_a,
+                         uint64_t* out_b, uint32_t k, uint32_t N, uint32_t n, uint64_t qKS, uint32_t baseKS);
+void orc_mklwe_tail(const orc_ctx* c, const uint64_t* acc, const uint64_t* A, const uint64_t* Bk, uint64_t qKS,
+                    uint32_t baseKS, uint32_t n_out, uint64_t* out_a, uint64_t* out_b);
+
 #ifdef __cplusplus
 }
 #endif

@@ -78,6 +78,22 @@ def lib():
         L.orc_evalacc_batch.restype = ctypes.c_int
         L.orc_evalacc_batch.argtypes = [ctypes.c_void_p, _u64p, _u64p, _u64p, _u64p, ctypes.c_size_t, ctypes.c_int]
         L.orc_fill_uniform.argtypes = [_u64p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64]
+        L.orc_round_qQ.restype = ctypes.c_uint64
+        L.orc_round_qQ.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]
+        L.orc_ks_digits.restype = ctypes.c_uint32
+        L.orc_ks_digits.argtypes = [ctypes.c_uint64, ctypes.c_uint32]
+        L.orc_mntru_head.argtypes = [_u64p, _u64p, _u64p, _u64p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]
+        L.orc_extract.argtypes = [ctypes.c_void_p, _u64p, _u64p]
+        L.orc_keyswitch2.argtypes = [_u64p, _u64p, _u64p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                     ctypes.c_uint64, ctypes.c_uint32]
+        L.orc_mntru_tail.argtypes = [ctypes.c_void_p, _u64p, _u64p, ctypes.c_uint64, ctypes.c_uint32,
+                                     ctypes.c_uint32, _u64p]
+        L.orc_mklwe_head.argtypes = [ctypes.c_void_p, _u64p, ctypes.c_uint64, _u64p, ctypes.c_uint64,
+                                     ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, _u64p, _u64p]
+        L.orc_mklwe_keyswitch.argtypes = [_u64p, _u64p, _u64p, ctypes.c_uint64, _u64p, _u64p, ctypes.c_uint32,
+                                          ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32]
+        L.orc_mklwe_tail.argtypes = [ctypes.c_void_p, _u64p, _u64p, _u64p, ctypes.c_uint64, ctypes.c_uint32,
+                                     ctypes.c_uint32, _u64p, _u64p]
         L.orc_fill_uniform_u32.argtypes = [_u32p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64]
         L.orc_mntru_testvector.argtypes = [ctypes.c_void_p, ctypes.c_uint64, _u64p]
         _lib = L
@@ -210,3 +226,65 @@ class Oracle:
         acc = np.zeros((self.k, self.N), dtype=np.uint64)
         lib().orc_mntru_testvector(self._ctx, p, _p64(acc))
         return acc
+
+
+# ---- gate head / tail (binfhe-base-scheme.cpp:380-515) ----------------------------
+
+def round_qQ(v: int, q: int, Q: int) -> int:
+    return lib().orc_round_qQ(v, q, Q)
+
+
+def ks_digits(qKS: int, baseKS: int) -> int:
+    return lib().orc_ks_digits(qKS, baseKS)
+
+
+def _u64(a):
+    return np.ascontiguousarray(a, dtype=np.uint64)
+
+
+def mntru_head(ct_nand, ct1, ct2, q: int) -> np.ndarray:
+    """ctNAND - (ct1 + ct2) mod q for one gate ([k][n] each)."""
+    cn, c1, c2 = _u64(ct_nand), _u64(ct1), _u64(ct2)
+    out = np.empty_like(c1)
+    k, n = c1.shape
+    lib().orc_mntru_head(_p64(cn), _p64(c1), _p64(c2), _p64(out), k, n, q)
+    return out
+
+
+def keyswitch2(ksk2, ct, k: int, N: int, n: int, qKS: int, baseKS: int) -> np.ndarray:
+    out = np.empty((k, n), dtype=np.uint64)
+    lib().orc_keyswitch2(_p64(_u64(ksk2)), _p64(_u64(ct)), _p64(out), k, N, n, qKS, baseKS)
+    return out
+
+
+def _oracle_methods():
+    def extract(self, acc):
+        out = np.empty((self.k, self.N), dtype=np.uint64)
+        lib().orc_extract(self._ctx, _p64(_u64(acc)), _p64(out))
+        return out
+
+    def mntru_tail(self, acc, ksk2, qKS: int, baseKS: int, n_out: int):
+        out = np.empty((self.k, n_out), dtype=np.uint64)
+        lib().orc_mntru_tail(self._ctx, _p64(_u64(acc)), _p64(_u64(ksk2)), qKS, baseKS, n_out, _p64(out))
+        return out
+
+    def mklwe_head(self, a1, b1, a2, b2, q: int, p: int = 4):
+        a1, a2 = _u64(a1), _u64(a2)
+        c = np.empty_like(a1)
+        acc = np.empty((self.k, self.N), dtype=np.uint64)
+        lib().orc_mklwe_head(self._ctx, _p64(a1), int(b1), _p64(a2), int(b2), q, a1.shape[1], p, _p64(c),
+                             _p64(acc))
+        return c, acc
+
+    def mklwe_tail(self, acc, A, Bk, qKS: int, baseKS: int, n_out: int):
+        oa = np.empty((self.k, n_out), dtype=np.uint64)
+        ob = np.zeros(1, dtype=np.uint64)
+        lib().orc_mklwe_tail(self._ctx, _p64(_u64(acc)), _p64(_u64(A)), _p64(_u64(Bk)), qKS, baseKS, n_out,
+                             _p64(oa), _p64(ob))
+        return oa, int(ob[0])
+
+    for f in (extract, mntru_tail, mklwe_head, mklwe_tail):
+        setattr(Oracle, f.__name__, f)
+
+
+_oracle_methods()

@@ -39,3 +39,9 @@ def make_case(pyoracle, method, k, n, q, baseG, B, seed, N=2048, Q=Q_MK):
     ct = pyoracle.fill_uniform(B * k * n, bound, seed * 1000 + 3).reshape(B, k, n)
     acc = pyoracle.fill_uniform(B * k * N, Q, seed * 1000 + 4).reshape(B, k, N)
     return orc, evk, pkey, ct, acc
+
+
+@pytest.fixture(scope="session")
+def mk_gpu():
+    import mkfhe_amd
+    return mkfhe_amd
