@@ -1,16 +1,20 @@
 #!/usr/bin/env python3
-"""Throughput bench of the MI355X multi-key accumulator (EvalAcc = blind rotation).
+"""Throughput bench of MK NAND gate bootstrapping on MI355X.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--paramset NAME] [--batch B]
+                    [--stage gate|evalacc]
 
-A "step" is one EvalAcc pass (all k*n accumulator steps) over one batch of B
-independent synthetic gates per GPU, inputs resident in HBM.  N > 1 runs one
-process per GPU (torch.distributed.run); rank 0 draws the bootstrapping keys
-and broadcasts them once over RCCL; gates are sharded by rank with no
-collective on the data path ("weak" scaling: B gates per GPU).
+A "step" is one pass over a batch of B independent synthetic NAND gates per
+GPU with inputs resident in HBM.  --stage gate (default) runs the whole
+EvalBinGate of the reference -- gate head, BootstrapGateCore (test vector +
+EvalAcc, the blind rotation) and the tail (extraction, ModSwitch, KeySwitch2 /
+KeySwitch); --stage evalacc runs the accumulator alone.  N > 1 runs one process
+per GPU (torch.distributed.run): rank 0 draws the bootstrapping and
+key-switching keys and broadcasts them once over RCCL; gates are sharded by
+rank with no collective on the data path ("weak" scaling: B gates per GPU).
 
-Rank 0 prints one JSON line (contract in the task statement); see DESIGN.md s6
-for the roofline accounting.
+Rank 0 prints one JSON line (contract in the task statement); DESIGN.md s4.4
+and s5 give the roofline accounting.
 """
 from __future__ import annotations
 
@@ -25,23 +29,27 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+
 # measured on this pool (tools/ubench_intops.hip, profiles/round1_ubench_intops.txt)
 PEAK_SHOUP_MULMOD_TPS = 7.744e12     # 27-bit Shoup mod-mul / s, whole chip
 PEAK_HBM_GBS = 8000.0                # MI355X_MICROARCH.md (spec)
 
 
-def algorithmic_counts(k: int, n: int, dg: int, N: int = 2048, B: int = 1):
+def algorithmic_counts(k: int, n: int, dg: int, nk: int, N: int = 2048, B: int = 1):
     """Per-launch algorithmic work of one accumulator step over B gates.
 
     mod-muls: (k+1)(dg+1) NTTs x N/2 log2 N butterflies (no N^-1 scaling: it is
     folded into the keys), k*N for acc*(X^c - 1), 2*dg*N key combination
-    (d_i, f_i), (2k+1)*dg*N MAC products.  Bytes: the step's key block and P
-    (read once per launch) + acc in/out per gate.
+    (d_i, f_i; XZW only), (2k+1)*dg*N MAC products.  Bytes: the step's key
+    block (nk key sets of [dg][2][N]) and P, read once per launch, plus the
+    accumulator in/out and the exponent per gate.
     """
     logn = N.bit_length() - 1
     ntt = (k + 1) * (dg + 1) * (N // 2) * logn
-    mulmods = B * (ntt + k * N + 2 * dg * N + (2 * k + 1) * dg * N)
-    key_bytes = 2 * dg * 2 * N * 4 + k * dg * N * 4
+    comb = 2 * dg * N if nk == 2 else 0
+    mulmods = B * (ntt + k * N + comb + (2 * k + 1) * dg * N)
+    key_bytes = nk * dg * 2 * N * 4 + k * dg * N * 4
     bytes_ = key_bytes + B * (2 * k * N * 4 + 4)
     return mulmods, bytes_
 
@@ -63,6 +71,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--paramset", default="STD128_MKNTRU")
     ap.add_argument("--batch", type=int, default=4096, help="gates per GPU")
+    ap.add_argument("--stage", choices=["gate", "evalacc"], default="gate")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--n-override", type=int, default=0,
@@ -70,9 +79,11 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(p, threads: int):
-    """Oracle restatement (oracle/, 'port') timed on the host cores: `threads`
-    independent gates, one per thread (bounded sample)."""
+def cpu_baseline(p, threads: int, stage: str, ks):
+    """The oracle restatement (oracle/, 'port') timed on the host cores:
+    `threads` independent gates, one per thread (bounded sample).  For the gate
+    stage the tail is the same contraction the oracle pins (tests/test_gate.py),
+    done in numpy; it is <2% of the gate."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
     pyoracle.build()
@@ -84,10 +95,19 @@ def cpu_baseline(p, threads: int):
     ct = pyoracle.fill_uniform(threads * p.k * p.n, bound, 103).reshape(threads, p.k, p.n)
     acc = np.broadcast_to(orc.mntru_testvector(4), (threads, p.k, p.N)).copy()
     t0 = time.perf_counter()
-    orc.evalacc_batch(evk, pkey, ct, acc, threads)
+    out = orc.evalacc_batch(evk, pkey, ct, acc, threads)
+    if stage == "gate":
+        qKS, baseKS, dks = ks
+        ksk = pyoracle.fill_uniform(p.k * p.N * dks * p.n, qKS, 104).reshape(p.k, p.N * dks, p.n).astype(np.int64)
+        for g in range(threads):
+            ext = orc.extract(out[g])
+            ms = np.vectorize(lambda v: pyoracle.round_qQ(int(v), qKS, p.Q), otypes=[np.int64])(ext)
+            digits = np.stack([(ms // baseKS ** t) % baseKS for t in range(dks)], axis=-1).reshape(p.k, -1)
+            _ = np.stack([(digits[u] @ ksk[u]) % qKS for u in range(p.k)])
     dt = time.perf_counter() - t0
+    what = "NAND gates (EvalAcc + extraction/ModSwitch/KeySwitch)" if stage == "gate" else "EvalAcc"
     return {"value": threads / dt, "unit": "bootstraps/s", "cores": threads, "kind": "port",
-            "sample": f"{threads} gates of {p.n}x{p.k}-step EvalAcc ({threads} threads, 1 gate each), "
+            "sample": f"{threads} {what} of {p.n}x{p.k} accumulator steps, one per thread on {threads} threads, "
                       f"{dt:.2f} s wall, CPU {os.uname().machine} nproc={os.cpu_count()}"}
 
 
@@ -105,6 +125,7 @@ def main():
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", rank=rank, world_size=world)
+    dev = f"cuda:{local}"
 
     import mkfhe_amd as mk
     from mkfhe_amd import shard
@@ -114,57 +135,104 @@ def main():
         p.n = args.n_override
     eng = mk.MKAccumulatorEngine(p, device=local)
     B = args.batch
+    lwe = p.method != mk.MKNTRU
+    qKS, baseKS = p.q, 32                     # modKS = mod and baseKS = 32 in every MK set (binfhecontext.cpp:129-144)
+    dks = int(np.ceil(np.log(qKS) / np.log(baseKS)))
 
     # ---- keys: drawn on rank 0, broadcast once over RCCL (xGMI) ----
     evk_n = int(np.prod(eng.evk_shape))
     pkey_n = int(np.prod(eng.pkey_shape))
-    keys = shard.broadcast_keys(evk_n + pkey_n, p.Q, seed=12345, device=f"cuda:{local}")
+    keys = shard.broadcast_keys(evk_n + pkey_n, p.Q, seed=12345, device=dev)
     keys_h = keys.cpu().numpy().view(np.uint32)
     eng.upload_keys(keys_h[:evk_n], keys_h[evk_n:])
     del keys, keys_h
+    if args.stage == "gate":
+        if lwe:
+            na = p.k * p.N * baseKS * dks * p.n
+            nb = p.k * p.N * baseKS * dks
+            ksk = shard.broadcast_keys(na + nb, qKS, seed=23456, device=dev).cpu().numpy().view(np.uint32)
+            eng.upload_ksk_mklwe(ksk[:na], ksk[na:], qKS, baseKS, p.n)
+        else:
+            nk = p.k * p.N * dks * p.n
+            ksk = shard.broadcast_keys(nk, qKS, seed=23456, device=dev).cpu().numpy().view(np.uint32)
+            eng.upload_ksk_mntru(ksk, qKS, baseKS, p.n)
+        del ksk
 
     # ---- this rank's shard of synthetic gates, resident in HBM ----
-    ct_h, acc_h = shard.synthetic_gates(eng, B, seed=1000 + rank)
-    d_ct = torch.from_numpy(ct_h.view(np.int32)).to(f"cuda:{local}")
-    d_in = torch.from_numpy(acc_h.view(np.int32)).to(f"cuda:{local}")
-    d_out = torch.empty_like(d_in)
+    rng = np.random.Generator(np.random.PCG64(1000 + rank))
+
+    def dev_u32(a):
+        return torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint32).view(np.int32)).to(dev)
+
     stream = torch.cuda.ExternalStream(eng.stream_handle())
+    if args.stage == "gate":
+        kn = p.k * p.n
+        d_a1 = dev_u32(rng.integers(0, p.q, size=(B, kn)))
+        d_a2 = dev_u32(rng.integers(0, p.q, size=(B, kn)))
+        d_nand = dev_u32(rng.integers(0, p.q, size=kn))
+        d_b1 = dev_u32(rng.integers(0, p.q, size=B)) if lwe else None
+        d_b2 = dev_u32(rng.integers(0, p.q, size=B)) if lwe else None
+        d_oa = torch.empty((B, p.k * p.n), dtype=torch.int32, device=dev)
+        d_ob = torch.empty(B, dtype=torch.int32, device=dev) if lwe else None
+
+        def run_step():
+            eng.eval_nand_device(d_nand, d_a1, d_b1, d_a2, d_b2, d_oa, d_ob, B)
+    else:
+        ct_h, acc_h = shard.synthetic_gates(eng, B, seed=1000 + rank)
+        d_ct, d_in = dev_u32(ct_h), dev_u32(acc_h)
+        d_out = torch.empty_like(d_in)
+
+        def run_step():
+            eng.eval_batch_device(d_ct, d_in, d_out, B)
 
     for _ in range(args.warmup):
-        eng.eval_batch_device(d_ct, d_in, d_out, B)
+        run_step()
     eng.sync()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    ev0.record(stream)
     for _ in range(args.steps):
-        eng.eval_batch_device(d_ct, d_in, d_out, B)
-    ev1.record(stream)
+        run_step()
     eng.sync()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    gpu_s = ev0.elapsed_time(ev1) / 1e3
-    elapsed = torch.tensor([wall], dtype=torch.float64, device=f"cuda:{local}")
+    elapsed = torch.tensor([wall], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     T = float(elapsed.item())
 
     # output sanity: residues stay canonical
-    assert int(d_out.max().item()) < p.Q and int(d_out.min().item()) >= 0
+    if args.stage == "gate":
+        assert int(d_oa.max().item()) < qKS and int(d_oa.min().item()) >= 0
+    else:
+        assert int(d_out.max().item()) < p.Q and int(d_out.min().item()) >= 0
 
-    kn = p.k * p.n
+    # ---- dominant kernel (the accumulator step) timed live with HIP events on
+    # the engine stream: one EvalAcc pass = k*n step launches (+2 tiny kernels)
+    ct_h, acc_h = shard.synthetic_gates(eng, B, seed=2000 + rank)
+    d_ct, d_in = dev_u32(ct_h), dev_u32(acc_h)
+    d_out = torch.empty_like(d_in)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)
+    eng.eval_batch_device(d_ct, d_in, d_out, B)
+    ev1.record(stream)
+    eng.sync()
+    kn_steps = p.k * p.n
+    per_launch_s = ev0.elapsed_time(ev1) / 1e3 / kn_steps
+
     dg = p.digitsG - 1
-    mm, by = algorithmic_counts(p.k, p.n, dg, p.N, B)
-    per_launch_s = gpu_s / (args.steps * kn)   # the step kernel dominates (>99% of GPU time)
+    nk = 1 if lwe else 2
+    mm, by = algorithmic_counts(p.k, p.n, dg, nk, p.N, B)
+    stage_txt = ("NAND gates: head + BootstrapGateCore (EvalAcc) + extraction/ModSwitch/"
+                 f"{'KeySwitch' if lwe else 'KeySwitch2'}") if args.stage == "gate" else "EvalAcc (blind rotation) only"
     result = {
-        "metric": "MK NAND bootstraps/sec (EvalAcc blind rotation) at k=2,4,8 parties; 1/2/4/8 MI355X; bit-exact vs CPU",
+        "metric": METRIC,
         "value": world * B * args.steps / T,
         "unit": "bootstraps/s",
         "n_gpus": world,
@@ -175,24 +243,23 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u32 (27-bit residues mod Q)",
-        "data": "synthetic: uniform keys/ciphertexts, MNTRU test-vector accumulators",
-        "config": {"workload": f"EvalAcc of {args.paramset} {p.k}-party {'MK-NTRU' if p.method == 0 else 'MK-LWE'} gate bootstraps "
-                               f"(k={p.k}, n={p.n}, N={p.N}, dg={dg}); gate tail (extraction/ModSwitch/"
-                               f"KeySwitch) not included",
-                   "paramset": args.paramset, "batch_per_gpu": B, "global_batch": world * B,
+        "data": "synthetic: uniform keys, key-switching keys and ciphertexts (seeded)",
+        "config": {"workload": f"{args.paramset} {p.k}-party {'MK-LWE' if lwe else 'MK-NTRU'} {stage_txt} "
+                               f"(k={p.k}, n={p.n}, N={p.N}, dg={dg})",
+                   "paramset": args.paramset, "stage": args.stage, "batch_per_gpu": B, "global_batch": world * B,
                    "parallelism": f"gate-sharded x{world}"},
         "roofline": {"bound": "hbm", "achieved": by / per_launch_s / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": by / per_launch_s / 1e9 / PEAK_HBM_GBS,
                      "traffic": measured_traffic(args.paramset) if not args.n_override else None,
                      "kernel": "mk_step_kernel", "per_launch_us": per_launch_s * 1e6,
                      "bytes_per_launch": by},
-        "roofline_valu": {"bound": "valu-int", "achieved": mm / per_launch_s / 1e12, "peak": PEAK_SHOUP_MULMOD_TPS / 1e12,
-                          "unit": "T mod-mul/s", "frac": mm / per_launch_s / PEAK_SHOUP_MULMOD_TPS,
-                          "mulmods_per_launch": mm},
+        "roofline_valu": {"bound": "valu-int", "achieved": mm / per_launch_s / 1e12,
+                          "peak": PEAK_SHOUP_MULMOD_TPS / 1e12, "unit": "T mod-mul/s",
+                          "frac": mm / per_launch_s / PEAK_SHOUP_MULMOD_TPS, "mulmods_per_launch": mm},
     }
     if rank == 0 and world == 1 and args.cpu_baseline:
         thr = args.cpu_threads or min(16, os.cpu_count() or 1)
-        result["cpu_baseline"] = cpu_baseline(p, thr)
+        result["cpu_baseline"] = cpu_baseline(p, thr, args.stage, (qKS, baseKS, dks))
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
