@@ -704,7 +704,7 @@ int ensure_gate_ws(mkacc_ctx* c, size_t B) {
     c->d_bh = nullptr;
     c->gate_B = 0;
     HIP_TRY(hipMalloc(&c->d_digits, B * c->p.k * (size_t)c->dks * kN));
-    HIP_TRY(hipMalloc(&c->d_bh, B * 4));
+    HIP_TRY(hipMalloc(&c->d_bh, B * c->p.k * 4));   // MK-LWE head rotation b [B], then partial b sums [B][k]
     c->gate_B = B;
     return MKACC_OK;
 }
@@ -757,8 +757,11 @@ void launch_tail(mkacc_ctx* c, const uint32_t* acc, uint32_t* out_a, uint32_t* o
                            (uint32_t)B, k, L, c->ks.n_out, c->n_pad, (uint32_t)c->ks.qKS, qinv);
     } else {
         const uint32_t b0 = round_qQ_host((c->p.Q >> 3) + 1, c->ks.qKS, c->p.Q);
-        hipLaunchKernelGGL(ks_mklwe_kernel, dim3((unsigned)B), dim3(256), 0, c->stream, c->d_digits, c->d_lweA,
-                           c->d_lweB, out_a, out_b, k, c->ks.n_out, c->ks.baseKS, c->dks, (uint32_t)c->ks.qKS, b0);
+        hipLaunchKernelGGL(ks_mklwe_kernel, dim3((unsigned)(B * k)), dim3(256), 0, c->stream, c->d_digits,
+                           c->d_lweA, c->d_lweB, out_a, c->d_bh, k, c->ks.n_out, c->ks.baseKS, c->dks,
+                           (uint32_t)c->ks.qKS);
+        hipLaunchKernelGGL(ks_mklwe_b_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, c->stream, c->d_bh,
+                           out_b, (uint32_t)B, k, (uint32_t)c->ks.qKS, b0);
     }
 }
 

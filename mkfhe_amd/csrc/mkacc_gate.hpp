@@ -196,36 +196,58 @@ __global__ __launch_bounds__(256) void ks_mntru_kernel(const uint8_t* __restrict
 
 // MK-LWE KeySwitch (mklwe-pke.cpp:260-298): for every party u, coefficient j
 // and digit t the row (u, j, D, t) of A is subtracted from a[u] and the entry
-// of B from b.  One block per gate; threads run over the n output columns and
-// walk the k*dks*N digit-selected rows (all sums < 2^31 before the final mod).
-//   A [k][N][Bks][dks][n] u16, Bv [k][N][Bks][dks] u16
+// of B from b.  One block per (gate, party); threads run over the n output
+// columns and stream the dks*N digit-selected rows, 16 independent row loads
+// in flight per thread (digits fetched 16 at a time, wave-uniform).  Sums of
+// dks*N words < 2^16 stay below 2^32 (dks*N <= 2^16).
+//   A [k][N][Bks][dks][n] u16, Bv [k][N][Bks][dks] u16, partial_b [B][k]
 __global__ __launch_bounds__(256) void ks_mklwe_kernel(const uint8_t* __restrict__ D, const uint16_t* __restrict__ A,
                                                        const uint16_t* __restrict__ Bv, uint32_t* __restrict__ out_a,
-                                                       uint32_t* __restrict__ out_b, uint32_t k, uint32_t n_out,
-                                                       uint32_t baseKS, uint32_t dks, uint32_t qKS, uint32_t b0) {
-    const uint32_t b = blockIdx.x;
-    const size_t L = (size_t)dks * kN;
-    uint32_t sb = 0;
-    for (uint32_t c = threadIdx.x; c < ((n_out + 255u) & ~255u); c += 256) {
-        for (uint32_t u = 0; u < k; ++u) {
-            const uint8_t* Dp = D + ((size_t)b * k + u) * L;
-            uint32_t s = 0;
-            for (uint32_t t = 0; t < dks; ++t) {
-                for (uint32_t j = 0; j < (uint32_t)kN; ++j) {
-                    const uint32_t d = Dp[(size_t)t * kN + j];          // wave-uniform
-                    const size_t row = (((size_t)u * kN + j) * baseKS + d) * dks + t;
-                    if (c < n_out) s += A[row * n_out + c];
-                    if (c == 0) sb += Bv[row];
-                }
+                                                       uint32_t* __restrict__ partial_b, uint32_t k, uint32_t n_out,
+                                                       uint32_t baseKS, uint32_t dks, uint32_t qKS) {
+    const uint32_t u = blockIdx.x % k, b = blockIdx.x / k;
+    const uint32_t L = dks * kN;
+    const uint4* Dp = reinterpret_cast<const uint4*>(D + ((size_t)b * k + u) * L);
+    const size_t rowbase = (size_t)u * kN * baseKS;     // row of (u, j=0, d=0, t=0) / dks
+    for (uint32_t c0 = 0; c0 < n_out; c0 += 256) {
+        const uint32_t c = c0 + threadIdx.x;
+        const bool on = c < n_out;
+        uint32_t s = 0, sb = 0;
+        for (uint32_t l0 = 0; l0 < L; l0 += 16) {
+            const uint4 dv = Dp[l0 >> 4];
+            const uint32_t dw[4] = {(uint32_t)__builtin_amdgcn_readfirstlane(dv.x),
+                                    (uint32_t)__builtin_amdgcn_readfirstlane(dv.y),
+                                    (uint32_t)__builtin_amdgcn_readfirstlane(dv.z),
+                                    (uint32_t)__builtin_amdgcn_readfirstlane(dv.w)};
+            uint32_t v[16];
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const uint32_t l = l0 + e, t = l / kN, j = l % kN;     // digits stored [t][j]
+                const uint32_t d = (dw[e >> 2] >> (8 * (e & 3))) & 0xFFu;
+                const size_t row = ((rowbase + (size_t)j * baseKS + d) * dks) + t;
+                v[e] = on ? A[row * n_out + c] : 0u;
+                if (c0 == 0 && threadIdx.x == 0) sb += Bv[row];
             }
-            s %= qKS;
-            if (c < n_out) out_a[((size_t)b * k + u) * n_out + c] = s == 0 ? 0 : qKS - s;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) s += v[e];
         }
+        s %= qKS;
+        if (on) out_a[((size_t)b * k + u) * n_out + c] = s == 0 ? 0 : qKS - s;
+        if (c0 == 0 && threadIdx.x == 0) partial_b[(size_t)b * k + u] = sb % qKS;
     }
-    if (threadIdx.x == 0) {
-        sb %= qKS;
-        out_b[b] = b0 >= sb ? b0 - sb : b0 + qKS - sb;
+}
+
+// b = b0 - sum_u partial_b[g][u] mod qKS
+__global__ void ks_mklwe_b_kernel(const uint32_t* __restrict__ partial_b, uint32_t* __restrict__ out_b, uint32_t B,
+                                  uint32_t k, uint32_t qKS, uint32_t b0) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= B) return;
+    uint32_t sb = 0;
+    for (uint32_t u = 0; u < k; ++u) {
+        sb += partial_b[(size_t)g * k + u];
+        sb = sb >= qKS ? sb - qKS : sb;
     }
+    out_b[g] = b0 >= sb ? b0 - sb : b0 + qKS - sb;
 }
 
 }  // namespace
