@@ -307,6 +307,7 @@ private:
         return *m_ctx;
     }
 
+public:
     // Flatten ek [k][nk][n+1] x [dg][2] x N and Pkey [k][dg] x N into the C-ABI
     // layout and upload them once per key object.
     static void upload(DeviceContext& dc, ConstUniEncACCKey& ek, const std::vector<std::vector<NativePoly>>& Pkey) {
@@ -341,6 +342,7 @@ private:
         dc.pkey_token = Pkey.data();
     }
 
+private:
     int m_device;
     mutable std::mutex m_mu;
     mutable std::unique_ptr<DeviceContext> m_ctx;
@@ -375,6 +377,273 @@ inline std::shared_ptr<UniEncAccumulator> MakeUniEncAccumulator(BINFHE_METHOD me
     if (method == MKNTRU_B || method == MKNTRU_LWE) return std::make_shared<UniEncAccumulatorXZW_B>(device);
     throw config_error("method is invalid");
 }
+
+
+// =====================================================================================
+// Gate level: BinFHEContext::EvalBinGate for MK-NTRU and MK-LWE
+// (binfhecontext.h:336-338, binfhe-base-scheme.cpp:380-515).
+// =====================================================================================
+
+// binfhe-constants.h:143
+enum BINGATE { OR, AND, NOR, NAND, XOR_FAST, XNOR_FAST, MAJORITY, AND3, OR3, AND4, OR4, CMUX, XOR, XNOR };
+
+// The multi-key parameter sets of binfhe-constants.h:95-110 (binfhecontext.cpp:129-144)
+enum BINFHE_PARAMSET {
+    STD128_MKNTRU, STD128_MKNTRU_2, STD128_MKNTRU_3, STD128_MKNTRU_4,
+    STD128_MKNTRU_LWE, STD128_MKNTRU_LWE_2, STD128_MKNTRU_LWE_3, STD128_MKNTRU_LWE_4,
+    STD100_MKNTRU, STD100_MKNTRU_2, STD100_MKNTRU_3, STD100_MKNTRU_4,
+    STD100_MKNTRU_LWE, STD100_MKNTRU_LWE_2, STD100_MKNTRU_LWE_3, STD100_MKNTRU_LWE_4,
+};
+inline const char* ParamSetName(BINFHE_PARAMSET s) {
+    static const char* names[] = {
+        "STD128_MKNTRU", "STD128_MKNTRU_2", "STD128_MKNTRU_3", "STD128_MKNTRU_4",
+        "STD128_MKNTRU_LWE", "STD128_MKNTRU_LWE_2", "STD128_MKNTRU_LWE_3", "STD128_MKNTRU_LWE_4",
+        "STD100_MKNTRU", "STD100_MKNTRU_2", "STD100_MKNTRU_3", "STD100_MKNTRU_4",
+        "STD100_MKNTRU_LWE", "STD100_MKNTRU_LWE_2", "STD100_MKNTRU_LWE_3", "STD100_MKNTRU_LWE_4"};
+    return names[s];
+}
+
+// MNTRU ciphertext: k vectors of n words mod q (mntru-ciphertext.h:28-31, p = 4)
+class MNTRUCiphertextImpl {
+public:
+    MNTRUCiphertextImpl() = default;
+    MNTRUCiphertextImpl(std::vector<NativeVector> e, uint64_t q) : m_elements(std::move(e)), m_q(q) {}
+    const std::vector<NativeVector>& GetElements() const { return m_elements; }
+    std::vector<NativeVector>& GetElements() { return m_elements; }
+    uint64_t GetModulus() const { return m_q; }
+    uint64_t GetptModulus() const { return m_p; }
+    uint32_t Getk() const { return (uint32_t)m_elements.size(); }
+    uint32_t GetLength() const { return m_elements.empty() ? 0 : (uint32_t)m_elements[0].size(); }
+
+private:
+    std::vector<NativeVector> m_elements;
+    uint64_t m_q = 0, m_p = 4;
+};
+using MNTRUCiphertext = std::shared_ptr<MNTRUCiphertextImpl>;
+using ConstMNTRUCiphertext = const std::shared_ptr<const MNTRUCiphertextImpl>;
+
+// MK-LWE ciphertext: (a_1..a_k, b) mod q (mklwe-ciphertext.h:55-58)
+class MKLWECiphertextImpl {
+public:
+    MKLWECiphertextImpl() = default;
+    MKLWECiphertextImpl(std::vector<NativeVector> a, uint64_t b, uint64_t q) : m_a(std::move(a)), m_b(b), m_q(q) {}
+    const std::vector<NativeVector>& GetA() const { return m_a; }
+    std::vector<NativeVector>& GetA() { return m_a; }
+    uint64_t GetB() const { return m_b; }
+    uint64_t GetModulus() const { return m_q; }
+    uint64_t GetptModulus() const { return m_p; }
+    uint32_t Getk() const { return (uint32_t)m_a.size(); }
+    uint32_t GetLength() const { return m_a.empty() ? 0 : (uint32_t)m_a[0].size(); }
+
+private:
+    std::vector<NativeVector> m_a;
+    uint64_t m_b = 0, m_q = 0, m_p = 4;
+};
+using MKLWECiphertext = std::shared_ptr<MKLWECiphertextImpl>;
+using ConstMKLWECiphertext = const std::shared_ptr<const MKLWECiphertextImpl>;
+
+// KeySwitchGen2's table KSK2[u][j][l] = j * KSK[u][l] mod qKS, [k][baseKS][N*dks]
+// of n-vectors (mntru-pke.cpp:624-760).  The engine reads KSK2[u][1].
+class MNTRUSwitchingKey2Impl {
+public:
+    explicit MNTRUSwitchingKey2Impl(std::vector<std::vector<std::vector<NativeVector>>> k) : m_key(std::move(k)) {}
+    const std::vector<std::vector<std::vector<NativeVector>>>& GetElements() const { return m_key; }
+
+private:
+    std::vector<std::vector<std::vector<NativeVector>>> m_key;
+};
+using MNTRUSwitchingKey2 = std::shared_ptr<const MNTRUSwitchingKey2Impl>;
+
+// MK-LWE KeySwitchGen (mklwe-pke.cpp:176-258): A[u][j][d][t] n-vectors, B[u][j][d][t]
+class MKLWESwitchingKeyImpl {
+public:
+    using A4 = std::vector<std::vector<std::vector<std::vector<NativeVector>>>>;
+    using B4 = std::vector<std::vector<std::vector<std::vector<uint64_t>>>>;
+    MKLWESwitchingKeyImpl(A4 a, B4 b) : m_a(std::move(a)), m_b(std::move(b)) {}
+    const A4& GetElementsA() const { return m_a; }
+    const B4& GetElementsB() const { return m_b; }
+
+private:
+    A4 m_a;
+    B4 m_b;
+};
+using MKLWESwitchingKey = std::shared_ptr<const MKLWESwitchingKeyImpl>;
+
+// The fields of the reference UniEncBTKey (binfhe-base-scheme.h:65-83) the
+// gate path reads.
+struct UniEncBTKey {
+    UniEncACCKey BSkey;
+    MNTRUSwitchingKey2 KSkey2;
+    MKLWESwitchingKey LKSkey;
+    std::vector<std::vector<NativePoly>> Pkey;
+    std::vector<NativePoly> f;
+};
+
+// BinFHEContext subset for multi-key NAND gates on one MI355X.  Key generation
+// (MNTRU_KeyGen / MKBTKeyGen / ctGateGen) needs NTL in the reference and is
+// not part of this engine: keys are loaded with BTKeyLoad / SetctNAND.
+class BinFHEContext {
+public:
+    void GenerateBinFHEContext(BINFHE_PARAMSET set, BINFHE_METHOD method, int device = 0) {
+        if (method != MKNTRU && method != MKNTRU_B && method != MKNTRU_LWE)
+            throw config_error("method is invalid");
+        m_method = method;
+        m_params = UniEncCryptoParams::FromParamSet(ParamSetName(set), method);
+        m_dc = std::make_unique<DeviceContext>(m_params->abi(), device);
+        m_params->set_abi(m_dc->params());
+        m_keys = false;
+        m_ctNAND.reset();
+    }
+    // custom parameters (the reference's explicit-parameter overload, binfhecontext.h:94)
+    void GenerateBinFHEContext(const UniEncCryptoParams& params, int device = 0) {
+        m_method = params.GetMethod();
+        m_params = std::make_shared<UniEncCryptoParams>(params);
+        m_dc = std::make_unique<DeviceContext>(m_params->abi(), device);
+        m_params->set_abi(m_dc->params());
+        m_keys = false;
+        m_ctNAND.reset();
+    }
+    const std::shared_ptr<UniEncCryptoParams>& GetParams() const { return m_params; }
+    // modKS = mod and baseKS = 32 in every MK set (binfhecontext.cpp:129-144)
+    mkacc_ks_params GetKSParams() const { return mkacc_ks_params{m_params->Getq(), 32, m_params->GetLatticeParam()}; }
+
+    void BTKeyLoad(const UniEncBTKey& ek) {
+        need_context();
+        if (!ek.BSkey) throw config_error("BSkey is empty");
+        UniEncAccumulator::upload(*m_dc, ek.BSkey, ek.Pkey);
+        const mkacc_ks_params ks = GetKSParams();
+        const uint32_t k = m_params->Getk(), N = m_params->GetN(), n = ks.n_out;
+        const uint32_t dks = mkacc_ks_digits(&ks);
+        if (m_method == MKNTRU) {
+            if (!ek.KSkey2) throw config_error("KSkey2 is empty");
+            const auto& K2 = ek.KSkey2->GetElements();
+            if (K2.size() != k) throw config_error("KSkey2 must have k parties");
+            std::vector<uint32_t> h((size_t)k * N * dks * n);
+            for (uint32_t u = 0; u < k; ++u) {
+                if (K2[u].size() < 2 || K2[u][1].size() != (size_t)N * dks)
+                    throw config_error("KSkey2[u] must be [baseKS][N*dks]");
+                for (size_t l = 0; l < (size_t)N * dks; ++l) {
+                    const NativeVector& row = K2[u][1][l];
+                    if (row.size() != n) throw config_error("KSkey2 rows must have n words");
+                    for (uint32_t i = 0; i < n; ++i) h[((size_t)u * N * dks + l) * n + i] = (uint32_t)row[i];
+                }
+            }
+            check(mkacc_upload_ksk_mntru(m_dc->get(), &ks, h.data()));
+        } else {
+            if (!ek.LKSkey) throw config_error("LKSkey is empty");
+            const auto& A = ek.LKSkey->GetElementsA();
+            const auto& Bk = ek.LKSkey->GetElementsB();
+            const size_t rows = (size_t)k * N * ks.baseKS * dks;
+            std::vector<uint32_t> ha(rows * n), hb(rows);
+            size_t r = 0;
+            for (uint32_t u = 0; u < k; ++u)
+                for (uint32_t j = 0; j < N; ++j)
+                    for (uint32_t d = 0; d < ks.baseKS; ++d)
+                        for (uint32_t t = 0; t < dks; ++t, ++r) {
+                            const NativeVector& row = A.at(u).at(j).at(d).at(t);
+                            if (row.size() != n) throw config_error("LKSkey rows must have n words");
+                            for (uint32_t i = 0; i < n; ++i) ha[r * n + i] = (uint32_t)row[i];
+                            hb[r] = (uint32_t)Bk.at(u).at(j).at(d).at(t);
+                        }
+            check(mkacc_upload_ksk_mklwe(m_dc->get(), &ks, ha.data(), hb.data()));
+        }
+        m_keys = true;
+    }
+    // the NAND constant ciphertext that ctGateGen produces (binfhe-base-scheme.cpp:340-376)
+    void SetctNAND(MNTRUCiphertext ct) { m_ctNAND = std::move(ct); }
+
+    MNTRUCiphertext EvalBinGate(BINGATE gate, ConstMNTRUCiphertext& ct1, ConstMNTRUCiphertext& ct2) const {
+        if (ct1 == ct2) throw config_error("Input ciphertexts should be independant");
+        return EvalBinGate(gate, std::vector<MNTRUCiphertext>{std::const_pointer_cast<MNTRUCiphertextImpl>(ct1)},
+                           std::vector<MNTRUCiphertext>{std::const_pointer_cast<MNTRUCiphertextImpl>(ct2)})[0];
+    }
+    MKLWECiphertext EvalBinGate(BINGATE gate, ConstMKLWECiphertext& ct1, ConstMKLWECiphertext& ct2) const {
+        if (ct1 == ct2) throw config_error("Input ciphertexts should be independant");
+        return EvalBinGate(gate, std::vector<MKLWECiphertext>{std::const_pointer_cast<MKLWECiphertextImpl>(ct1)},
+                           std::vector<MKLWECiphertext>{std::const_pointer_cast<MKLWECiphertextImpl>(ct2)})[0];
+    }
+
+    // Batch extension: B independent NAND gates in one engine pass.
+    std::vector<MNTRUCiphertext> EvalBinGate(BINGATE gate, const std::vector<MNTRUCiphertext>& ct1,
+                                             const std::vector<MNTRUCiphertext>& ct2) const {
+        need_gate(gate, MKNTRU);
+        if (!m_ctNAND) throw config_error("ctNAND has not been generated (ctGateGen)");
+        const uint32_t k = m_params->Getk(), n = m_params->GetLatticeParam();
+        const size_t B = ct1.size();
+        if (ct2.size() != B) throw config_error("ct1 and ct2 must have the same length");
+        std::vector<uint32_t> a1(B * k * n), a2(B * k * n), nand(k * n), out(B * k * n);
+        pack(*m_ctNAND, nand.data(), k, n);
+        for (size_t b = 0; b < B; ++b) {
+            if (ct1[b] == ct2[b]) throw config_error("Input ciphertexts should be independant");
+            pack(*ct1[b], a1.data() + b * k * n, k, n);
+            pack(*ct2[b], a2.data() + b * k * n, k, n);
+        }
+        check(mkacc_eval_nand_mntru(m_dc->get(), nand.data(), a1.data(), a2.data(), out.data(), B));
+        std::vector<MNTRUCiphertext> res(B);
+        for (size_t b = 0; b < B; ++b) {
+            std::vector<NativeVector> e(k, NativeVector(n));
+            for (uint32_t u = 0; u < k; ++u)
+                for (uint32_t i = 0; i < n; ++i) e[u][i] = out[(b * k + u) * n + i];
+            res[b] = std::make_shared<MNTRUCiphertextImpl>(std::move(e), GetKSParams().qKS);
+        }
+        return res;
+    }
+    std::vector<MKLWECiphertext> EvalBinGate(BINGATE gate, const std::vector<MKLWECiphertext>& ct1,
+                                             const std::vector<MKLWECiphertext>& ct2) const {
+        need_gate(gate, MKNTRU_LWE);
+        const uint32_t k = m_params->Getk(), n = m_params->GetLatticeParam();
+        const size_t B = ct1.size();
+        if (ct2.size() != B) throw config_error("ct1 and ct2 must have the same length");
+        std::vector<uint32_t> a1(B * k * n), a2(B * k * n), b1(B), b2(B), oa(B * k * n), ob(B);
+        for (size_t b = 0; b < B; ++b) {
+            if (ct1[b] == ct2[b]) throw config_error("Input ciphertexts should be independant");
+            packA(*ct1[b], a1.data() + b * k * n, k, n);
+            packA(*ct2[b], a2.data() + b * k * n, k, n);
+            b1[b] = (uint32_t)ct1[b]->GetB();
+            b2[b] = (uint32_t)ct2[b]->GetB();
+        }
+        check(mkacc_eval_nand_mklwe(m_dc->get(), a1.data(), b1.data(), a2.data(), b2.data(), oa.data(), ob.data(),
+                                    B));
+        std::vector<MKLWECiphertext> res(B);
+        for (size_t b = 0; b < B; ++b) {
+            std::vector<NativeVector> a(k, NativeVector(n));
+            for (uint32_t u = 0; u < k; ++u)
+                for (uint32_t i = 0; i < n; ++i) a[u][i] = oa[(b * k + u) * n + i];
+            res[b] = std::make_shared<MKLWECiphertextImpl>(std::move(a), ob[b], GetKSParams().qKS);
+        }
+        return res;
+    }
+
+private:
+    void need_context() const {
+        if (!m_dc) throw config_error("call GenerateBinFHEContext first");
+    }
+    void need_gate(BINGATE gate, BINFHE_METHOD family) const {
+        need_context();
+        if (gate != NAND) throw not_implemented_error("only NAND is supported (ctGateGen, binfhe-base-scheme.cpp:341-342)");
+        const bool lwe = m_method != MKNTRU;
+        if (lwe != (family != MKNTRU)) throw config_error("ciphertext type does not match the context method");
+        if (!m_keys)
+            throw config_error(
+                "Bootstrapping keys have not been generated. Please call MKBTKeyGen before calling bootstrapping.");
+    }
+    static void pack(const MNTRUCiphertextImpl& c, uint32_t* dst, uint32_t k, uint32_t n) {
+        if (c.Getk() != k || c.GetLength() != n) throw config_error("ciphertext must be k x n");
+        for (uint32_t u = 0; u < k; ++u)
+            for (uint32_t i = 0; i < n; ++i) dst[u * n + i] = (uint32_t)c.GetElements()[u][i];
+    }
+    static void packA(const MKLWECiphertextImpl& c, uint32_t* dst, uint32_t k, uint32_t n) {
+        if (c.Getk() != k || c.GetLength() != n) throw config_error("ciphertext must be k x n");
+        for (uint32_t u = 0; u < k; ++u)
+            for (uint32_t i = 0; i < n; ++i) dst[u * n + i] = (uint32_t)c.GetA()[u][i];
+    }
+
+    BINFHE_METHOD m_method = MKNTRU;
+    std::shared_ptr<UniEncCryptoParams> m_params;
+    std::unique_ptr<DeviceContext> m_dc;
+    bool m_keys = false;
+    MNTRUCiphertext m_ctNAND;
+};
 
 }  // namespace mkfhe_amd
 

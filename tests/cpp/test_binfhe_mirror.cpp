@@ -175,6 +175,152 @@ static void run_case(const Case& cs, uint64_t seed) {
     orc_ctx_destroy(oc);
 }
 
+// ---- full NAND gates through BinFHEContext ----------------------------------------------
+static void test_gpu_gates(BINFHE_METHOD method, uint32_t k, uint32_t n, uint32_t baseG, uint64_t seed) {
+    const uint32_t N = 2048, B = 3, baseKS = 32;
+    const bool lwe = method != MKNTRU;
+    const uint64_t q = lwe ? 32749 : 45181, qKS = q;
+    BinFHEContext cc;
+    cc.GenerateBinFHEContext(UniEncCryptoParams(k, N, kQ, q, baseG, method, n));
+    // reference error behaviour before keys exist
+    auto c0 = std::make_shared<MNTRUCiphertextImpl>(std::vector<NativeVector>(k, NativeVector(n, 0)), q);
+    auto c1 = std::make_shared<MNTRUCiphertextImpl>(*c0);
+    if (!lwe) EXPECT(throws<config_error>([&] { cc.EvalBinGate(NAND, c0, c1); }));
+    EXPECT(throws<config_error>([&] { cc.EvalBinGate(NAND, c0, c0); }));
+    const mkacc_params eff = cc.GetParams()->abi();
+    const uint32_t dg = eff.digitsG - 1, nk = lwe ? 1 : 2;
+    mkacc_ks_params ks{qKS, baseKS, n};
+    const uint32_t dks = mkacc_ks_digits(&ks);
+
+    orc_params op{};
+    op.method = lwe ? ORC_XZW_B : ORC_XZW;
+    op.k = k; op.n = n; op.N = N; op.Q = kQ; op.q = q; op.baseG = baseG; op.digitsG = eff.digitsG; op.psi = eff.root;
+    orc_ctx* oc = orc_ctx_create(&op);
+
+    UniEncBTKey ek;
+    auto evk = uniform(orc_evk_words(&op), kQ, seed * 10 + 1);
+    auto pk = uniform((size_t)k * dg * N, kQ, seed * 10 + 2);
+    auto acck = std::make_shared<UniEncACCKeyImpl>(k, nk, n + 1);
+    size_t o = 0;
+    for (uint32_t u = 0; u < k; ++u)
+        for (uint32_t j = 0; j < nk; ++j)
+            for (uint32_t i = 0; i <= n; ++i) {
+                auto key = std::make_shared<UniEncEvalKeyImpl>(dg, 2);
+                for (uint32_t d = 0; d < dg; ++d)
+                    for (uint32_t c = 0; c < 2; ++c, o += N)
+                        key->GetElements()[d][c] = NativePoly(NativeVector(evk.begin() + o, evk.begin() + o + N), EVALUATION);
+                (*acck)[u][j][i] = key;
+            }
+    ek.BSkey = acck;
+    ek.Pkey.resize(k);
+    for (uint32_t u = 0; u < k; ++u)
+        for (uint32_t d = 0; d < dg; ++d) {
+            const size_t b = ((size_t)u * dg + d) * N;
+            ek.Pkey[u].emplace_back(NativeVector(pk.begin() + b, pk.begin() + b + N), EVALUATION);
+        }
+    // key-switching keys, shaped as KeySwitchGen2 / KeySwitchGen produce them
+    std::vector<uint64_t> ksk2, A, Bk;
+    if (!lwe) {
+        auto ksk = uniform((size_t)k * N * dks * n, qKS, seed * 10 + 3);
+        ksk2.resize((size_t)k * baseKS * N * dks * n);
+        std::vector<std::vector<std::vector<NativeVector>>> K2(k, std::vector<std::vector<NativeVector>>(baseKS));
+        for (uint32_t u = 0; u < k; ++u)
+            for (uint32_t jj = 0; jj < baseKS; ++jj) {
+                K2[u][jj].resize((size_t)N * dks);
+                for (size_t l = 0; l < (size_t)N * dks; ++l) {
+                    NativeVector row(n);
+                    for (uint32_t i = 0; i < n; ++i) {
+                        row[i] = (jj * ksk[((size_t)u * N * dks + l) * n + i]) % qKS;
+                        ksk2[(((size_t)u * baseKS + jj) * N * dks + l) * n + i] = row[i];
+                    }
+                    K2[u][jj][l] = std::move(row);
+                }
+            }
+        ek.KSkey2 = std::make_shared<MNTRUSwitchingKey2Impl>(std::move(K2));
+    } else {
+        A = uniform((size_t)k * N * baseKS * dks * n, qKS, seed * 10 + 4);
+        Bk = uniform((size_t)k * N * baseKS * dks, qKS, seed * 10 + 5);
+        MKLWESwitchingKeyImpl::A4 a4(k, std::vector<std::vector<std::vector<NativeVector>>>(
+                                            N, std::vector<std::vector<NativeVector>>(baseKS, std::vector<NativeVector>(dks))));
+        MKLWESwitchingKeyImpl::B4 b4(k, std::vector<std::vector<std::vector<uint64_t>>>(
+                                            N, std::vector<std::vector<uint64_t>>(baseKS, std::vector<uint64_t>(dks))));
+        size_t r = 0;
+        for (uint32_t u = 0; u < k; ++u)
+            for (uint32_t j = 0; j < N; ++j)
+                for (uint32_t d = 0; d < baseKS; ++d)
+                    for (uint32_t t = 0; t < dks; ++t, ++r) {
+                        a4[u][j][d][t] = NativeVector(A.begin() + r * n, A.begin() + (r + 1) * n);
+                        b4[u][j][d][t] = Bk[r];
+                    }
+        ek.LKSkey = std::make_shared<MKLWESwitchingKeyImpl>(std::move(a4), std::move(b4));
+    }
+    cc.BTKeyLoad(ek);
+
+    auto w1 = uniform((size_t)B * k * n, q, seed * 10 + 6), w2 = uniform((size_t)B * k * n, q, seed * 10 + 7);
+    auto wb = uniform(2 * B, q, seed * 10 + 8), wn = uniform((size_t)k * n, q, seed * 10 + 9);
+    auto vecs = [&](const std::vector<uint64_t>& w, uint32_t b) {
+        std::vector<NativeVector> e(k);
+        for (uint32_t u = 0; u < k; ++u) e[u] = NativeVector(w.begin() + ((size_t)b * k + u) * n, w.begin() + ((size_t)b * k + u + 1) * n);
+        return e;
+    };
+    size_t bad = 0;
+    std::vector<uint64_t> acc((size_t)k * N), out((size_t)k * n);
+    if (!lwe) {
+        std::vector<NativeVector> nv(k);
+        for (uint32_t u = 0; u < k; ++u) nv[u] = NativeVector(wn.begin() + (size_t)u * n, wn.begin() + (size_t)(u + 1) * n);
+        cc.SetctNAND(std::make_shared<MNTRUCiphertextImpl>(nv, q));
+        std::vector<MNTRUCiphertext> x1, x2;
+        for (uint32_t b = 0; b < B; ++b) {
+            x1.push_back(std::make_shared<MNTRUCiphertextImpl>(vecs(w1, b), q));
+            x2.push_back(std::make_shared<MNTRUCiphertextImpl>(vecs(w2, b), q));
+        }
+        auto res = cc.EvalBinGate(NAND, x1, x2);
+        auto single = cc.EvalBinGate(NAND, ConstMNTRUCiphertext(x1[1]), ConstMNTRUCiphertext(x2[1]));
+        EXPECT(single->GetElements() == res[1]->GetElements());
+        for (uint32_t b = 0; b < B; ++b) {
+            std::vector<uint64_t> ct((size_t)k * n);
+            orc_mntru_head(wn.data(), w1.data() + (size_t)b * k * n, w2.data() + (size_t)b * k * n, ct.data(), k, n, q);
+            orc_mntru_testvector(oc, 4, acc.data());
+            EXPECT(orc_evalacc(oc, evk.data(), pk.data(), ct.data(), acc.data()) == 0);
+            orc_mntru_tail(oc, acc.data(), ksk2.data(), qKS, baseKS, n, out.data());
+            for (uint32_t u = 0; u < k; ++u)
+                for (uint32_t i = 0; i < n; ++i) bad += res[b]->GetElements()[u][i] != out[(size_t)u * n + i];
+        }
+    } else {
+        std::vector<MKLWECiphertext> x1, x2;
+        for (uint32_t b = 0; b < B; ++b) {
+            x1.push_back(std::make_shared<MKLWECiphertextImpl>(vecs(w1, b), wb[b], q));
+            x2.push_back(std::make_shared<MKLWECiphertextImpl>(vecs(w2, b), wb[B + b], q));
+        }
+        auto res = cc.EvalBinGate(NAND, x1, x2);
+        for (uint32_t b = 0; b < B; ++b) {
+            std::vector<uint64_t> c((size_t)k * n);
+            orc_mklwe_head(oc, w1.data() + (size_t)b * k * n, wb[b], w2.data() + (size_t)b * k * n, wb[B + b], q, n, 4,
+                           c.data(), acc.data());
+            EXPECT(orc_evalacc(oc, evk.data(), pk.data(), c.data(), acc.data()) == 0);
+            uint64_t ob = 0;
+            orc_mklwe_tail(oc, acc.data(), A.data(), Bk.data(), qKS, baseKS, n, out.data(), &ob);
+            bad += res[b]->GetB() != ob;
+            for (uint32_t u = 0; u < k; ++u)
+                for (uint32_t i = 0; i < n; ++i) bad += res[b]->GetA()[u][i] != out[(size_t)u * n + i];
+        }
+    }
+    if (bad) std::fprintf(stderr, "gate method=%d k=%u n=%u: %zu words differ\n", method, k, n, bad);
+    EXPECT(bad == 0);
+    EXPECT(throws<not_implemented_error>([&] {
+        if (lwe) {
+            auto a = std::make_shared<MKLWECiphertextImpl>(vecs(w1, 0), 0, q);
+            auto b = std::make_shared<MKLWECiphertextImpl>(vecs(w2, 0), 0, q);
+            cc.EvalBinGate(AND, ConstMKLWECiphertext(a), ConstMKLWECiphertext(b));
+        } else {
+            auto a = std::make_shared<MNTRUCiphertextImpl>(vecs(w1, 0), q);
+            auto b = std::make_shared<MNTRUCiphertextImpl>(vecs(w2, 0), q);
+            cc.EvalBinGate(AND, ConstMNTRUCiphertext(a), ConstMNTRUCiphertext(b));
+        }
+    }));
+    orc_ctx_destroy(oc);
+}
+
 static void test_gpu() {
     const Case cases[] = {
         {MKNTRU, 2, 4, 45181, 1 << 9, 3},      // STD100_MKNTRU shape
@@ -184,6 +330,8 @@ static void test_gpu() {
     };
     uint64_t seed = 1;
     for (const Case& c : cases) run_case(c, seed++);
+    test_gpu_gates(MKNTRU, 2, 3, 1 << 7, 11);
+    test_gpu_gates(MKNTRU_LWE, 2, 3, 1 << 9, 12);
 }
 
 int main(int argc, char** argv) {
