@@ -77,6 +77,28 @@ __device__ __forceinline__ uint32_t reduce58(uint64_t x, const Mod& m) {
 __device__ __forceinline__ uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {
     return (uint64_t)a * b + c;           // v_mad_u64_u32
 }
+// v_mad_u64_u32 pinned as ONE instruction.  Where only the low word of a*b + c
+// is used the compiler narrows C++ to v_mul_lo_u32 + v_add_u32; the 64-bit
+// form does both in one issue slot (tools/ubench_isa.hip: all three cost about
+// the same).  SB: b is wave-uniform (SGPR operand).  Carry-out goes to VCC.
+template <bool SB>
+__device__ __forceinline__ uint64_t mad64_pin(uint32_t a, uint32_t b, uint64_t c) {
+    uint64_t r;
+    if constexpr (SB)
+        asm("v_mad_u64_u32 %0, vcc, %1, %2, %3" : "=v"(r) : "v"(a), "s"(b), "v"(c) : "vcc");
+    else
+        asm("v_mad_u64_u32 %0, vcc, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c) : "vcc");
+    return r;
+}
+template <bool SB>
+__device__ __forceinline__ uint64_t mul64_pin(uint32_t a, uint32_t b) {
+    uint64_t r;
+    if constexpr (SB)
+        asm("v_mad_u64_u32 %0, vcc, %1, %2, 0" : "=v"(r) : "v"(a), "s"(b) : "vcc");
+    else
+        asm("v_mad_u64_u32 %0, vcc, %1, %2, 0" : "=v"(r) : "v"(a), "v"(b) : "vcc");
+    return r;
+}
 
 // ---- LDS transposes ---------------------------------------------------------
 // Row padding of one word per 32 (addr = j + j/32) makes every layout's access
@@ -138,10 +160,17 @@ __device__ __forceinline__ void transpose(uint32_t (&x)[kRegs], uint32_t* lds, u
 // (Q < 2^27) through stages 0..9; stage 10 brings a back under 2Q and emits
 // [0, 4Q).  Shoup's product is formed negated so both outputs take one
 // instruction.  The inverse (GS) keeps values in [0, 2Q).
+// Forward twiddle pairs hold { -w mod 2^32, floor(w 2^32 / Q) }: the negated
+// Shoup product -T = q*Q - b*w is then two pinned multiply-adds.
+template <bool SW>
+__device__ __forceinline__ uint32_t shoup_neg(uint32_t b, uint2 w, uint32_t Q) {
+    const uint32_t q = __umulhi(b, w.y);
+    return (uint32_t)mad64_pin<true>(q, Q, mul64_pin<SW>(b, w.x));   // -T, T in [0, 2Q)
+}
+template <bool SW = false>
 __device__ __forceinline__ void ct_bfly_lazy(uint32_t& a, uint32_t& b, uint2 w, uint32_t Q) {
     const uint32_t X = a;
-    const uint32_t q = __umulhi(b, w.y);
-    const uint32_t Tn = q * Q - b * w.x;                         // -T, T in [0, 2Q)
+    const uint32_t Tn = shoup_neg<SW>(b, w, Q);
     a = X - Tn;                                                  // X + T
     b = X + Tn + 2u * Q;                                         // X - T + 2Q
 }
@@ -151,25 +180,19 @@ __device__ __forceinline__ void ct_bfly_last(uint32_t& a, uint32_t& b, uint2 w, 
     X = min(X, X - 8u * Q);
     X = min(X, X - 4u * Q);
     X = min(X, X - 2u * Q);                                      // [0, 2Q)
-    const uint32_t q = __umulhi(b, w.y);
-    const uint32_t Tn = q * Q - b * w.x;
+    const uint32_t Tn = shoup_neg<false>(b, w, Q);
     a = X - Tn;                                                  // [0, 4Q)
     b = X + Tn + 2u * Q;                                         // (0, 4Q)
 }
-__device__ __forceinline__ void ct_bfly(uint32_t& a, uint32_t& b, uint2 w, uint32_t Q) {
-    const uint32_t X = min(a, a - 2u * Q);                      // [0, 2Q)
-    const uint32_t q = __umulhi(b, w.y);
-    const uint32_t Tn = q * Q - b * w.x;                         // -(b*w mod~ Q), T in [0, 2Q)
-    a = X - Tn;                                                  // X + T      in [0, 4Q)
-    b = X + Tn + 2u * Q;                                         // X - T + 2Q in (0, 4Q)
-}
+// inverse twiddle pairs are { w, floor(w 2^32 / Q) } (not negated)
+template <bool SW = false>
 __device__ __forceinline__ void gs_bfly(uint32_t& a, uint32_t& b, uint2 w, uint32_t Q) {
     const uint32_t lo = a, hi = b;                               // [0, 2Q)
     const uint32_t s = lo + hi;
     a = min(s, s - 2u * Q);                                      // [0, 2Q)
     const uint32_t d = lo - hi + 2u * Q;                         // (0, 4Q)
     const uint32_t q = __umulhi(d, w.y);
-    b = d * w.x - q * Q;                                         // [0, 2Q)
+    b = (uint32_t)mad64_pin<true>(q, 0u - Q, mul64_pin<SW>(d, w.x));   // d*w - q*Q in [0, 2Q)
 }
 // [0, 4Q) -> [0, Q)
 __device__ __forceinline__ uint32_t canon4(uint32_t x, uint32_t Q) {
@@ -276,7 +299,7 @@ __device__ __forceinline__ void ntt_fwd(uint32_t (&x)[kRegs], uint32_t* lds, con
         for (int r = 0; r < kRegs; ++r) {
             if (r & h) continue;
             const uint2 w = twc[(1 << s) + (r >> (5 - s))];
-            ct_bfly_lazy(x[r], x[r + h], w, Q);
+            ct_bfly_lazy<true>(x[r], x[r + h], w, Q);
         }
         sched_fence();
     }
@@ -338,7 +361,7 @@ __device__ __forceinline__ void ntt_inv_noscale(uint32_t (&x)[kRegs], uint32_t* 
         for (int r = 0; r < kRegs; ++r) {
             if (r & h) continue;
             const uint2 w = twc[(1 << (10 - b)) + (r >> (b - 5))];
-            gs_bfly(x[r], x[r + h], w, Q);
+            gs_bfly<true>(x[r], x[r + h], w, Q);
         }
         sched_fence();
     }

@@ -86,6 +86,7 @@ struct StepArgs {
     const uint32_t* key2;      // ev2 = (*ek)[u][1][i] (XZW)
     const uint32_t* keys;      // evs = (*ek)[0][0][n] (first step)
     const uint32_t* pkey;      // [k][dg][N]
+    uint32_t* deff;            // [B][dg][N] per-gate scratch: d_i of this step (XZW, not first)
     const uint32_t* img;       // table image [kImgWords]
     const uint2* tw_fwd;       // [N] reference forward table (pass A, scalar reads)
     const uint2* tw_inv;       // [N]
@@ -203,18 +204,22 @@ template <int DG, int METHOD, bool FIRST, bool START>
 __device__ __forceinline__ void mac_digit(const uint32_t (&g)[kRegs], int i, uint32_t u, uint64_t (&uj)[kRegs],
                                           uint64_t (&sv)[kRegs], __amdgpu_buffer_rsrc_t rk1,
                                           __amdgpu_buffer_rsrc_t rk2, __amdgpu_buffer_rsrc_t rks,
-                                          __amdgpu_buffer_rsrc_t rpk, __amdgpu_buffer_rsrc_t rin, const uint2* psi,
-                                          const Mono& mp, const Mono& mn, uint32_t vo, uint32_t Q) {
+                                          __amdgpu_buffer_rsrc_t rpk, __amdgpu_buffer_rsrc_t rin,
+                                          __amdgpu_buffer_rsrc_t rd, const uint2* psi, const Mono& mp,
+                                          const Mono& mn, uint32_t vo, uint32_t Q) {
     const uint32_t polyB = kN * 4u;
-    const uint32_t koff = (uint32_t)(2 * i) * polyB;
+    // XZW steps after the first read d_i from the per-gate scratch written by
+    // precompute_d (the same d_i serves all k parties)
+    constexpr bool kDPre = METHOD == XZW && !FIRST;
+    const uint32_t koff = kDPre ? (uint32_t)i * polyB : (uint32_t)(2 * i) * polyB;
     const uint32_t poff = (u * DG + (uint32_t)i) * polyB;
     constexpr int kPrefetch = Prefetch<DG>::value;
     KeyGroup kg[kPrefetch + 1];
     auto issue = [&](KeyGroup& t, int gq) {
         const uint32_t go = gq * 1024u;
-        t.k1 = bload4(rk1, vo, koff + go);
+        t.k1 = bload4(kDPre ? rd : rk1, vo, koff + go);
         t.pk = bload4(rpk, vo, poff + go);
-        if (METHOD == XZW) t.k2 = bload4(rk2, vo, koff + go);
+        if (METHOD == XZW && !kDPre) t.k2 = bload4(rk2, vo, koff + go);
         if (FIRST) t.ks = bload4(rks, vo, koff + go);
         if (START && !FIRST) t.acc = bload4(rin, vo, u * polyB + go);
     };
@@ -227,7 +232,8 @@ __device__ __forceinline__ void mac_digit(const uint32_t (&g)[kRegs], int i, uin
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const int r = 4 * gq + e;
-            const uint32_t deff = key_eff<METHOD, FIRST>(t.k1[e], t.k2[e], t.ks[e], psi, mp, mn, r, Q);
+            const uint32_t deff =
+                kDPre ? t.k1[e] : key_eff<METHOD, FIRST>(t.k1[e], t.k2[e], t.ks[e], psi, mp, mn, r, Q);
             uj[r] = mad64(g[r], deff, START ? (uint64_t)(FIRST ? 0u : t.acc[e]) : uj[r]);
             sv[r] = mad64(g[r], t.pk[e], sv[r]);
         }
@@ -285,8 +291,33 @@ struct StepCtx {
     SddConsts sd;
     Mono mp, mn;
     uint32_t l, vo;
-    __amdgpu_buffer_rsrc_t rin, rout, rk1, rk2, rks, rpk;
+    __amdgpu_buffer_rsrc_t rin, rout, rk1, rk2, rks, rpk, rd;
 };
+
+// d_i = ev1_i - ev2_i * X^-c for all digits i into the gate's scratch
+// (xzw.cpp:322-325): computed once per step instead of once per party.
+// Each lane later reads back exactly the words it wrote.
+template <int DG>
+__device__ __forceinline__ void precompute_d(const StepCtx& s, uint32_t Q) {
+    const uint32_t polyB = kN * 4u;
+#pragma unroll 1
+    for (int i = 0; i < DG; ++i) {
+        u32x4 k1[8], k2[8];
+#pragma unroll
+        for (int gq = 0; gq < 8; ++gq) {
+            k1[gq] = bload4(s.rk1, s.vo, (uint32_t)(2 * i) * polyB + gq * 1024u);
+            k2[gq] = bload4(s.rk2, s.vo, (uint32_t)(2 * i) * polyB + gq * 1024u);
+        }
+#pragma unroll
+        for (int gq = 0; gq < 8; ++gq) {
+            u32x4 t;
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                t[e] = key_eff<XZW, false>(k1[gq][e], k2[gq][e], 0u, s.tb.psi, s.mp, s.mn, 4 * gq + e, Q);
+            bstore4(t, s.rd, s.vo, (uint32_t)i * polyB + gq * 1024u);
+        }
+    }
+}
 
 // One party u of HbProd (mk-acc-xzw.cpp:245-270) fused with AddToAccXZW's
 // rotation and final add (xzw.cpp:336-344):
@@ -329,16 +360,16 @@ __device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_
     }
     ntt_fwd(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, s.l, Q);
     digit_range<DG>(x, Q);
-    mac_digit<DG, METHOD, FIRST, true>(x, 0, u, uj, sv, s.rk1, s.rk2, s.rks, s.rpk, s.rin, s.tb.psi, s.mp, s.mn,
-                                       s.vo, Q);
+    mac_digit<DG, METHOD, FIRST, true>(x, 0, u, uj, sv, s.rk1, s.rk2, s.rks, s.rpk, s.rin, s.rd, s.tb.psi, s.mp,
+                                       s.mn, s.vo, Q);
 #pragma unroll kDigitUnroll
     for (int i = 1; i < DG; ++i) {
 #pragma unroll
         for (int r = 0; r < kRegs; ++r) x[r] = pd.get(r, i + 1, s.sd);
         ntt_fwd(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, s.l, Q);
         digit_range<DG>(x, Q);
-        mac_digit<DG, METHOD, FIRST, false>(x, i, u, uj, sv, s.rk1, s.rk2, s.rks, s.rpk, s.rin, s.tb.psi, s.mp,
-                                            s.mn, s.vo, Q);
+        mac_digit<DG, METHOD, FIRST, false>(x, i, u, uj, sv, s.rk1, s.rk2, s.rks, s.rpk, s.rin, s.rd, s.tb.psi,
+                                            s.mp, s.mn, s.vo, Q);
     }
     // acc_u <- uj_u (canonical); sumV reduced per party
 #pragma unroll
@@ -395,7 +426,9 @@ __global__ __launch_bounds__(kThreads, 2) void mk_step_kernel(StepArgs a) {
                     make_rsrc(a.key1, DG * 2 * polyB),
                     make_rsrc(a.key2, DG * 2 * polyB),
                     make_rsrc(a.keys, DG * 2 * polyB),
-                    make_rsrc(a.pkey, k * DG * polyB)};
+                    make_rsrc(a.pkey, k * DG * polyB),
+                    make_rsrc(a.deff + (size_t)gate * DG * kN, DG * polyB)};
+    if (METHOD == XZW && !FIRST) precompute_d<DG>(s, Q);
 
     uint64_t sv[kRegs];
 #pragma unroll
@@ -580,7 +613,7 @@ struct mkacc_ctx {
     uint32_t* d_acc0 = nullptr;
     uint32_t* d_acc1 = nullptr;
     uint32_t* d_cvals = nullptr;
-    uint32_t* d_sumv = nullptr;
+    uint32_t* d_deff = nullptr;   // [B][dg][N] step scratch (d_i shared by the k parties)
     // host-pointer API staging
     size_t io_B = 0;
     uint32_t* d_ct = nullptr;
@@ -615,14 +648,14 @@ int ensure_ws(mkacc_ctx* c, size_t B) {
     if (c->d_acc0) HIP_TRY(hipFree(c->d_acc0));
     if (c->d_acc1) HIP_TRY(hipFree(c->d_acc1));
     if (c->d_cvals) HIP_TRY(hipFree(c->d_cvals));
-    if (c->d_sumv) HIP_TRY(hipFree(c->d_sumv));
-    c->d_acc0 = c->d_acc1 = c->d_cvals = c->d_sumv = nullptr;
+    if (c->d_deff) HIP_TRY(hipFree(c->d_deff));
+    c->d_acc0 = c->d_acc1 = c->d_cvals = c->d_deff = nullptr;
     c->ws_B = 0;
     const size_t accw = B * c->p.k * (size_t)kN;
     HIP_TRY(hipMalloc(&c->d_acc0, accw * 4));
     HIP_TRY(hipMalloc(&c->d_acc1, accw * 4));
     HIP_TRY(hipMalloc(&c->d_cvals, B * c->p.k * (size_t)c->p.n * 4));
-    HIP_TRY(hipMalloc(&c->d_sumv, B * (size_t)kN * 4));
+    HIP_TRY(hipMalloc(&c->d_deff, B * c->dg * (size_t)kN * 4));
     c->ws_B = B;
     return MKACC_OK;
 }
@@ -647,6 +680,7 @@ uint32_t* launch_steps(mkacc_ctx* c, size_t B) {
             a.key2 = c->nk == 2 ? key_step(c, u, i, 1) : a.key1;
             a.keys = key_step(c, 0, n, 0);
             a.pkey = c->d_pkey;
+            a.deff = c->d_deff;
             a.tw_fwd = c->d_twf;
             a.tw_inv = c->d_twi;
             a.img = c->d_img;
@@ -983,6 +1017,7 @@ int mkacc_create(const mkacc_params* pin, int device, mkacc_ctx** out) {
         for (uint32_t i = 0; i < 2u * kN; ++i) { pw[i] = e; e = mulmod(e, psi, Q); }
     }
     auto htf = shoup_table(tf, p.Q), hti = shoup_table(ti, p.Q), hpw = shoup_table(pw, p.Q);
+    for (uint2& t : htf) t.x = 0u - t.x;   // forward pairs carry -w (ct_bfly_lazy's negated product)
     HIP_TRY(hipMalloc(&c->d_twf, htf.size() * sizeof(uint2)));
     HIP_TRY(hipMalloc(&c->d_twi, hti.size() * sizeof(uint2)));
     // LDS image: per-lane twiddle runs of both directions + swizzled psi table
@@ -1012,7 +1047,7 @@ void mkacc_destroy(mkacc_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (void* p : {(void*)c->d_twf, (void*)c->d_twi, (void*)c->d_img, (void*)c->d_keys, (void*)c->d_pkey,
-                    (void*)c->d_acc0, (void*)c->d_acc1, (void*)c->d_cvals, (void*)c->d_sumv, (void*)c->d_ct,
+                    (void*)c->d_acc0, (void*)c->d_acc1, (void*)c->d_cvals, (void*)c->d_deff, (void*)c->d_ct,
                     (void*)c->d_io, (void*)c->d_ksk, (void*)c->d_lweA, (void*)c->d_lweB, (void*)c->d_tv,
                     (void*)c->d_digits, (void*)c->d_bh, (void*)c->d_gin, (void*)c->d_gout})
         if (p) (void)hipFree(p);
