@@ -200,7 +200,12 @@ struct KeyGroup {
 // START (digit 0): uj_u starts from acc_u (AddToAccXZW's acc + acctemp,
 // xzw.cpp:342-344), streamed in with the keys; 0 in the FIRST step, where
 // AddToAccXZW0 overwrites acc (xzw.cpp:380).
-template <int DG, int METHOD, bool FIRST, bool START>
+// How a party pass obtains d_i of an XZW step after the first (xzw.cpp:322-325),
+// which is the same for all k parties: the first party computes it and stores
+// it to the gate's scratch, later parties load it back.
+enum DMode { D_COMPUTE = 0, D_STORE = 1, D_LOAD = 2 };
+
+template <int DG, int METHOD, bool FIRST, bool START, int DM>
 __device__ __forceinline__ void mac_digit(const uint32_t (&g)[kRegs], int i, uint32_t u, uint64_t (&uj)[kRegs],
                                           uint64_t (&sv)[kRegs], __amdgpu_buffer_rsrc_t rk1,
                                           __amdgpu_buffer_rsrc_t rk2, __amdgpu_buffer_rsrc_t rks,
@@ -208,18 +213,16 @@ __device__ __forceinline__ void mac_digit(const uint32_t (&g)[kRegs], int i, uin
                                           __amdgpu_buffer_rsrc_t rd, const uint2* psi, const Mono& mp,
                                           const Mono& mn, uint32_t vo, uint32_t Q) {
     const uint32_t polyB = kN * 4u;
-    // XZW steps after the first read d_i from the per-gate scratch written by
-    // precompute_d (the same d_i serves all k parties)
-    constexpr bool kDPre = METHOD == XZW && !FIRST;
-    const uint32_t koff = kDPre ? (uint32_t)i * polyB : (uint32_t)(2 * i) * polyB;
+    constexpr bool kDLoad = DM == D_LOAD;
+    const uint32_t koff = (uint32_t)(2 * i) * polyB, doff = (uint32_t)i * polyB;
     const uint32_t poff = (u * DG + (uint32_t)i) * polyB;
     constexpr int kPrefetch = Prefetch<DG>::value;
     KeyGroup kg[kPrefetch + 1];
     auto issue = [&](KeyGroup& t, int gq) {
         const uint32_t go = gq * 1024u;
-        t.k1 = bload4(kDPre ? rd : rk1, vo, koff + go);
+        t.k1 = kDLoad ? bload4(rd, vo, doff + go) : bload4(rk1, vo, koff + go);
         t.pk = bload4(rpk, vo, poff + go);
-        if (METHOD == XZW && !kDPre) t.k2 = bload4(rk2, vo, koff + go);
+        if (METHOD == XZW && !kDLoad) t.k2 = bload4(rk2, vo, koff + go);
         if (FIRST) t.ks = bload4(rks, vo, koff + go);
         if (START && !FIRST) t.acc = bload4(rin, vo, u * polyB + go);
     };
@@ -229,14 +232,17 @@ __device__ __forceinline__ void mac_digit(const uint32_t (&g)[kRegs], int i, uin
     for (int gq = 0; gq < 8; ++gq) {
         if (gq + kPrefetch < 8) issue(kg[(gq + kPrefetch) % (kPrefetch + 1)], gq + kPrefetch);
         const KeyGroup& t = kg[gq % (kPrefetch + 1)];
+        u32x4 dd;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const int r = 4 * gq + e;
             const uint32_t deff =
-                kDPre ? t.k1[e] : key_eff<METHOD, FIRST>(t.k1[e], t.k2[e], t.ks[e], psi, mp, mn, r, Q);
+                kDLoad ? t.k1[e] : key_eff<METHOD, FIRST>(t.k1[e], t.k2[e], t.ks[e], psi, mp, mn, r, Q);
+            dd[e] = deff;
             uj[r] = mad64(g[r], deff, START ? (uint64_t)(FIRST ? 0u : t.acc[e]) : uj[r]);
             sv[r] = mad64(g[r], t.pk[e], sv[r]);
         }
+        if (DM == D_STORE) bstore4(dd, rd, vo, doff + gq * 1024u);
         sched_fence();
     }
 }
@@ -294,38 +300,13 @@ struct StepCtx {
     __amdgpu_buffer_rsrc_t rin, rout, rk1, rk2, rks, rpk, rd;
 };
 
-// d_i = ev1_i - ev2_i * X^-c for all digits i into the gate's scratch
-// (xzw.cpp:322-325): computed once per step instead of once per party.
-// Each lane later reads back exactly the words it wrote.
-template <int DG>
-__device__ __forceinline__ void precompute_d(const StepCtx& s, uint32_t Q) {
-    const uint32_t polyB = kN * 4u;
-#pragma unroll 1
-    for (int i = 0; i < DG; ++i) {
-        u32x4 k1[8], k2[8];
-#pragma unroll
-        for (int gq = 0; gq < 8; ++gq) {
-            k1[gq] = bload4(s.rk1, s.vo, (uint32_t)(2 * i) * polyB + gq * 1024u);
-            k2[gq] = bload4(s.rk2, s.vo, (uint32_t)(2 * i) * polyB + gq * 1024u);
-        }
-#pragma unroll
-        for (int gq = 0; gq < 8; ++gq) {
-            u32x4 t;
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-                t[e] = key_eff<XZW, false>(k1[gq][e], k2[gq][e], 0u, s.tb.psi, s.mp, s.mn, 4 * gq + e, Q);
-            bstore4(t, s.rd, s.vo, (uint32_t)i * polyB + gq * 1024u);
-        }
-    }
-}
-
 // One party u of HbProd (mk-acc-xzw.cpp:245-270) fused with AddToAccXZW's
 // rotation and final add (xzw.cpp:336-344):
 //   uj_u = (FIRST ? 0 : acc_u) + sum_i NTT(g_i) * d_i,   g = SDD(iNTT(acc_u * (X^c - 1)))
 //   sv  += sum_i NTT(g_i) * P[u][i]
 // Party `index` is processed last (LAST): its sum stays in registers (`keep`)
 // and receives the f-part of HbProd before the single store.
-template <int DG, int METHOD, bool FIRST, bool LAST>
+template <int DG, int METHOD, bool FIRST, bool LAST, int DM>
 __device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_t (&sv)[kRegs],
                                            uint32_t (&keep)[kRegs]) {
     constexpr int kDigitUnroll = 1;
@@ -360,7 +341,7 @@ __device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_
     }
     ntt_fwd(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, s.l, Q);
     digit_range<DG>(x, Q);
-    mac_digit<DG, METHOD, FIRST, true>(x, 0, u, uj, sv, s.rk1, s.rk2, s.rks, s.rpk, s.rin, s.rd, s.tb.psi, s.mp,
+    mac_digit<DG, METHOD, FIRST, true, DM>(x, 0, u, uj, sv, s.rk1, s.rk2, s.rks, s.rpk, s.rin, s.rd, s.tb.psi, s.mp,
                                        s.mn, s.vo, Q);
 #pragma unroll kDigitUnroll
     for (int i = 1; i < DG; ++i) {
@@ -368,7 +349,7 @@ __device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_
         for (int r = 0; r < kRegs; ++r) x[r] = pd.get(r, i + 1, s.sd);
         ntt_fwd(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, s.l, Q);
         digit_range<DG>(x, Q);
-        mac_digit<DG, METHOD, FIRST, false>(x, i, u, uj, sv, s.rk1, s.rk2, s.rks, s.rpk, s.rin, s.rd, s.tb.psi,
+        mac_digit<DG, METHOD, FIRST, false, DM>(x, i, u, uj, sv, s.rk1, s.rk2, s.rks, s.rpk, s.rin, s.rd, s.tb.psi,
                                             s.mp, s.mn, s.vo, Q);
     }
     // acc_u <- uj_u (canonical); sumV reduced per party
@@ -428,17 +409,27 @@ __global__ __launch_bounds__(kThreads, 2) void mk_step_kernel(StepArgs a) {
                     make_rsrc(a.keys, DG * 2 * polyB),
                     make_rsrc(a.pkey, k * DG * polyB),
                     make_rsrc(a.deff + (size_t)gate * DG * kN, DG * polyB)};
-    if (METHOD == XZW && !FIRST) precompute_d<DG>(s, Q);
 
     uint64_t sv[kRegs];
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) sv[r] = 0;
     uint32_t keep[kRegs];
-    for (uint32_t t = 1; t < k; ++t) {
-        const uint32_t u = index + t < k ? index + t : index + t - k;
-        party_pass<DG, METHOD, FIRST, false>(s, u, sv, keep);
+    if constexpr (METHOD == XZW && !FIRST) {
+        // d_i is the same for all parties: the first pass computes and stores
+        // it, the later ones load it (k == 1: the single pass computes it)
+        if (k == 1) {
+            party_pass<DG, METHOD, FIRST, true, D_COMPUTE>(s, index, sv, keep);
+        } else {
+            party_pass<DG, METHOD, FIRST, false, D_STORE>(s, index + 1 < k ? index + 1 : index + 1 - k, sv, keep);
+            for (uint32_t t = 2; t < k; ++t)
+                party_pass<DG, METHOD, FIRST, false, D_LOAD>(s, index + t < k ? index + t : index + t - k, sv, keep);
+            party_pass<DG, METHOD, FIRST, true, D_LOAD>(s, index, sv, keep);
+        }
+    } else {
+        for (uint32_t t = 1; t < k; ++t) party_pass<DG, METHOD, FIRST, false, D_COMPUTE>(s, index + t < k ? index + t : index + t - k, sv,
+                                                                 keep);
+        party_pass<DG, METHOD, FIRST, true, D_COMPUTE>(s, index, sv, keep);
     }
-    party_pass<DG, METHOD, FIRST, true>(s, index, sv, keep);
 
     // second half of HbProd: iNTT(sumV) -> SDD -> NTT -> acc[index] += <., f>
     uint32_t x[kRegs];
