@@ -10,7 +10,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libmkfhe_amd.so")
+# MKFHE_LIB: load another build of the engine (A/B timing of kernel variants)
+LIB_PATH = os.environ.get("MKFHE_LIB") or os.path.join(_HERE, "lib", "libmkfhe_amd.so")
 
 MKACC_OK = 0
 MKACC_E_ARG = -1

@@ -27,6 +27,7 @@ constexpr int kRegs = 32;          // residues per lane
 struct Mod {
     uint32_t Q;      // modulus, 2^26 < Q < 2^27
     uint32_t mu;     // floor(2^58 / Q)
+    uint32_t r32;    // 2^32 mod Q
 };
 
 // ---- buffer-resource memory access -------------------------------------------
@@ -72,6 +73,13 @@ __device__ __forceinline__ uint32_t reduce58(uint64_t x, const Mod& m) {
     uint32_t q = __umulhi(xh, m.mu);
     uint32_t r = (uint32_t)x - q * m.Q;   // in [0, 3Q)
     r = min(r, r - m.Q);
+    return min(r, r - m.Q);
+}
+// ... to [0, 2Q) (the accumulator between steps is kept in this range)
+__device__ __forceinline__ uint32_t reduce58_lazy(uint64_t x, const Mod& m) {
+    uint32_t xh = (uint32_t)(x >> 26);
+    uint32_t q = __umulhi(xh, m.mu);
+    uint32_t r = (uint32_t)x - q * m.Q;   // in [0, 3Q)
     return min(r, r - m.Q);
 }
 __device__ __forceinline__ uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {

@@ -79,7 +79,7 @@ __host__ __device__ __forceinline__ uint32_t psi_pos(uint32_t e) { return e ^ ((
 enum { XZW = 0, XZW_B = 1 };
 
 struct StepArgs {
-    const uint32_t* acc_in;    // [B][k][N] C4, scaled by N^-1
+    const uint32_t* acc_in;    // [B][k][N] C4, scaled by N^-1, residues in [0, 2Q)
     uint32_t* acc_out;         // [B][k][N]
     const uint32_t* cvals;     // [B] monomial exponents c of this step, in [0, 2N)
     const uint32_t* key1;      // ev1 = (*ek)[u][0][i] : [dg][2][N] C4
@@ -146,7 +146,8 @@ __device__ __forceinline__ Mono make_mono(uint32_t c, uint32_t l) {
 
 // Lazy Shoup product x*w in [0, 2Q) (x < 2^32)
 __device__ __forceinline__ uint32_t mul_shoup_lazy(uint32_t x, uint2 w, uint32_t Q) {
-    return x * w.x - __umulhi(x, w.y) * Q;
+    const uint32_t q = __umulhi(x, w.y);
+    return (uint32_t)mad64_pin<true>(q, 0u - Q, mul64_pin<false>(x, w.x));   // x*w - q*Q
 }
 
 // effective key word d_i / f_i of mk-acc-xzw(_B).cpp AddToAccXZW{,0}, canonical
@@ -216,7 +217,8 @@ __device__ __forceinline__ void mac_digit(const uint32_t (&g)[kRegs], int i, uin
     constexpr bool kDLoad = DM == D_LOAD;
     const uint32_t koff = (uint32_t)(2 * i) * polyB, doff = (uint32_t)i * polyB;
     const uint32_t poff = (u * DG + (uint32_t)i) * polyB;
-    constexpr int kPrefetch = Prefetch<DG>::value;
+    // loading d_i instead of two key words frees the registers for a deeper pipeline
+    constexpr int kPrefetch = DM == D_LOAD && DG <= 3 ? 3 : Prefetch<DG>::value;
     KeyGroup kg[kPrefetch + 1];
     auto issue = [&](KeyGroup& t, int gq) {
         const uint32_t go = gq * 1024u;
@@ -320,12 +322,12 @@ __device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_
     }
     if (!FIRST) {
         // acctemp = acc * (X^c - 1)                     (xzw.cpp:336-338)
-        // x canonical -> x*X^c - x + Q in (0, 3Q) -> [0, 2Q)
+        // x in [0, 2Q) -> x*X^c - x + 2Q in (0, 4Q) -> [0, 2Q)
 #pragma unroll
         for (int r0 = 0; r0 < kRegs; r0 += 8) {
 #pragma unroll
             for (int r = r0; r < r0 + 8; ++r) {
-                const uint32_t y = mul_shoup_lazy(x[r], s.mp.at(s.tb.psi, r), Q) + Q - x[r];
+                const uint32_t y = mul_shoup_lazy(x[r], s.mp.at(s.tb.psi, r), Q) + 2u * Q - x[r];
                 x[r] = min(y, y - 2u * Q);
             }
             sched_fence();
@@ -359,8 +361,14 @@ __device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const int r = 4 * gq + e;
-            t[e] = reduce58(uj[r], s.m);
-            sv[r] = reduce58(sv[r], s.m);
+            t[e] = reduce58_lazy(uj[r], s.m);
+            // sumV: a full reduction only before its iNTT; in between, folding the
+            // high word (hi * 2^32 mod Q, < 2^53) keeps the next party's DG <= 3
+            // products under reduce58's 2^58
+            if (LAST || DG > 3)
+                sv[r] = reduce58(sv[r], s.m);
+            else
+                sv[r] = mad64((uint32_t)(sv[r] >> 32), s.m.r32, (uint32_t)sv[r]);
             if (LAST) keep[r] = t[e];
         }
         if (!LAST) bstore4(t, s.rout, s.vo, u * polyB + gq * 1024u);
@@ -460,7 +468,7 @@ __global__ __launch_bounds__(kThreads, 2) void mk_step_kernel(StepArgs a) {
     for (int gq = 0; gq < 8; ++gq) {
         u32x4 t;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) t[e] = reduce58(w[4 * gq + e], s.m);
+        for (int e = 0; e < 4; ++e) t[e] = reduce58_lazy(w[4 * gq + e], s.m);
         bstore4(t, s.rout, s.vo, ioff + gq * 1024u);
     }
 }
@@ -973,6 +981,7 @@ int mkacc_create(const mkacc_params* pin, int device, mkacc_ctx** out) {
     c->nk = c->method_class == XZW ? 2 : 1;
     c->mod.Q = (uint32_t)p.Q;
     c->mod.mu = (uint32_t)((1ull << 58) / p.Q);
+    c->mod.r32 = (uint32_t)((1ull << 32) % p.Q);
     {
         // offset-word digit decomposition constants (mkacc_device.hpp)
         const uint32_t b = (uint32_t)__builtin_ctz(p.baseG);
