@@ -1,0 +1,55 @@
+// boolean-mklwe on the MI355X engine: the reference example
+// (src/binfhe/examples/boolean-mklwe.cpp) against the C++ mirror
+// include/mkfhe_amd_binfhe.hpp, for all four input pairs.  Exit status 0 iff
+// every NAND decrypts correctly.
+//
+//   g++ -std=c++17 -O2 -Iinclude examples/boolean-mklwe.cpp -Lmkfhe_amd/lib
+//       -lmkfhe_amd -lmkfhe_keys -Wl,-rpath,$PWD/mkfhe_amd/lib -o boolean-mklwe
+//   ./boolean-mklwe [STD100_MKNTRU_LWE|...]
+#include <cstdio>
+#include <cstring>
+#include <ctime>
+#include <iostream>
+
+#include "mkfhe_amd_binfhe.hpp"
+
+using namespace mkfhe_amd;
+using namespace std;
+
+static BINFHE_PARAMSET parse(const char* s) {
+    for (int i = STD128_MKNTRU; i <= STD100_MKNTRU_LWE_4; ++i)
+        if (!strcmp(ParamSetName((BINFHE_PARAMSET)i), s)) return (BINFHE_PARAMSET)i;
+    throw config_error(string("unknown parameter set ") + s);
+}
+
+int main(int argc, char** argv) {
+    // Sample Program: Step 1: Set CryptoContext
+    auto cc = BinFHEContext();
+    cc.GenerateBinFHEContext(argc > 1 ? parse(argv[1]) : STD100_MKNTRU_LWE, MKNTRU_LWE);
+    cout << "Generating sk" << endl;
+    auto sk = cc.MKLWE_KeyGen();
+
+    // Generate the bootstrapping keys (refresh and switching keys)
+    std::cout << "Generating the bootstrapping keys..." << std::endl;
+    cc.MKBTKeyGen(sk);
+    std::cout << "Completed the key generation." << std::endl;
+
+    int bad = 0;
+    for (int m0 = 0; m0 < 2; ++m0)
+        for (int m1 = 0; m1 < 2; ++m1) {
+            MKLWECiphertext ct1 = cc.Encrypt(sk, m0);
+            MKLWECiphertext ct2 = cc.Encrypt(sk, m1);
+            MKLWEPlaintext result;
+
+            clock_t start = clock();
+            MKLWECiphertext ctOUT = cc.EvalBinGate(NAND, ct1, ct2);
+            std::cout << "Time of gate bootstrapping:\t" << float(clock() - start) * 1000 / CLOCKS_PER_SEC << "ms"
+                      << std::endl;
+
+            cc.Decrypt(sk, ctOUT, &result);
+            std::cout << "Result of encrypted computation of ( " << m0 << " NAND " << m1 << " ) = " << result
+                      << std::endl;
+            bad += result != !(m0 & m1);
+        }
+    return bad ? 1 : 0;
+}

@@ -1,0 +1,59 @@
+// boolean-mkntru on the MI355X engine: the reference example
+// (src/binfhe/examples/boolean-mkntru.cpp) against the C++ mirror
+// include/mkfhe_amd_binfhe.hpp -- the same calls, in the same order, for all
+// four input pairs.  Exit status 0 iff every NAND decrypts correctly.
+//
+//   g++ -std=c++17 -O2 -Iinclude examples/boolean-mkntru.cpp -Lmkfhe_amd/lib
+//       -lmkfhe_amd -lmkfhe_keys -Wl,-rpath,$PWD/mkfhe_amd/lib -o boolean-mkntru
+//   ./boolean-mkntru [STD100_MKNTRU|STD128_MKNTRU|...]
+#include <cstdio>
+#include <cstring>
+#include <ctime>
+#include <iostream>
+
+#include "mkfhe_amd_binfhe.hpp"
+
+using namespace mkfhe_amd;
+using namespace std;
+
+static BINFHE_PARAMSET parse(const char* s) {
+    for (int i = STD128_MKNTRU; i <= STD100_MKNTRU_LWE_4; ++i)
+        if (!strcmp(ParamSetName((BINFHE_PARAMSET)i), s)) return (BINFHE_PARAMSET)i;
+    throw config_error(string("unknown parameter set ") + s);
+}
+
+int main(int argc, char** argv) {
+    // Sample Program: Step 1: Set CryptoContext
+    auto cc = BinFHEContext();
+    cc.GenerateBinFHEContext(argc > 1 ? parse(argv[1]) : STD100_MKNTRU, MKNTRU);
+
+    // Sample Program: Step 2: Key Generation
+    cout << "Generating sk" << endl;
+    auto sk = cc.MNTRU_KeyGen();
+    std::cout << "Generating the bootstrapping keys..." << std::endl;
+    cc.MKBTKeyGen(sk);
+    std::cout << "Completed the key generation." << std::endl;
+    cc.ctGateGen(sk, NAND);
+    std::cout << "Completed the ctNAND." << std::endl;
+
+    int bad = 0;
+    for (int m0 = 0; m0 < 2; ++m0)
+        for (int m1 = 0; m1 < 2; ++m1) {
+            // Sample Program: Step 3: Encryption
+            auto ct1 = cc.Encrypt(sk, m0);
+            auto ct2 = cc.Encrypt(sk, m1);
+
+            MNTRUPlaintext result;
+            clock_t start = clock();
+            MNTRUCiphertext ctOUT = cc.EvalBinGate(NAND, ct1, ct2);
+            clock_t end = clock();
+            std::cout << "Time of  gate bootstrapping:\t" << double(end - start) * 1000 / CLOCKS_PER_SEC << "ms"
+                      << std::endl;
+
+            cc.Decrypt(sk, ctOUT, &result);
+            std::cout << "Result of encrypted computation of ( " << m0 << " NAND " << m1 << " ) = " << result
+                      << std::endl;
+            bad += result != !(m0 & m1);
+        }
+    return bad ? 1 : 0;
+}

@@ -14,8 +14,13 @@
 //   accumulator choice by method       src/binfhe/include/binfhe-base-scheme.h:137-151
 //   OPENFHE_THROW(config_error, ...)   src/core/include/utils/exception.h:162
 //
+//   BinFHEContext MK subset            src/binfhe/include/binfhecontext.h:98-338
+//     (GenerateBinFHEContext, MNTRU_KeyGen, MKLWE_KeyGen, MKBTKeyGen, ctGateGen,
+//      Encrypt, EvalBinGate(NAND), Decrypt / Decrypt2 / DecryptNAND)
+//
 // Every evaluation runs on the HIP engine (libmkfhe_amd.so); there is no CPU
-// path.  Link with -lmkfhe_amd.  Header-only.
+// path.  Key material comes from libmkfhe_keys.so (host C++, include/mkfhe_keys.h).
+// Link with -lmkfhe_amd -lmkfhe_keys.  Header-only.
 #ifndef MKFHE_AMD_BINFHE_HPP
 #define MKFHE_AMD_BINFHE_HPP
 
@@ -29,6 +34,7 @@
 #include <vector>
 
 #include "mkfhe_amd.h"
+#include "mkfhe_keys.h"
 
 namespace mkfhe_amd {
 
@@ -385,6 +391,7 @@ inline std::shared_ptr<UniEncAccumulator> MakeUniEncAccumulator(BINFHE_METHOD me
 // =====================================================================================
 
 // binfhe-constants.h:143
+enum BINFHE_OUTPUT { INVALID_OUTPUT = 0, FRESH, BOOTSTRAPPED, LARGE_DIM, SMALL_DIM };  // binfhe-constants.h:117-123
 enum BINGATE { OR, AND, NOR, NAND, XOR_FAST, XNOR_FAST, MAJORITY, AND3, OR3, AND4, OR4, CMUX, XOR, XNOR };
 
 // The multi-key parameter sets of binfhe-constants.h:95-110 (binfhecontext.cpp:129-144)
@@ -412,6 +419,7 @@ public:
     std::vector<NativeVector>& GetElements() { return m_elements; }
     uint64_t GetModulus() const { return m_q; }
     uint64_t GetptModulus() const { return m_p; }
+    void SetptModulus(uint64_t p) { m_p = p; }
     uint32_t Getk() const { return (uint32_t)m_elements.size(); }
     uint32_t GetLength() const { return m_elements.empty() ? 0 : (uint32_t)m_elements[0].size(); }
 
@@ -432,6 +440,7 @@ public:
     uint64_t GetB() const { return m_b; }
     uint64_t GetModulus() const { return m_q; }
     uint64_t GetptModulus() const { return m_p; }
+    void SetptModulus(uint64_t p) { m_p = p; }
     uint32_t Getk() const { return (uint32_t)m_a.size(); }
     uint32_t GetLength() const { return m_a.empty() ? 0 : (uint32_t)m_a[0].size(); }
 
@@ -469,19 +478,87 @@ private:
 };
 using MKLWESwitchingKey = std::shared_ptr<const MKLWESwitchingKeyImpl>;
 
+// ---- secret keys (NTL-free generation: include/mkfhe_keys.h) --------------------------
+using MNTRUPlaintext = int64_t;
+using MKLWEPlaintext = int64_t;
+
+// MNTRUPrivateKeyImpl (mntru-privatekey.h:23-110): per party an n x n matrix F
+// and its inverse mod qKS, stored flat [k][n][n] (row l, column j).
+class MNTRUPrivateKeyImpl {
+public:
+    MNTRUPrivateKeyImpl(uint32_t k, uint32_t n, uint64_t mod, std::vector<uint32_t> F, std::vector<uint32_t> Finv)
+        : m_k(k), m_n(n), m_mod(mod), m_F(std::move(F)), m_Finv(std::move(Finv)) {}
+    uint32_t Getk() const { return m_k; }
+    uint32_t GetLength() const { return m_n; }
+    uint64_t GetModulus() const { return m_mod; }
+    const std::vector<uint32_t>& F() const { return m_F; }
+    const std::vector<uint32_t>& Finv() const { return m_Finv; }
+    // GetF_col0 (mntru-privatekey.h:56-70): the LWE-style secret, [k][n]
+    std::vector<NativeVector> GetF_col0() const {
+        std::vector<NativeVector> r(m_k, NativeVector(m_n));
+        for (uint32_t u = 0; u < m_k; ++u)
+            for (uint32_t l = 0; l < m_n; ++l) r[u][l] = m_F[((size_t)u * m_n + l) * m_n];
+        return r;
+    }
+    // GetF_inv_coli (mntru-privatekey.h:87-101): column j of every F_u^-1
+    std::vector<NativeVector> GetF_inv_coli(uint32_t j) const {
+        std::vector<NativeVector> r(m_k, NativeVector(m_n));
+        for (uint32_t u = 0; u < m_k; ++u)
+            for (uint32_t l = 0; l < m_n; ++l) r[u][l] = m_Finv[((size_t)u * m_n + l) * m_n + j];
+        return r;
+    }
+
+private:
+    uint32_t m_k, m_n;
+    uint64_t m_mod;
+    std::vector<uint32_t> m_F, m_Finv;
+};
+using MNTRUPrivateKey = std::shared_ptr<const MNTRUPrivateKeyImpl>;
+using ConstMNTRUPrivateKey = const std::shared_ptr<const MNTRUPrivateKeyImpl>;
+
+// MKLWEPrivateKeyImpl (mklwe-privatekey.h): k binary vectors of length n
+class MKLWEPrivateKeyImpl {
+public:
+    MKLWEPrivateKeyImpl(uint32_t k, uint32_t n, uint64_t mod, std::vector<uint32_t> s)
+        : m_k(k), m_n(n), m_mod(mod), m_s(std::move(s)) {}
+    uint32_t Getk() const { return m_k; }
+    uint32_t GetLength() const { return m_n; }
+    uint64_t GetModulus() const { return m_mod; }
+    const std::vector<uint32_t>& flat() const { return m_s; }
+    std::vector<NativeVector> GetElement() const {
+        std::vector<NativeVector> r(m_k, NativeVector(m_n));
+        for (uint32_t u = 0; u < m_k; ++u)
+            for (uint32_t i = 0; i < m_n; ++i) r[u][i] = m_s[(size_t)u * m_n + i];
+        return r;
+    }
+
+private:
+    uint32_t m_k, m_n;
+    uint64_t m_mod;
+    std::vector<uint32_t> m_s;
+};
+using MKLWEPrivateKey = std::shared_ptr<const MKLWEPrivateKeyImpl>;
+using ConstMKLWEPrivateKey = const std::shared_ptr<const MKLWEPrivateKeyImpl>;
+
 // The fields of the reference UniEncBTKey (binfhe-base-scheme.h:65-83) the
-// gate path reads.
+// gate path reads.  BTKeyLoad takes the reference-shaped members; MKBTKeyGen
+// fills the flat members (the C-ABI layouts of mkfhe_amd.h / mkfhe_keys.h)
+// and uploads them without building the nested objects.
 struct UniEncBTKey {
     UniEncACCKey BSkey;
     MNTRUSwitchingKey2 KSkey2;
     MKLWESwitchingKey LKSkey;
     std::vector<std::vector<NativePoly>> Pkey;
     std::vector<NativePoly> f;
+    // flat key material from MKBTKeyGen
+    std::vector<uint32_t> crs, fvec, f_eval, finv_eval, pkey, evk, ksk, ksk_a, ksk_b;
 };
 
-// BinFHEContext subset for multi-key NAND gates on one MI355X.  Key generation
-// (MNTRU_KeyGen / MKBTKeyGen / ctGateGen) needs NTL in the reference and is
-// not part of this engine: keys are loaded with BTKeyLoad / SetctNAND.
+// BinFHEContext for multi-key NAND gates on one MI355X, with the reference's
+// key-generation / encryption / decryption calls (binfhecontext.h:98-338) over
+// libmkfhe_keys.so and the gates over libmkfhe_amd.so.  The device context is
+// created on first use, so key generation, encryption and decryption run on a
+// host without a GPU.
 class BinFHEContext {
 public:
     void GenerateBinFHEContext(BINFHE_PARAMSET set, BINFHE_METHOD method, int device = 0) {
@@ -489,28 +566,138 @@ public:
             throw config_error("method is invalid");
         m_method = method;
         m_params = UniEncCryptoParams::FromParamSet(ParamSetName(set), method);
-        m_dc = std::make_unique<DeviceContext>(m_params->abi(), device);
-        m_params->set_abi(m_dc->params());
-        m_keys = false;
-        m_ctNAND.reset();
+        check(mkkg_paramset(ParamSetName(set), to_abi_method(method), &m_kp));
+        m_have_kp = true;
+        reset(device);
     }
-    // custom parameters (the reference's explicit-parameter overload, binfhecontext.h:94)
+    // custom parameters (the reference's explicit-parameter overload, binfhecontext.h:94);
+    // key generation then needs SetKeyParams.
     void GenerateBinFHEContext(const UniEncCryptoParams& params, int device = 0) {
         m_method = params.GetMethod();
         m_params = std::make_shared<UniEncCryptoParams>(params);
-        m_dc = std::make_unique<DeviceContext>(m_params->abi(), device);
-        m_params->set_abi(m_dc->params());
-        m_keys = false;
-        m_ctNAND.reset();
+        m_have_kp = false;
+        reset(device);
+        dc();  // validates the parameters and derives digitsG / root (mkacc_create)
     }
+    void SetKeyParams(const mkkg_params& kp) {
+        m_kp = kp;
+        m_have_kp = true;
+    }
+    // Extension: seed of the key/encryption sampler (0 = random, the reference's behaviour).
+    void SetSeed(uint64_t seed) { m_seed = seed; }
     const std::shared_ptr<UniEncCryptoParams>& GetParams() const { return m_params; }
     // modKS = mod and baseKS = 32 in every MK set (binfhecontext.cpp:129-144)
-    mkacc_ks_params GetKSParams() const { return mkacc_ks_params{m_params->Getq(), 32, m_params->GetLatticeParam()}; }
+    mkacc_ks_params GetKSParams() const {
+        if (m_have_kp) return m_kp.ks;
+        return mkacc_ks_params{m_params->Getq(), 32, m_params->GetLatticeParam()};
+    }
 
+    // ---- key generation (binfhecontext.cpp:235-250, 520-575) ----
+    MNTRUPrivateKey MNTRU_KeyGen() const {
+        need_keyparams();
+        const uint32_t k = m_kp.acc.k, n = m_kp.acc.n;
+        std::vector<uint32_t> F((size_t)k * n * n), Fi((size_t)k * n * n);
+        check(mkkg_mntru_keygen(&m_kp, next_seed(), F.data(), Fi.data()));
+        return std::make_shared<const MNTRUPrivateKeyImpl>(k, n, m_kp.ks.qKS, std::move(F), std::move(Fi));
+    }
+    MKLWEPrivateKey MKLWE_KeyGen() const {
+        need_keyparams();
+        if (m_kp.lwe_keydist != MKKG_DIST_BINARY) throw config_error("Support BINARY PrivateKey Only");
+        const uint32_t k = m_kp.acc.k, n = m_kp.acc.n;
+        std::vector<uint32_t> s((size_t)k * n);
+        check(mkkg_mklwe_keygen(&m_kp, next_seed(), s.data()));
+        return std::make_shared<const MKLWEPrivateKeyImpl>(k, n, m_kp.ks.qKS, std::move(s));
+    }
+    void MKBTKeyGen(ConstMNTRUPrivateKey& sk) {
+        if (m_method == MKNTRU_LWE) throw config_error("MK-NTRU key for an MKNTRU_LWE context");
+        std::vector<uint32_t> col0((size_t)sk->Getk() * sk->GetLength());
+        const auto c = sk->GetF_col0();
+        for (uint32_t u = 0; u < sk->Getk(); ++u)
+            for (uint32_t l = 0; l < sk->GetLength(); ++l) col0[(size_t)u * sk->GetLength() + l] = (uint32_t)c[u][l];
+        UniEncBTKey ek = common_btkey(col0);
+        ek.ksk.resize(mkkg_ksk_mntru_words(&m_kp));
+        check(mkkg_ksk_mntru(&m_kp, next_seed(), ek.fvec.data(), sk->Finv().data(), ek.ksk.data()));
+        const mkacc_ks_params ks = GetKSParams();
+        check(mkacc_upload_ksk_mntru(dc().get(), &ks, ek.ksk.data()));
+        m_BTKey = std::move(ek);
+        m_keys = true;
+    }
+    void MKBTKeyGen(ConstMKLWEPrivateKey& sk) {
+        if (m_method != MKNTRU_LWE) throw config_error("MK-LWE key for an MK-NTRU context");
+        UniEncBTKey ek = common_btkey(sk->flat());
+        ek.ksk_a.resize(mkkg_ksk_mklwe_a_words(&m_kp));
+        ek.ksk_b.resize(mkkg_ksk_mklwe_b_words(&m_kp));
+        check(mkkg_ksk_mklwe(&m_kp, next_seed(), ek.fvec.data(), sk->flat().data(), ek.ksk_a.data(),
+                             ek.ksk_b.data()));
+        const mkacc_ks_params ks = GetKSParams();
+        check(mkacc_upload_ksk_mklwe(dc().get(), &ks, ek.ksk_a.data(), ek.ksk_b.data()));
+        m_BTKey = std::move(ek);
+        m_keys = true;
+    }
+    // ctGateGen (binfhe-base-scheme.cpp:340-376)
+    void ctGateGen(ConstMNTRUPrivateKey& sk, BINGATE gate) {
+        if (gate != NAND) throw config_error("Support NAND gate Only");
+        need_keyparams();
+        std::vector<uint32_t> c((size_t)sk->Getk() * sk->GetLength());
+        check(mkkg_mntru_ctgate(&m_kp, next_seed(), sk->Finv().data(), c.data()));
+        m_ctNAND = unpack_mntru(c.data(), sk->Getk(), sk->GetLength(), m_kp.acc.q);
+    }
+    const UniEncBTKey& GetBTKey() const { return m_BTKey; }
+
+    // ---- encryption / decryption (binfhecontext.cpp:276-292, 330-375) ----
+    MNTRUCiphertext Encrypt(ConstMNTRUPrivateKey& sk, MNTRUPlaintext m, BINFHE_OUTPUT output = BOOTSTRAPPED,
+                            uint32_t p = 4, uint64_t mod = 0) const {
+        (void)output;  // obsolete in the reference too (binfhecontext.cpp:268-272)
+        need_keyparams();
+        mkkg_params kp = m_kp;
+        if (mod) kp.acc.q = mod;
+        const uint32_t mm = (uint32_t)m;
+        std::vector<uint32_t> c((size_t)sk->Getk() * sk->GetLength());
+        check(mkkg_mntru_encrypt(&kp, next_seed(), sk->Finv().data(), &mm, p, 1, c.data()));
+        auto ct = unpack_mntru(c.data(), sk->Getk(), sk->GetLength(), kp.acc.q);
+        ct->SetptModulus(p);
+        return ct;
+    }
+    MKLWECiphertext Encrypt(ConstMKLWEPrivateKey& sk, MKLWEPlaintext m, BINFHE_OUTPUT output = BOOTSTRAPPED,
+                            uint32_t p = 4, uint64_t mod = 0) const {
+        (void)output;
+        need_keyparams();
+        mkkg_params kp = m_kp;
+        if (mod) kp.acc.q = mod;
+        const uint32_t mm = (uint32_t)m, k = sk->Getk(), n = sk->GetLength();
+        std::vector<uint32_t> a((size_t)k * n);
+        uint32_t b = 0;
+        check(mkkg_mklwe_encrypt(&kp, next_seed(), sk->flat().data(), &mm, p, 1, a.data(), &b));
+        std::vector<NativeVector> av(k, NativeVector(n));
+        for (uint32_t u = 0; u < k; ++u)
+            for (uint32_t i = 0; i < n; ++i) av[u][i] = a[(size_t)u * n + i];
+        auto ct = std::make_shared<MKLWECiphertextImpl>(std::move(av), b, kp.acc.q);
+        ct->SetptModulus(p);
+        return ct;
+    }
+    void Decrypt(ConstMNTRUPrivateKey& sk, ConstMNTRUCiphertext& ct, MNTRUPlaintext* result, uint32_t p = 4) const {
+        decrypt_mntru(sk, ct, result, p, MKKG_DECRYPT);
+    }
+    void Decrypt2(ConstMNTRUPrivateKey& sk, ConstMNTRUCiphertext& ct, MNTRUPlaintext* result, uint32_t p = 4) const {
+        decrypt_mntru(sk, ct, result, p, MKKG_DECRYPT2);
+    }
+    void DecryptNAND(ConstMNTRUPrivateKey& sk, ConstMNTRUCiphertext& ct, MNTRUPlaintext* result,
+                     uint32_t p = 4) const {
+        decrypt_mntru(sk, ct, result, p, MKKG_DECRYPT_NAND);
+    }
+    void Decrypt(ConstMKLWEPrivateKey& sk, ConstMKLWECiphertext& ct, MKLWEPlaintext* result, uint32_t p = 4) const {
+        decrypt_mklwe(sk, ct, result, p, MKKG_DECRYPT);
+    }
+    void DecryptNAND(ConstMKLWEPrivateKey& sk, ConstMKLWECiphertext& ct, MKLWEPlaintext* result,
+                     uint32_t p = 4) const {
+        decrypt_mklwe(sk, ct, result, p, MKKG_DECRYPT_NAND);
+    }
+
+    // ---- reference-shaped key loading (keys produced elsewhere) ----
     void BTKeyLoad(const UniEncBTKey& ek) {
         need_context();
         if (!ek.BSkey) throw config_error("BSkey is empty");
-        UniEncAccumulator::upload(*m_dc, ek.BSkey, ek.Pkey);
+        UniEncAccumulator::upload(dc(), ek.BSkey, ek.Pkey);
         const mkacc_ks_params ks = GetKSParams();
         const uint32_t k = m_params->Getk(), N = m_params->GetN(), n = ks.n_out;
         const uint32_t dks = mkacc_ks_digits(&ks);
@@ -528,7 +715,7 @@ public:
                     for (uint32_t i = 0; i < n; ++i) h[((size_t)u * N * dks + l) * n + i] = (uint32_t)row[i];
                 }
             }
-            check(mkacc_upload_ksk_mntru(m_dc->get(), &ks, h.data()));
+            check(mkacc_upload_ksk_mntru(dc().get(), &ks, h.data()));
         } else {
             if (!ek.LKSkey) throw config_error("LKSkey is empty");
             const auto& A = ek.LKSkey->GetElementsA();
@@ -545,7 +732,7 @@ public:
                             for (uint32_t i = 0; i < n; ++i) ha[r * n + i] = (uint32_t)row[i];
                             hb[r] = (uint32_t)Bk.at(u).at(j).at(d).at(t);
                         }
-            check(mkacc_upload_ksk_mklwe(m_dc->get(), &ks, ha.data(), hb.data()));
+            check(mkacc_upload_ksk_mklwe(dc().get(), &ks, ha.data(), hb.data()));
         }
         m_keys = true;
     }
@@ -578,14 +765,9 @@ public:
             pack(*ct1[b], a1.data() + b * k * n, k, n);
             pack(*ct2[b], a2.data() + b * k * n, k, n);
         }
-        check(mkacc_eval_nand_mntru(m_dc->get(), nand.data(), a1.data(), a2.data(), out.data(), B));
+        check(mkacc_eval_nand_mntru(dc().get(), nand.data(), a1.data(), a2.data(), out.data(), B));
         std::vector<MNTRUCiphertext> res(B);
-        for (size_t b = 0; b < B; ++b) {
-            std::vector<NativeVector> e(k, NativeVector(n));
-            for (uint32_t u = 0; u < k; ++u)
-                for (uint32_t i = 0; i < n; ++i) e[u][i] = out[(b * k + u) * n + i];
-            res[b] = std::make_shared<MNTRUCiphertextImpl>(std::move(e), GetKSParams().qKS);
-        }
+        for (size_t b = 0; b < B; ++b) res[b] = unpack_mntru(out.data() + b * k * n, k, n, GetKSParams().qKS);
         return res;
     }
     std::vector<MKLWECiphertext> EvalBinGate(BINGATE gate, const std::vector<MKLWECiphertext>& ct1,
@@ -602,7 +784,7 @@ public:
             b1[b] = (uint32_t)ct1[b]->GetB();
             b2[b] = (uint32_t)ct2[b]->GetB();
         }
-        check(mkacc_eval_nand_mklwe(m_dc->get(), a1.data(), b1.data(), a2.data(), b2.data(), oa.data(), ob.data(),
+        check(mkacc_eval_nand_mklwe(dc().get(), a1.data(), b1.data(), a2.data(), b2.data(), oa.data(), ob.data(),
                                     B));
         std::vector<MKLWECiphertext> res(B);
         for (size_t b = 0; b < B; ++b) {
@@ -615,8 +797,76 @@ public:
     }
 
 private:
+    void reset(int device) {
+        m_device = device;
+        m_dc.reset();
+        m_keys = false;
+        m_ctNAND.reset();
+        m_BTKey = UniEncBTKey{};
+    }
+    DeviceContext& dc() const {
+        need_context();
+        if (!m_dc) {
+            m_dc = std::make_unique<DeviceContext>(m_params->abi(), m_device);
+            m_params->set_abi(m_dc->params());
+        }
+        return *m_dc;
+    }
     void need_context() const {
-        if (!m_dc) throw config_error("call GenerateBinFHEContext first");
+        if (!m_params) throw config_error("call GenerateBinFHEContext first");
+    }
+    void need_keyparams() const {
+        need_context();
+        if (!m_have_kp) throw config_error("key parameters are not set (GenerateBinFHEContext(set) or SetKeyParams)");
+    }
+    uint64_t next_seed() const { return m_seed ? m_seed + (m_calls++) * 0x9E3779B97F4A7C15ull : 0; }
+    // CRS, ring secrets, P and the accumulator key (binfhe-base-scheme.cpp:198-338), uploaded
+    UniEncBTKey common_btkey(const std::vector<uint32_t>& lwe_sk) {
+        need_keyparams();
+        const uint32_t k = m_kp.acc.k, N = m_kp.acc.N;
+        const uint32_t dg = (m_kp.acc.digitsG ? m_kp.acc.digitsG : m_params->GetDigitsG()) - 1;
+        UniEncBTKey ek;
+        ek.crs.resize((size_t)dg * N);
+        ek.fvec.resize((size_t)k * N);
+        ek.f_eval.resize((size_t)k * N);
+        ek.finv_eval.resize((size_t)k * N);
+        ek.pkey.resize(mkkg_pkey_words(&m_kp));
+        ek.evk.resize(mkkg_evk_words(&m_kp));
+        check(mkkg_crs(&m_kp, next_seed(), ek.crs.data()));
+        check(mkkg_ring_secrets(&m_kp, next_seed(), ek.fvec.data(), ek.f_eval.data(), ek.finv_eval.data()));
+        check(mkkg_pkey(&m_kp, next_seed(), ek.crs.data(), ek.f_eval.data(), ek.pkey.data()));
+        check(mkkg_acc_keygen(&m_kp, next_seed(), ek.crs.data(), ek.finv_eval.data(), lwe_sk.data(), ek.evk.data()));
+        check(mkacc_upload_keys(dc().get(), ek.evk.data(), ek.pkey.data()));
+        return ek;
+    }
+    static MNTRUCiphertext unpack_mntru(const uint32_t* c, uint32_t k, uint32_t n, uint64_t q) {
+        std::vector<NativeVector> e(k, NativeVector(n));
+        for (uint32_t u = 0; u < k; ++u)
+            for (uint32_t i = 0; i < n; ++i) e[u][i] = c[(size_t)u * n + i];
+        return std::make_shared<MNTRUCiphertextImpl>(std::move(e), q);
+    }
+    void decrypt_mntru(ConstMNTRUPrivateKey& sk, ConstMNTRUCiphertext& ct, MNTRUPlaintext* result, uint32_t p,
+                       uint32_t variant) const {
+        need_keyparams();
+        if (!result) throw config_error("null result");
+        const uint32_t k = sk->Getk(), n = sk->GetLength();
+        std::vector<uint32_t> c((size_t)k * n);
+        pack(*ct, c.data(), k, n);
+        uint32_t m = 0;
+        check(mkkg_mntru_decrypt(&m_kp, sk->F().data(), c.data(), ct->GetModulus(), p, variant, 1, &m));
+        *result = m;
+    }
+    void decrypt_mklwe(ConstMKLWEPrivateKey& sk, ConstMKLWECiphertext& ct, MKLWEPlaintext* result, uint32_t p,
+                       uint32_t variant) const {
+        need_keyparams();
+        if (!result) throw config_error("null result");
+        const uint32_t k = sk->Getk(), n = sk->GetLength();
+        std::vector<uint32_t> a((size_t)k * n);
+        packA(*ct, a.data(), k, n);
+        const uint32_t b = (uint32_t)ct->GetB();
+        uint32_t m = 0;
+        check(mkkg_mklwe_decrypt(&m_kp, sk->flat().data(), a.data(), &b, ct->GetModulus(), p, variant, 1, &m));
+        *result = m;
     }
     void need_gate(BINGATE gate, BINFHE_METHOD family) const {
         need_context();
@@ -640,9 +890,15 @@ private:
 
     BINFHE_METHOD m_method = MKNTRU;
     std::shared_ptr<UniEncCryptoParams> m_params;
-    std::unique_ptr<DeviceContext> m_dc;
+    mutable std::unique_ptr<DeviceContext> m_dc;
+    int m_device = 0;
     bool m_keys = false;
     MNTRUCiphertext m_ctNAND;
+    mkkg_params m_kp{};
+    bool m_have_kp = false;
+    uint64_t m_seed = 0;
+    mutable uint64_t m_calls = 1;
+    UniEncBTKey m_BTKey;
 };
 
 }  // namespace mkfhe_amd

@@ -1,0 +1,148 @@
+/*
+ * mkfhe_keys.h -- C ABI of the host-side key material for the MK gate path:
+ * key generation, encryption and decryption for MK-NTRU (MNTRU + XZW) and
+ * MK-LWE (MKLWE + XZW_B), without NTL.
+ *
+ * Library: mkfhe_amd/lib/libmkfhe_keys.so (plain C++, CPU only; no GPU is
+ * touched).  Its outputs are exactly the inputs of include/mkfhe_amd.h:
+ *   evk/pkey        -> mkacc_upload_keys
+ *   ksk (MK-NTRU)   -> mkacc_upload_ksk_mntru
+ *   A/B (MK-LWE)    -> mkacc_upload_ksk_mklwe
+ *   ciphertexts     -> mkacc_eval_nand_mntru / mkacc_eval_nand_mklwe
+ *
+ * What each entry point replaces in the reference (src/binfhe/lib/):
+ *   mkkg_mntru_keygen   MNTRUEncryptionScheme::KeyGen / KeyGenGaussian +
+ *                       Get_invertible_Matrix (mntru-pke.cpp:19-156; NTL's
+ *                       mat_ZZ_p inv -> Gauss-Jordan mod q)
+ *   mkkg_mklwe_keygen   MKLWEEncryptionScheme::KeyGenBinary (mklwe-pke.cpp:19-34)
+ *   mkkg_crs            UniEncCryptoParams CRS (mk-cryptoparameters.h:173-178)
+ *   mkkg_ring_secrets   Get_invertible_NativeVector (binfhe-base-scheme.cpp:104-195;
+ *                       NTL's InvMod mod X^N+1 -> pointwise inverse in EVAL)
+ *   mkkg_pkey           Pkey = e - CRS_i * s_u (binfhe-base-scheme.cpp:255-268, 318-331)
+ *   mkkg_acc_keygen     UniEncAccumulatorXZW{,_B}::KeyGenAcc + KeyGenXZW /
+ *                       KDMKeyGenXZW (mk-acc-xzw.cpp:38-87, 132-228;
+ *                       mk-acc-xzw_B.cpp:38-101, 135-220)
+ *   mkkg_ksk_mntru      MNTRUEncryptionScheme::KeySwitchGen2 (mntru-pke.cpp:624-760),
+ *                       KSK2[u][1] (the engine derives KSK2[u][j] = j*KSK2[u][1])
+ *   mkkg_ksk_mklwe      MKLWEEncryptionScheme::KeySwitchGen (mklwe-pke.cpp:176-258)
+ *   mkkg_mntru_encrypt  MNTRUEncryptionScheme::Encrypt (mntru-pke.cpp:158-206)
+ *   mkkg_mntru_ctgate   BinFHEScheme::ctGateGen(NAND) (binfhe-base-scheme.cpp:340-376)
+ *   mkkg_mntru_decrypt  MNTRUEncryptionScheme::Decrypt / Decrypt2 / DecryptNAND
+ *                       (mntru-pke.cpp:208-357)
+ *   mkkg_mklwe_encrypt  MKLWEEncryptionScheme::Encrypt (mklwe-pke.cpp:36-64)
+ *   mkkg_mklwe_decrypt  MKLWEEncryptionScheme::Decrypt / DecryptNAND (mklwe-pke.cpp:66-158)
+ *
+ * Sampling follows the reference's distributions (OpenFHE's Peikert-inversion
+ * discrete Gaussian, std::normal_distribution truncated to an integer where
+ * the reference assigns a double to an NTL ZZ_p, uniform ternary / binary).
+ * The reference seeds from the clock, so its keys are not reproducible; here
+ * every call takes a 64-bit seed (0 = draw one from std::random_device) and
+ * the output is a deterministic function of it, independent of the thread
+ * count.  Randomness is xoshiro256** keyed by SplitMix64 -- NOT a CSPRNG.
+ *
+ * Layouts (row-major, canonical residues):
+ *   F, Finv  [k][n][n] mod qKS: F[u][l][j] = row l, column j of party u's
+ *            matrix (MNTRUPrivateKeyImpl m_F / m_F_inv); F_col0[u][l] = F[u][l][0]
+ *   s (LWE)  [k][n] mod q (MKLWEPrivateKeyImpl)
+ *   skN      [k][N] mod Q, COEFF (UniEncBTKey::fvec); skN_eval / skNinv_eval EVAL
+ *   crs      [dg][N] EVAL, dg = digitsG - 1
+ *   pkey     [k][dg][N] EVAL;  evk [k][nk][n+1][dg][2][N] EVAL (mkfhe_amd.h)
+ *   MNTRU ct [count][k][n] mod q;  MKLWE a [count][k][n], b [count] mod q
+ *   EVAL is the reference's bit-reversed NTT order (mkfhe_amd.h).
+ * Status codes are those of mkfhe_amd.h (MKACC_OK / MKACC_E_*).
+ */
+#ifndef MKFHE_KEYS_H
+#define MKFHE_KEYS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "mkfhe_amd.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MKKG_ABI_VERSION 1
+
+/* SecretKeyDist values used by the MK parameter sets (binfhe-constants.h) */
+#define MKKG_DIST_TERNARY  0  /* UNIFORM_TERNARY */
+#define MKKG_DIST_GAUSSIAN 1  /* GAUSSIAN        */
+#define MKKG_DIST_BINARY   2  /* BINARY          */
+
+/* Decryption variants of MNTRUEncryptionScheme (mntru-pke.cpp:208-357) */
+#define MKKG_DECRYPT      0  /* Decrypt:     floor(p * (<c,F_col0> + q/p) / q)        */
+#define MKKG_DECRYPT2     1  /* Decrypt2:    floor(p * (<c,F_col0> + q/(2p)) / q)     */
+#define MKKG_DECRYPT_NAND 2  /* DecryptNAND: floor(p/2 * (<c,F_col0> + q/(p/2*2)) / q) */
+
+typedef struct mkkg_params {
+    mkacc_params acc;     /* accumulator parameters (method, k, n, N, Q, q, baseG, digitsG, root) */
+    mkacc_ks_params ks;   /* key switching (qKS, baseKS, n_out = n) */
+    double sigma;         /* stdDev column: MNTRU/MKLWE dgg and dggKS (binfhecontext.cpp:85-87) */
+    double sigma_unienc;  /* UniEncCryptoParams m_dgg  = 0.25 (mk-cryptoparameters.h:143) */
+    double sigma_r;       /* UniEncCryptoParams m_dggR = 0.15 (mk-cryptoparameters.h:144) */
+    uint32_t lwe_keydist; /* MKKG_DIST_*: keyDist column (MNTRU_KeyGen / MKLWE_KeyGen) */
+    uint32_t ring_keydist;/* MKKG_DIST_*: ring secret s_u (GAUSSIAN for MKNTRU, TERNARY for MKNTRU_LWE) */
+} mkkg_params;
+
+/* Fill *out for a named MK parameter set (binfhecontext.cpp:129-144) and a
+ * method (MKACC_METHOD_*): GenerateBinFHEContext(set, method). */
+int mkkg_paramset(const char* name, uint32_t method, mkkg_params* out);
+
+/* Word counts of the buffers below for *p. */
+size_t mkkg_evk_words(const mkkg_params* p);   /* k * nk * (n+1) * dg * 2 * N */
+size_t mkkg_pkey_words(const mkkg_params* p);  /* k * dg * N */
+size_t mkkg_ksk_mntru_words(const mkkg_params* p);   /* k * N * dks * n */
+size_t mkkg_ksk_mklwe_a_words(const mkkg_params* p); /* k * N * baseKS * dks * n */
+size_t mkkg_ksk_mklwe_b_words(const mkkg_params* p); /* k * N * baseKS * dks */
+
+/* ---- secret keys -------------------------------------------------------- */
+/* MNTRU_KeyGen: k invertible n x n matrices mod qKS and their inverses. */
+int mkkg_mntru_keygen(const mkkg_params* p, uint64_t seed, uint32_t* F, uint32_t* Finv);
+/* MKLWE_KeyGen: k binary vectors of length n (mod qKS). */
+int mkkg_mklwe_keygen(const mkkg_params* p, uint64_t seed, uint32_t* s);
+
+/* ---- bootstrapping key (MKBTKeyGen) --------------------------------------- */
+/* Common reference string: dg polys sampled from m_dgg, EVAL. */
+int mkkg_crs(const mkkg_params* p, uint64_t seed, uint32_t* crs);
+/* k invertible ring secrets s_u: COEFF, EVAL and EVAL inverse. */
+int mkkg_ring_secrets(const mkkg_params* p, uint64_t seed, uint32_t* skN, uint32_t* skN_eval,
+                      uint32_t* skNinv_eval);
+/* Pkey[u][i] = NTT(e) - CRS[i] * s_u (EVAL). */
+int mkkg_pkey(const mkkg_params* p, uint64_t seed, const uint32_t* crs, const uint32_t* skN_eval, uint32_t* pkey);
+/* KeyGenAcc: uni-encryptions of the LWE secret bits (lwe_sk [k][n] mod q:
+ * F_col0 for MK-NTRU, s for MK-LWE) under 1/s_u. */
+int mkkg_acc_keygen(const mkkg_params* p, uint64_t seed, const uint32_t* crs, const uint32_t* skNinv_eval,
+                    const uint32_t* lwe_sk, uint32_t* evk);
+/* KeySwitchGen2 (MK-NTRU): ksk [k][N*dks][n] = KSK2[u][1]. */
+int mkkg_ksk_mntru(const mkkg_params* p, uint64_t seed, const uint32_t* skN, const uint32_t* Finv, uint32_t* ksk);
+/* KeySwitchGen (MK-LWE): A [k][N][baseKS][dks][n], B [k][N][baseKS][dks]. */
+int mkkg_ksk_mklwe(const mkkg_params* p, uint64_t seed, const uint32_t* skN, const uint32_t* s, uint32_t* A,
+                   uint32_t* B);
+
+/* ---- encryption / decryption ------------------------------------------------ */
+/* count MNTRU encryptions of m[i] (plaintext modulus pt, reference default 4). */
+int mkkg_mntru_encrypt(const mkkg_params* p, uint64_t seed, const uint32_t* Finv, const uint32_t* m, uint32_t pt,
+                       size_t count, uint32_t* ct);
+/* ctGateGen(sk, NAND): the encryption of 5q/8 the NAND head subtracts from. */
+int mkkg_mntru_ctgate(const mkkg_params* p, uint64_t seed, const uint32_t* Finv, uint32_t* ct_nand);
+/* count MNTRU decryptions (variant MKKG_DECRYPT*; ct modulus `mod`, 0 = q). */
+int mkkg_mntru_decrypt(const mkkg_params* p, const uint32_t* F, const uint32_t* ct, uint64_t mod, uint32_t pt,
+                       uint32_t variant, size_t count, uint32_t* m);
+int mkkg_mklwe_encrypt(const mkkg_params* p, uint64_t seed, const uint32_t* s, const uint32_t* m, uint32_t pt,
+                       size_t count, uint32_t* a, uint32_t* b);
+/* variant MKKG_DECRYPT (Decrypt, + q/(2p)) or MKKG_DECRYPT_NAND (DecryptNAND). */
+int mkkg_mklwe_decrypt(const mkkg_params* p, const uint32_t* s, const uint32_t* a, const uint32_t* b, uint64_t mod,
+                       uint32_t pt, uint32_t variant, size_t count, uint32_t* m);
+
+/* ---- host ring transform (the reference's EVAL order), for tests ------------ */
+int mkkg_ntt_forward(const mkkg_params* p, const uint32_t* in, uint32_t* out, size_t count);
+int mkkg_ntt_inverse(const mkkg_params* p, const uint32_t* in, uint32_t* out, size_t count);
+
+const char* mkkg_last_error(void);
+int mkkg_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MKFHE_KEYS_H */

@@ -1,4 +1,6 @@
-"""Build the in-tree HIP engine: mkfhe_amd/lib/libmkfhe_amd.so (gfx950).
+"""Build the in-tree libraries:
+    mkfhe_amd/lib/libmkfhe_amd.so   HIP engine for gfx950 (hipcc)
+    mkfhe_amd/lib/libmkfhe_keys.so  host key material (g++, include/mkfhe_keys.h)
 
     python -m mkfhe_amd.build [--force]
 
@@ -17,22 +19,46 @@ SOURCES = [os.path.join(_HERE, "csrc", "mkacc_engine.hip")]
 HEADERS = [os.path.join(_HERE, "csrc", f) for f in ("mkacc_device.hpp", "mkacc_host_math.hpp", "mkacc_gate.hpp")] + [
     os.path.join(ROOT, "include", "mkfhe_amd.h")]
 OUT = os.path.join(_HERE, "lib", "libmkfhe_amd.so")
+KEYS_SOURCES = [os.path.join(_HERE, "csrc", "mkkeys.cpp")]
+KEYS_HEADERS = [os.path.join(_HERE, "csrc", "mkacc_host_math.hpp"), os.path.join(ROOT, "include", "mkfhe_keys.h"),
+                os.path.join(ROOT, "include", "mkfhe_amd.h")]
+KEYS_OUT = os.path.join(_HERE, "lib", "libmkfhe_keys.so")
 ARCH = os.environ.get("MKFHE_OFFLOAD_ARCH", "gfx950")
 
 
-def _stale() -> bool:
-    if not os.path.exists(OUT):
+def _stale(out, deps) -> bool:
+    if not os.path.exists(out):
         return True
-    t = os.path.getmtime(OUT)
-    return any(os.path.getmtime(f) > t for f in SOURCES + HEADERS)
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(f) > t for f in deps)
+
+
+def build_keys(force: bool = False, verbose: bool = False) -> str:
+    """Host key-material library (plain C++, no GPU)."""
+    if not force and not _stale(KEYS_OUT, KEYS_SOURCES + KEYS_HEADERS):
+        return KEYS_OUT
+    os.makedirs(os.path.dirname(KEYS_OUT), exist_ok=True)
+    cxx = os.environ.get("CXX", "g++")
+    # inline helpers stay private to each library (both include mkacc_host_math.hpp)
+    cmd = [cxx, "-O3", "-march=x86-64-v3", "-std=c++17", "-fPIC", "-shared", "-pthread",
+           "-fvisibility-inlines-hidden", "-Wl,-Bsymbolic",
+           "-I", os.path.join(ROOT, "include"), "-I", os.path.join(_HERE, "csrc"),
+           "-o", KEYS_OUT + ".tmp"] + KEYS_SOURCES
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.check_call(cmd)
+    os.replace(KEYS_OUT + ".tmp", KEYS_OUT)
+    return KEYS_OUT
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not _stale():
+    build_keys(force, verbose)
+    if not force and not _stale(OUT, SOURCES + HEADERS):
         return OUT
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-fvisibility-inlines-hidden", "-Wl,-Bsymbolic",
            "-Wno-unused-result", "-Wno-pass-failed", "-I", os.path.join(ROOT, "include"),
            "-o", OUT + ".tmp"] + SOURCES
     if verbose:

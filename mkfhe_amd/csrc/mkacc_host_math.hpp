@@ -110,25 +110,27 @@ inline uint32_t digits_g(uint64_t Q, uint32_t baseG) {
 struct ParamRow {
     const char* name;
     uint32_t numUser, numberBits, cyclOrder, latticeParam, mod, modKS, baseKS, gadgetBase, baseRK;
+    double stdDev;     // STD_NTRU 0.5 / STD_NTRU2 0.75 / STD_DEV 1.9 (binfhecontext.cpp:85-87)
+    uint32_t keyDist;  // 0 UNIFORM_TERNARY, 1 GAUSSIAN, 2 BINARY
 };
 inline const ParamRow* find_paramset(const char* name) {
     static const ParamRow rows[] = {
-        {"STD128_MKNTRU", 2, 27, 4096, 765, 45181, 45181, 32, 1u << 7, 32},
-        {"STD128_MKNTRU_2", 4, 27, 4096, 765, 45181, 45181, 32, 1u << 7, 32},
-        {"STD128_MKNTRU_3", 8, 27, 4096, 765, 45181, 45181, 32, 1u << 6, 32},
-        {"STD128_MKNTRU_4", 16, 27, 4096, 765, 45181, 45181, 32, 1u << 5, 32},
-        {"STD128_MKNTRU_LWE", 2, 27, 4096, 635, 32749, 32749, 32, 1u << 9, 2},
-        {"STD128_MKNTRU_LWE_2", 4, 27, 4096, 635, 32749, 32749, 32, 1u << 9, 2},
-        {"STD128_MKNTRU_LWE_3", 8, 27, 4096, 635, 32749, 32749, 32, 1u << 9, 2},
-        {"STD128_MKNTRU_LWE_4", 16, 27, 4096, 635, 32749, 32749, 32, 1u << 7, 2},
-        {"STD100_MKNTRU", 2, 27, 4096, 560, 45181, 45181, 32, 1u << 9, 32},
-        {"STD100_MKNTRU_2", 4, 27, 4096, 560, 45181, 45181, 32, 1u << 9, 32},
-        {"STD100_MKNTRU_3", 8, 27, 4096, 560, 45181, 45181, 32, 1u << 9, 32},
-        {"STD100_MKNTRU_4", 16, 27, 4096, 560, 45181, 45181, 32, 1u << 9, 32},
-        {"STD100_MKNTRU_LWE", 2, 27, 4096, 500, 32749, 32749, 32, 1u << 9, 2},
-        {"STD100_MKNTRU_LWE_2", 4, 27, 4096, 500, 32749, 32749, 32, 1u << 9, 2},
-        {"STD100_MKNTRU_LWE_3", 8, 27, 4096, 500, 32749, 32749, 32, 1u << 9, 2},
-        {"STD100_MKNTRU_LWE_4", 16, 27, 4096, 500, 32749, 32749, 32, 1u << 9, 2},
+        {"STD128_MKNTRU", 2, 27, 4096, 765, 45181, 45181, 32, 1u << 7, 32, 0.5, 0},
+        {"STD128_MKNTRU_2", 4, 27, 4096, 765, 45181, 45181, 32, 1u << 7, 32, 0.5, 0},
+        {"STD128_MKNTRU_3", 8, 27, 4096, 765, 45181, 45181, 32, 1u << 6, 32, 0.5, 0},
+        {"STD128_MKNTRU_4", 16, 27, 4096, 765, 45181, 45181, 32, 1u << 5, 32, 0.5, 0},
+        {"STD128_MKNTRU_LWE", 2, 27, 4096, 635, 32749, 32749, 32, 1u << 9, 2, 1.9, 2},
+        {"STD128_MKNTRU_LWE_2", 4, 27, 4096, 635, 32749, 32749, 32, 1u << 9, 2, 1.9, 2},
+        {"STD128_MKNTRU_LWE_3", 8, 27, 4096, 635, 32749, 32749, 32, 1u << 9, 2, 1.9, 2},
+        {"STD128_MKNTRU_LWE_4", 16, 27, 4096, 635, 32749, 32749, 32, 1u << 7, 2, 1.9, 2},
+        {"STD100_MKNTRU", 2, 27, 4096, 560, 45181, 45181, 32, 1u << 9, 32, 0.75, 0},
+        {"STD100_MKNTRU_2", 4, 27, 4096, 560, 45181, 45181, 32, 1u << 9, 32, 0.75, 0},
+        {"STD100_MKNTRU_3", 8, 27, 4096, 560, 45181, 45181, 32, 1u << 9, 32, 0.75, 0},
+        {"STD100_MKNTRU_4", 16, 27, 4096, 560, 45181, 45181, 32, 1u << 9, 32, 0.75, 0},
+        {"STD100_MKNTRU_LWE", 2, 27, 4096, 500, 32749, 32749, 32, 1u << 9, 2, 1.9, 2},
+        {"STD100_MKNTRU_LWE_2", 4, 27, 4096, 500, 32749, 32749, 32, 1u << 9, 2, 1.9, 2},
+        {"STD100_MKNTRU_LWE_3", 8, 27, 4096, 500, 32749, 32749, 32, 1u << 9, 2, 1.9, 2},
+        {"STD100_MKNTRU_LWE_4", 16, 27, 4096, 500, 32749, 32749, 32, 1u << 9, 2, 1.9, 2},
     };
     for (const auto& r : rows)
         if (std::strcmp(r.name, name) == 0) return &r;

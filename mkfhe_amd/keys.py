@@ -1,0 +1,263 @@
+"""ctypes binding of the host key-material library (include/mkfhe_keys.h,
+mkfhe_amd/lib/libmkfhe_keys.so): NTL-free key generation, encryption and
+decryption for MK-NTRU and MK-LWE.
+
+CPU only.  The reference functions each call replaces are listed in the
+header; the Python names follow the reference's (MNTRU_KeyGen, MKBTKeyGen,
+ctGateGen, Encrypt, Decrypt) in ``mkfhe_amd.binfhe``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+from ._lib import MkaccError, MkaccKsParams, MkaccParams
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+KEYS_LIB_PATH = os.environ.get("MKFHE_KEYS_LIB") or os.path.join(_HERE, "lib", "libmkfhe_keys.so")
+
+DIST_TERNARY, DIST_GAUSSIAN, DIST_BINARY = 0, 1, 2
+DECRYPT, DECRYPT2, DECRYPT_NAND = 0, 1, 2
+
+
+class MkkgParams(ctypes.Structure):
+    """struct mkkg_params (include/mkfhe_keys.h)."""
+
+    _fields_ = [
+        ("acc", MkaccParams),
+        ("ks", MkaccKsParams),
+        ("sigma", ctypes.c_double),
+        ("sigma_unienc", ctypes.c_double),
+        ("sigma_r", ctypes.c_double),
+        ("lwe_keydist", ctypes.c_uint32),
+        ("ring_keydist", ctypes.c_uint32),
+    ]
+
+
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+_pp = ctypes.POINTER(MkkgParams)
+_sz = ctypes.c_size_t
+_u64 = ctypes.c_uint64
+_u32 = ctypes.c_uint32
+_int = ctypes.c_int
+
+SIGNATURES = {
+    "mkkg_paramset": (_int, [ctypes.c_char_p, _u32, _pp]),
+    "mkkg_evk_words": (_sz, [_pp]),
+    "mkkg_pkey_words": (_sz, [_pp]),
+    "mkkg_ksk_mntru_words": (_sz, [_pp]),
+    "mkkg_ksk_mklwe_a_words": (_sz, [_pp]),
+    "mkkg_ksk_mklwe_b_words": (_sz, [_pp]),
+    "mkkg_mntru_keygen": (_int, [_pp, _u64, _u32p, _u32p]),
+    "mkkg_mklwe_keygen": (_int, [_pp, _u64, _u32p]),
+    "mkkg_crs": (_int, [_pp, _u64, _u32p]),
+    "mkkg_ring_secrets": (_int, [_pp, _u64, _u32p, _u32p, _u32p]),
+    "mkkg_pkey": (_int, [_pp, _u64, _u32p, _u32p, _u32p]),
+    "mkkg_acc_keygen": (_int, [_pp, _u64, _u32p, _u32p, _u32p, _u32p]),
+    "mkkg_ksk_mntru": (_int, [_pp, _u64, _u32p, _u32p, _u32p]),
+    "mkkg_ksk_mklwe": (_int, [_pp, _u64, _u32p, _u32p, _u32p, _u32p]),
+    "mkkg_mntru_encrypt": (_int, [_pp, _u64, _u32p, _u32p, _u32, _sz, _u32p]),
+    "mkkg_mntru_ctgate": (_int, [_pp, _u64, _u32p, _u32p]),
+    "mkkg_mntru_decrypt": (_int, [_pp, _u32p, _u32p, _u64, _u32, _u32, _sz, _u32p]),
+    "mkkg_mklwe_encrypt": (_int, [_pp, _u64, _u32p, _u32p, _u32, _sz, _u32p, _u32p]),
+    "mkkg_mklwe_decrypt": (_int, [_pp, _u32p, _u32p, _u32p, _u64, _u32, _u32, _sz, _u32p]),
+    "mkkg_ntt_forward": (_int, [_pp, _u32p, _u32p, _sz]),
+    "mkkg_ntt_inverse": (_int, [_pp, _u32p, _u32p, _sz]),
+    "mkkg_last_error": (ctypes.c_char_p, []),
+    "mkkg_abi_version": (_int, []),
+}
+
+_lib = None
+
+
+def load():
+    """Load libmkfhe_keys.so (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(KEYS_LIB_PATH):
+            raise RuntimeError(f"{KEYS_LIB_PATH} not found: build it first (python -m mkfhe_amd.build)")
+        L = ctypes.CDLL(KEYS_LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _check(rc: int):
+    if rc != 0:
+        raise MkaccError(rc, load().mkkg_last_error().decode())
+
+
+def _p(a: np.ndarray):
+    assert a.dtype == np.uint32 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(_u32p)
+
+
+def _in(a) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(a, dtype=np.uint32))
+
+
+def paramset(name: str, method: int) -> MkkgParams:
+    p = MkkgParams()
+    _check(load().mkkg_paramset(name.encode(), method, ctypes.byref(p)))
+    return p
+
+
+def dims(p: MkkgParams):
+    """(k, n, N, dg, nk, dks) of a parameter struct."""
+    a = p.acc
+    import math
+    digitsG = a.digitsG or math.ceil(math.log(a.Q) / math.log(a.baseG))
+    dks = math.ceil(math.log(p.ks.qKS) / math.log(p.ks.baseKS))
+    nk = 2 if a.method == 0 else 1
+    return a.k, a.n, a.N, digitsG - 1, nk, dks
+
+
+# ---- secret keys ------------------------------------------------------------------------
+
+@dataclass
+class MNTRUPrivateKey:
+    """MNTRUPrivateKeyImpl (mntru-privatekey.h): F, F^-1 [k][n][n] mod qKS."""
+    F: np.ndarray
+    Finv: np.ndarray
+
+    @property
+    def F_col0(self) -> np.ndarray:
+        """GetF_col0 (mntru-privatekey.h:56-70): [k][n]."""
+        return np.ascontiguousarray(self.F[:, :, 0])
+
+
+@dataclass
+class MKLWEPrivateKey:
+    """MKLWEPrivateKeyImpl: s [k][n] binary."""
+    s: np.ndarray
+
+
+def mntru_keygen(p: MkkgParams, seed: int = 0) -> MNTRUPrivateKey:
+    k, n = p.acc.k, p.acc.n
+    F = np.empty((k, n, n), np.uint32)
+    Fi = np.empty((k, n, n), np.uint32)
+    _check(load().mkkg_mntru_keygen(ctypes.byref(p), seed, _p(F), _p(Fi)))
+    return MNTRUPrivateKey(F, Fi)
+
+
+def mklwe_keygen(p: MkkgParams, seed: int = 0) -> MKLWEPrivateKey:
+    s = np.empty((p.acc.k, p.acc.n), np.uint32)
+    _check(load().mkkg_mklwe_keygen(ctypes.byref(p), seed, _p(s)))
+    return MKLWEPrivateKey(s)
+
+
+# ---- bootstrapping key -------------------------------------------------------------------
+
+@dataclass
+class UniEncBTKey:
+    """UniEncBTKey (binfhe-base-scheme.h:64-84): accumulator key, P, ring secrets, KS key."""
+    crs: np.ndarray
+    skN: np.ndarray            # fvec: [k][N] COEFF
+    skN_eval: np.ndarray       # f:    [k][N] EVAL
+    skNinv_eval: np.ndarray    # [k][N] EVAL
+    pkey: np.ndarray           # [k][dg][N] EVAL
+    evk: np.ndarray            # [k][nk][n+1][dg][2][N] EVAL
+    ksk: np.ndarray | None = None      # MK-NTRU KSK2[u][1]: [k][N*dks][n]
+    ksk_A: np.ndarray | None = None    # MK-LWE: [k][N][baseKS][dks][n]
+    ksk_B: np.ndarray | None = None    # MK-LWE: [k][N][baseKS][dks]
+
+
+def crs(p: MkkgParams, seed: int) -> np.ndarray:
+    k, n, N, dg, nk, dks = dims(p)
+    out = np.empty((dg, N), np.uint32)
+    _check(load().mkkg_crs(ctypes.byref(p), seed, _p(out)))
+    return out
+
+
+def ring_secrets(p: MkkgParams, seed: int):
+    k, N = p.acc.k, p.acc.N
+    c, e, ei = (np.empty((k, N), np.uint32) for _ in range(3))
+    _check(load().mkkg_ring_secrets(ctypes.byref(p), seed, _p(c), _p(e), _p(ei)))
+    return c, e, ei
+
+
+def bt_keygen(p: MkkgParams, sk, seed: int = 0, crs_seed: int | None = None) -> UniEncBTKey:
+    """MKKeyGen for an MNTRU (binfhe-base-scheme.cpp:198-277) or MKLWE (:279-338) secret key."""
+    import secrets
+    if seed == 0:
+        seed = secrets.randbits(63) | 1
+    L = load()
+    k, n, N, dg, nk, dks = dims(p)
+    c = crs(p, crs_seed if crs_seed is not None else seed ^ 0xC25)
+    skN, skN_eval, skNinv = ring_secrets(p, seed + 1)
+    pkey = np.empty((k, dg, N), np.uint32)
+    _check(L.mkkg_pkey(ctypes.byref(p), seed + 2, _p(c), _p(skN_eval), _p(pkey)))
+    evk = np.empty((k, nk, n + 1, dg, 2, N), np.uint32)
+    lwe_sk = _in(sk.F_col0 if isinstance(sk, MNTRUPrivateKey) else sk.s)
+    _check(L.mkkg_acc_keygen(ctypes.byref(p), seed + 3, _p(c), _p(skNinv), _p(lwe_sk), _p(evk)))
+    key = UniEncBTKey(c, skN, skN_eval, skNinv, pkey, evk)
+    if isinstance(sk, MNTRUPrivateKey):
+        key.ksk = np.empty((k, N * dks, n), np.uint32)
+        _check(L.mkkg_ksk_mntru(ctypes.byref(p), seed + 4, _p(skN), _p(_in(sk.Finv)), _p(key.ksk)))
+    else:
+        B = p.ks.baseKS
+        key.ksk_A = np.empty((k, N, B, dks, n), np.uint32)
+        key.ksk_B = np.empty((k, N, B, dks), np.uint32)
+        _check(L.mkkg_ksk_mklwe(ctypes.byref(p), seed + 4, _p(skN), _p(_in(sk.s)), _p(key.ksk_A), _p(key.ksk_B)))
+    return key
+
+
+# ---- encryption / decryption ------------------------------------------------------------------
+
+def mntru_encrypt(p: MkkgParams, sk: MNTRUPrivateKey, m, pt: int = 4, seed: int = 0) -> np.ndarray:
+    m = _in(np.atleast_1d(m))
+    ct = np.empty((m.size, p.acc.k, p.acc.n), np.uint32)
+    _check(load().mkkg_mntru_encrypt(ctypes.byref(p), seed, _p(_in(sk.Finv)), _p(m), pt, m.size, _p(ct)))
+    return ct
+
+
+def mntru_ctgate(p: MkkgParams, sk: MNTRUPrivateKey, seed: int = 0) -> np.ndarray:
+    ct = np.empty((p.acc.k, p.acc.n), np.uint32)
+    _check(load().mkkg_mntru_ctgate(ctypes.byref(p), seed, _p(_in(sk.Finv)), _p(ct)))
+    return ct
+
+
+def mntru_decrypt(p: MkkgParams, sk: MNTRUPrivateKey, ct, pt: int = 4, variant: int = DECRYPT,
+                  mod: int = 0) -> np.ndarray:
+    ct = _in(ct).reshape(-1, p.acc.k, p.acc.n)
+    m = np.empty(ct.shape[0], np.uint32)
+    _check(load().mkkg_mntru_decrypt(ctypes.byref(p), _p(_in(sk.F)), _p(ct), mod, pt, variant, ct.shape[0], _p(m)))
+    return m
+
+
+def mklwe_encrypt(p: MkkgParams, sk: MKLWEPrivateKey, m, pt: int = 4, seed: int = 0):
+    m = _in(np.atleast_1d(m))
+    a = np.empty((m.size, p.acc.k, p.acc.n), np.uint32)
+    b = np.empty(m.size, np.uint32)
+    _check(load().mkkg_mklwe_encrypt(ctypes.byref(p), seed, _p(_in(sk.s)), _p(m), pt, m.size, _p(a), _p(b)))
+    return a, b
+
+
+def mklwe_decrypt(p: MkkgParams, sk: MKLWEPrivateKey, a, b, pt: int = 4, variant: int = DECRYPT,
+                  mod: int = 0) -> np.ndarray:
+    a = _in(a).reshape(-1, p.acc.k, p.acc.n)
+    b = _in(b).reshape(-1)
+    m = np.empty(a.shape[0], np.uint32)
+    _check(load().mkkg_mklwe_decrypt(ctypes.byref(p), _p(_in(sk.s)), _p(a), _p(b), mod, pt, variant,
+                                     a.shape[0], _p(m)))
+    return m
+
+
+def ntt_forward(p: MkkgParams, a) -> np.ndarray:
+    a = _in(a)
+    out = np.empty_like(a)
+    _check(load().mkkg_ntt_forward(ctypes.byref(p), _p(a), _p(out), a.size // p.acc.N))
+    return out
+
+
+def ntt_inverse(p: MkkgParams, a) -> np.ndarray:
+    a = _in(a)
+    out = np.empty_like(a)
+    _check(load().mkkg_ntt_inverse(ctypes.byref(p), _p(a), _p(out), a.size // p.acc.N))
+    return out

@@ -596,6 +596,33 @@ void orc_mntru_tail(const orc_ctx* c, const uint64_t* acc, const uint64_t* ksk2,
     free(ext);
 }
 
+/* orc_mntru_tail with the key given as KSK2[u][1] only ([k][N*dks][n]): the
+ * row KeySwitch2 adds for digit j is KSK2[u][j][l] = j * KSK2[u][1][l] mod qKS,
+ * exactly as KeySwitchGen2 stores the table (mntru-pke.cpp:744-755). */
+void orc_mntru_tail_ksk1(const orc_ctx* c, const uint64_t* acc, const uint32_t* ksk1, uint64_t qKS,
+                         uint32_t baseKS, uint32_t n_out, uint64_t* out) {
+    const uint32_t N = c->p.N, k = c->p.k, dks = ks_digits(qKS, baseKS);
+    const size_t L = (size_t)N * dks;
+    uint64_t* ext = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)k * N);
+    orc_extract(c, acc, ext);
+    for (size_t i = 0; i < (size_t)k * N; ++i) ext[i] = orc_round_qQ(ext[i], qKS, c->p.Q);
+    for (uint32_t u = 0; u < k; ++u) {
+        uint64_t* o = out + (size_t)u * n_out;
+        memset(o, 0, n_out * sizeof(uint64_t));
+        for (uint32_t i = 0; i < N; ++i) {
+            uint64_t t = ext[(size_t)u * N + i];
+            for (uint32_t j = 0; j < dks; ++j) {
+                const uint64_t index = t % baseKS;
+                t /= baseKS;
+                if (index == 0) continue;
+                const uint32_t* row = ksk1 + ((size_t)u * L + (size_t)i * dks + j) * n_out;
+                for (uint32_t x = 0; x < n_out; ++x) o[x] = addmod(o[x], index * row[x] % qKS, qKS);
+            }
+        }
+    }
+    free(ext);
+}
+
 /* MK-LWE gate head (binfhe-base-scheme.cpp:380-406, 1004-1065):
  *   ct_temp = (0, 5q/8) - (ct1 + ct2) mod q; ModSwitch to 2N (mklwe-pke.cpp:160-174);
  *   acc[0] = NTT(X^b * Rx), Rx[j] = j < N/2 ? Q/8+1 : Q - (Q/8+1)  (:1017-1043);

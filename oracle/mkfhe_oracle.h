@@ -107,6 +107,9 @@ void orc_keyswitch2(const uint64_t* ksk2, const uint64_t* ct, uint64_t* out, uin
                     uint64_t qKS, uint32_t baseKS);
 void orc_mntru_tail(const orc_ctx* c, const uint64_t* acc, const uint64_t* ksk2, uint64_t qKS, uint32_t baseKS,
                     uint32_t n_out, uint64_t* out);
+/* same, with the key as KSK2[u][1] ([k][N*dks][n], u32); row j = j*KSK2[u][1] */
+void orc_mntru_tail_ksk1(const orc_ctx* c, const uint64_t* acc, const uint32_t* ksk1, uint64_t qKS,
+                         uint32_t baseKS, uint32_t n_out, uint64_t* out);
 void orc_mklwe_head(const orc_ctx* c, const uint64_t* a1, uint64_t b1, const uint64_t* a2, uint64_t b2, uint64_t q,
                     uint32_t n, uint64_t p, uint64_t* cout, uint64_t* acc);
 void orc_mklwe_keyswitch(const uint64_t* A, const uint64_t* Bk, const uint64_t* a, uint64_t b, uint64_t* out_a,

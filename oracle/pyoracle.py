@@ -88,6 +88,8 @@ def lib():
                                      ctypes.c_uint64, ctypes.c_uint32]
         L.orc_mntru_tail.argtypes = [ctypes.c_void_p, _u64p, _u64p, ctypes.c_uint64, ctypes.c_uint32,
                                      ctypes.c_uint32, _u64p]
+        L.orc_mntru_tail_ksk1.argtypes = [ctypes.c_void_p, _u64p, _u32p, ctypes.c_uint64, ctypes.c_uint32,
+                                          ctypes.c_uint32, _u64p]
         L.orc_mklwe_head.argtypes = [ctypes.c_void_p, _u64p, ctypes.c_uint64, _u64p, ctypes.c_uint64,
                                      ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, _u64p, _u64p]
         L.orc_mklwe_keyswitch.argtypes = [_u64p, _u64p, _u64p, ctypes.c_uint64, _u64p, _u64p, ctypes.c_uint32,
@@ -268,6 +270,14 @@ def _oracle_methods():
         lib().orc_mntru_tail(self._ctx, _p64(_u64(acc)), _p64(_u64(ksk2)), qKS, baseKS, n_out, _p64(out))
         return out
 
+    def mntru_tail_ksk1(self, acc, ksk1, qKS: int, baseKS: int, n_out: int):
+        """Tail with the key as KSK2[u][1] ([k][N*dks][n] u32, mkfhe_keys.h layout)."""
+        out = np.empty((self.k, n_out), dtype=np.uint64)
+        k1 = np.ascontiguousarray(ksk1, dtype=np.uint32)
+        lib().orc_mntru_tail_ksk1(self._ctx, _p64(_u64(acc)), k1.ctypes.data_as(_u32p), qKS, baseKS, n_out,
+                                  _p64(out))
+        return out
+
     def mklwe_head(self, a1, b1, a2, b2, q: int, p: int = 4):
         a1, a2 = _u64(a1), _u64(a2)
         c = np.empty_like(a1)
@@ -283,7 +293,7 @@ def _oracle_methods():
                              _p64(oa), _p64(ob))
         return oa, int(ob[0])
 
-    for f in (extract, mntru_tail, mklwe_head, mklwe_tail):
+    for f in (extract, mntru_tail, mntru_tail_ksk1, mklwe_head, mklwe_tail):
         setattr(Oracle, f.__name__, f)
 
 

@@ -62,6 +62,34 @@ static void test_cpu() {
     auto accB = MakeUniEncAccumulator(MKNTRU_B);
     ConstUniEncACCKey some = std::make_shared<const UniEncACCKeyImpl>();
     EXPECT(throws<config_error>([&] { accB->EvalAcc(p, some, {}, {}, a, {}); }));
+
+    // BinFHEContext key generation / encryption / decryption run on the host
+    // (libmkfhe_keys.so); the device context is only created by MKBTKeyGen / EvalBinGate.
+    BinFHEContext cc;
+    cc.GenerateBinFHEContext(STD100_MKNTRU, MKNTRU);
+    cc.SetSeed(7);
+    auto sk = cc.MNTRU_KeyGen();
+    EXPECT(sk->Getk() == 2 && sk->GetLength() == 560 && sk->GetModulus() == 45181);
+    EXPECT(throws<config_error>([&] { cc.MKLWE_KeyGen(); }));          // binfhecontext.cpp:244-249
+    EXPECT(throws<config_error>([&] { cc.ctGateGen(sk, AND); }));      // binfhe-base-scheme.cpp:341-342
+    for (int m = 0; m < 2; ++m) {
+        auto ct = cc.Encrypt(sk, m);
+        EXPECT(ct->GetModulus() == 45181 && ct->GetptModulus() == 4);
+        MNTRUPlaintext r = -1;
+        cc.Decrypt2(sk, ct, &r);
+        EXPECT(r == m);
+    }
+    auto c0 = cc.Encrypt(sk, 0), c1 = cc.Encrypt(sk, 1);
+    EXPECT(throws<config_error>([&] { cc.EvalBinGate(NAND, c0, c1); }));  // keys not generated
+    BinFHEContext cl;
+    cl.GenerateBinFHEContext(STD100_MKNTRU_LWE, MKNTRU_LWE);
+    auto skl = cl.MKLWE_KeyGen();
+    for (int m = 0; m < 2; ++m) {
+        auto ct = cl.Encrypt(skl, m);
+        MKLWEPlaintext r = -1;
+        cl.Decrypt(skl, ct, &r);
+        EXPECT(r == m);
+    }
 }
 
 // ---- GPU parity ------------------------------------------------------------------

@@ -16,13 +16,15 @@ def binary(oracle):
     from mkfhe_amd import _lib
     lib_dir = os.path.dirname(_lib.LIB_PATH)
     orc_dir = os.path.join(ROOT, "oracle", "build")
-    deps = [SRC, os.path.join(ROOT, "include", "mkfhe_amd_binfhe.hpp"), _lib.LIB_PATH]
+    from mkfhe_amd import build
+    build.build_keys()
+    deps = [SRC, os.path.join(ROOT, "include", "mkfhe_amd_binfhe.hpp"), _lib.LIB_PATH, build.KEYS_OUT]
     if not os.path.exists(OUT) or os.path.getmtime(OUT) < max(os.path.getmtime(d) for d in deps):
         os.makedirs(os.path.dirname(OUT), exist_ok=True)
         subprocess.check_call([
             "g++", "-std=c++17", "-O2", "-Wall", "-Wextra", SRC, "-o", OUT,
             "-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROOT, "oracle"),
-            "-L", lib_dir, "-lmkfhe_amd", f"-Wl,-rpath,{lib_dir}",
+            "-L", lib_dir, "-lmkfhe_amd", "-lmkfhe_keys", f"-Wl,-rpath,{lib_dir}",
             "-L", orc_dir, "-lmkfhe_oracle", f"-Wl,-rpath,{orc_dir}"])
     return OUT
 
