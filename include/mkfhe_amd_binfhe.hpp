@@ -644,6 +644,72 @@ public:
     }
     const UniEncBTKey& GetBTKey() const { return m_BTKey; }
 
+    // ---- key files (mkfhe_keys.h wire format; the reference has none for MK keys) ----
+    void SaveBTKey(const std::string& path) const {
+        need_keyparams();
+        const UniEncBTKey& k = m_BTKey;
+        if (k.evk.empty()) throw config_error("no bootstrapping key generated by MKBTKeyGen");
+        std::vector<mkkg_section> s;
+        auto add = [&](const char* nm, const std::vector<uint32_t>& v) {
+            if (v.empty()) return;
+            mkkg_section x{};
+            std::strncpy(x.name, nm, 15);
+            x.words = v.size();
+            x.data = v.data();
+            s.push_back(x);
+        };
+        add("crs", k.crs); add("skN", k.fvec); add("skN_eval", k.f_eval); add("skNinv_eval", k.finv_eval);
+        add("pkey", k.pkey); add("evk", k.evk); add("ksk", k.ksk); add("ksk_a", k.ksk_a); add("ksk_b", k.ksk_b);
+        check(mkkg_file_write(path.c_str(), MKKG_FILE_BTKEY, &m_kp, s.data(), (uint32_t)s.size()));
+    }
+    // Load a bootstrapping key written by SaveBTKey (or mkfhe_amd.keys.save_btkey) and upload it.
+    void LoadBTKey(const std::string& path) {
+        need_keyparams();
+        uint32_t kind = 0;
+        mkkg_params fp{};
+        check(mkkg_file_info(path.c_str(), &kind, &fp, nullptr));
+        if (kind != MKKG_FILE_BTKEY) throw config_error(path + " is not a bootstrapping-key file");
+        if (fp.acc.method != m_kp.acc.method || fp.acc.k != m_kp.acc.k || fp.acc.n != m_kp.acc.n ||
+            fp.acc.Q != m_kp.acc.Q || fp.acc.baseG != m_kp.acc.baseG || fp.ks.qKS != m_kp.ks.qKS)
+            throw config_error(path + " was generated for a different context");
+        UniEncBTKey ek;
+        auto get = [&](const char* nm, std::vector<uint32_t>& v) {
+            v.resize(mkkg_file_section_words(path.c_str(), nm));
+            if (!v.empty()) check(mkkg_file_read_section(path.c_str(), nm, v.data(), v.size()));
+        };
+        get("crs", ek.crs); get("skN", ek.fvec); get("skN_eval", ek.f_eval); get("skNinv_eval", ek.finv_eval);
+        get("pkey", ek.pkey); get("evk", ek.evk); get("ksk", ek.ksk); get("ksk_a", ek.ksk_a); get("ksk_b", ek.ksk_b);
+        if (ek.evk.size() != mkkg_evk_words(&m_kp) || ek.pkey.size() != mkkg_pkey_words(&m_kp))
+            throw config_error(path + ": key sizes do not match the context");
+        check(mkacc_upload_keys(dc().get(), ek.evk.data(), ek.pkey.data()));
+        const mkacc_ks_params ks = GetKSParams();
+        if (m_method == MKNTRU_LWE)
+            check(mkacc_upload_ksk_mklwe(dc().get(), &ks, ek.ksk_a.data(), ek.ksk_b.data()));
+        else
+            check(mkacc_upload_ksk_mntru(dc().get(), &ks, ek.ksk.data()));
+        m_BTKey = std::move(ek);
+        m_keys = true;
+    }
+    void SaveSecretKey(const std::string& path, ConstMNTRUPrivateKey& sk) const {
+        need_keyparams();
+        mkkg_section s[2] = {};
+        std::strncpy(s[0].name, "F", 15);
+        s[0].words = sk->F().size();
+        s[0].data = sk->F().data();
+        std::strncpy(s[1].name, "Finv", 15);
+        s[1].words = sk->Finv().size();
+        s[1].data = sk->Finv().data();
+        check(mkkg_file_write(path.c_str(), MKKG_FILE_MNTRU_SK, &m_kp, s, 2));
+    }
+    MNTRUPrivateKey LoadMNTRUSecretKey(const std::string& path) const {
+        need_keyparams();
+        const uint32_t k = m_kp.acc.k, n = m_kp.acc.n;
+        std::vector<uint32_t> F((size_t)k * n * n), Fi((size_t)k * n * n);
+        check(mkkg_file_read_section(path.c_str(), "F", F.data(), F.size()));
+        check(mkkg_file_read_section(path.c_str(), "Finv", Fi.data(), Fi.size()));
+        return std::make_shared<const MNTRUPrivateKeyImpl>(k, n, m_kp.ks.qKS, std::move(F), std::move(Fi));
+    }
+
     // ---- encryption / decryption (binfhecontext.cpp:276-292, 330-375) ----
     MNTRUCiphertext Encrypt(ConstMNTRUPrivateKey& sk, MNTRUPlaintext m, BINFHE_OUTPUT output = BOOTSTRAPPED,
                             uint32_t p = 4, uint64_t mod = 0) const {

@@ -135,6 +135,35 @@ int mkkg_mklwe_encrypt(const mkkg_params* p, uint64_t seed, const uint32_t* s, c
 int mkkg_mklwe_decrypt(const mkkg_params* p, const uint32_t* s, const uint32_t* a, const uint32_t* b, uint64_t mod,
                        uint32_t pt, uint32_t variant, size_t count, uint32_t* m);
 
+/* ---- key wire format ------------------------------------
+ * The reference has no serialization for the MK key types (binfhecontext-ser.h
+ * registers the single-key schemes only).  A key file is little-endian:
+ *   "MKFHEKEY" | u32 version (1) | u32 kind (MKKG_FILE_*) |
+ *   parameter block: 18 x u64 (every mkkg_params field; doubles as IEEE bits) |
+ *   u32 section count | per section: char name[16], u64 words, u32 data[words],
+ *   u64 FNV-1a of the data bytes
+ * so a file names the exact context it belongs to.  Readers reject a bad magic,
+ * version, truncated data or checksum with MKACC_E_ARG. */
+#define MKKG_FILE_MNTRU_SK   1  /* F, Finv                                                  */
+#define MKKG_FILE_MKLWE_SK   2  /* s                                                        */
+#define MKKG_FILE_BTKEY      3  /* crs, skN, skN_eval, skNinv, pkey, evk + ksk | ksk_a, ksk_b */
+#define MKKG_FILE_CIPHERTEXT 4  /* ct (MNTRU) | a, b (MKLWE)                                 */
+
+typedef struct mkkg_section {
+    char name[16];         /* NUL-padded */
+    uint64_t words;
+    const uint32_t* data;  /* source of mkkg_file_write */
+} mkkg_section;
+
+int mkkg_file_write(const char* path, uint32_t kind, const mkkg_params* p, const mkkg_section* sections,
+                    uint32_t count);
+/* kind, parameters and section count of a file (any output may be NULL). */
+int mkkg_file_info(const char* path, uint32_t* kind, mkkg_params* p, uint32_t* count);
+/* words of section `name`; 0 if the file has no such section or is unreadable. */
+uint64_t mkkg_file_section_words(const char* path, const char* name);
+/* read section `name` (exactly `words` words) into out, verifying its checksum. */
+int mkkg_file_read_section(const char* path, const char* name, uint32_t* out, uint64_t words);
+
 /* ---- host ring transform (the reference's EVAL order), for tests ------------ */
 int mkkg_ntt_forward(const mkkg_params* p, const uint32_t* in, uint32_t* out, size_t count);
 int mkkg_ntt_inverse(const mkkg_params* p, const uint32_t* in, uint32_t* out, size_t count);

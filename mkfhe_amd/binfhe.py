@@ -88,15 +88,30 @@ class BinFHEContext:
         if is_lwe != (self.method == MKNTRU_LWE):
             raise ConfigError("secret key type does not match the context method")
         seed = self._next()
-        bk = K.bt_keygen(self.kp, sk, seed=seed, crs_seed=(seed ^ 0xC25) if seed else None)
+        self._upload(K.bt_keygen(self.kp, sk, seed=seed, crs_seed=(seed ^ 0xC25) if seed else None))
+
+    def _upload(self, bk: K.UniEncBTKey):
         eng = self.engine()
         eng.upload_keys(bk.evk, bk.pkey)
         ks = self.kp.ks
-        if is_lwe:
+        if self.method == MKNTRU_LWE:
             eng.upload_ksk_mklwe(bk.ksk_A, bk.ksk_B, ks.qKS, ks.baseKS, ks.n_out)
         else:
             eng.upload_ksk_mntru(bk.ksk, ks.qKS, ks.baseKS, ks.n_out)
         self.BTKey = bk
+
+    # ---- key files (mkfhe_keys.h wire format) ---------------------------------------------
+    def SaveBTKey(self, path: str):
+        if self.BTKey is None:
+            raise ConfigError("no bootstrapping key generated")
+        K.save_btkey(path, self.kp, self.BTKey)
+
+    def LoadBTKey(self, path: str):
+        p, bk = K.load_btkey(path)
+        a, b = p.acc, self.kp.acc
+        if (a.method, a.k, a.n, a.Q, a.baseG, p.ks.qKS) != (b.method, b.k, b.n, b.Q, b.baseG, self.kp.ks.qKS):
+            raise ConfigError(f"{path} was generated for a different context")
+        self._upload(bk)
 
     def ctGateGen(self, sk: K.MNTRUPrivateKey, gate: int = NAND):
         if gate != NAND:

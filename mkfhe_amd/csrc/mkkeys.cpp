@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <random>
 #include <string>
@@ -761,6 +762,141 @@ int mkkg_mklwe_decrypt(const mkkg_params* pp, const uint32_t* s, const uint32_t*
             m[c] = (uint32_t)((pt / 2) * r / mod);
         }
     }
+    return MKACC_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// key wire format (include/mkfhe_keys.h)
+// ---------------------------------------------------------------------------
+namespace {
+
+constexpr char kMagic[8] = {'M', 'K', 'F', 'H', 'E', 'K', 'E', 'Y'};
+constexpr uint32_t kFileVersion = 1;
+constexpr int kParamWords = 18;
+
+uint64_t fnv1a(const void* p, size_t n, uint64_t h = 0xCBF29CE484222325ull) {
+    const unsigned char* b = static_cast<const unsigned char*>(p);
+    for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 0x100000001B3ull;
+    return h;
+}
+uint64_t dbits(double d) {
+    uint64_t u;
+    std::memcpy(&u, &d, 8);
+    return u;
+}
+double bitsd(uint64_t u) {
+    double d;
+    std::memcpy(&d, &u, 8);
+    return d;
+}
+void pack_params(const mkkg_params& p, uint64_t (&w)[kParamWords]) {
+    const uint64_t v[kParamWords] = {p.acc.method, p.acc.k, p.acc.n, p.acc.N, p.acc.Q, p.acc.q, p.acc.baseG,
+                                     p.acc.digitsG, p.acc.root, p.ks.qKS, p.ks.baseKS, p.ks.n_out,
+                                     dbits(p.sigma), dbits(p.sigma_unienc), dbits(p.sigma_r), p.lwe_keydist,
+                                     p.ring_keydist, 0};
+    for (int i = 0; i < kParamWords; ++i) w[i] = v[i];
+}
+void unpack_params(const uint64_t (&w)[kParamWords], mkkg_params& p) {
+    p = mkkg_params{};
+    p.acc.method = (uint32_t)w[0]; p.acc.k = (uint32_t)w[1]; p.acc.n = (uint32_t)w[2]; p.acc.N = (uint32_t)w[3];
+    p.acc.Q = w[4]; p.acc.q = w[5]; p.acc.baseG = (uint32_t)w[6]; p.acc.digitsG = (uint32_t)w[7]; p.acc.root = w[8];
+    p.ks.qKS = w[9]; p.ks.baseKS = (uint32_t)w[10]; p.ks.n_out = (uint32_t)w[11];
+    p.sigma = bitsd(w[12]); p.sigma_unienc = bitsd(w[13]); p.sigma_r = bitsd(w[14]);
+    p.lwe_keydist = (uint32_t)w[15]; p.ring_keydist = (uint32_t)w[16];
+}
+
+struct File {
+    FILE* f = nullptr;
+    explicit File(const char* path, const char* mode) : f(path ? std::fopen(path, mode) : nullptr) {}
+    ~File() {
+        if (f) std::fclose(f);
+    }
+    bool get(void* p, size_t n) { return std::fread(p, 1, n, f) == n; }
+    bool put(const void* p, size_t n) { return std::fwrite(p, 1, n, f) == n; }
+};
+
+// header; leaves the file positioned at the first section
+int read_header(File& fl, uint32_t* kind, mkkg_params* p, uint32_t* count) {
+    if (!fl.f) return fail(MKACC_E_ARG, "cannot open key file");
+    char magic[8];
+    uint32_t ver = 0, knd = 0, cnt = 0;
+    uint64_t w[kParamWords];
+    if (!fl.get(magic, 8) || std::memcmp(magic, kMagic, 8)) return fail(MKACC_E_ARG, "not an MKFHEKEY file");
+    if (!fl.get(&ver, 4) || ver != kFileVersion) return fail(MKACC_E_ARG, "unsupported key file version");
+    if (!fl.get(&knd, 4) || !fl.get(w, sizeof(w)) || !fl.get(&cnt, 4)) return fail(MKACC_E_ARG, "truncated key file");
+    if (kind) *kind = knd;
+    if (p) unpack_params(w, *p);
+    if (count) *count = cnt;
+    return MKACC_OK;
+}
+
+// find section `name`; on success the file is positioned at its data and *words is set
+int seek_section(File& fl, const char* name, uint64_t* words) {
+    uint32_t count = 0;
+    int rc = read_header(fl, nullptr, nullptr, &count);
+    if (rc) return rc;
+    for (uint32_t s = 0; s < count; ++s) {
+        char nm[16];
+        uint64_t w = 0;
+        if (!fl.get(nm, 16) || !fl.get(&w, 8)) return fail(MKACC_E_ARG, "truncated key file");
+        if (!std::strncmp(nm, name, 16)) {
+            *words = w;
+            return MKACC_OK;
+        }
+        if (std::fseek(fl.f, (long)(w * 4 + 8), SEEK_CUR)) return fail(MKACC_E_ARG, "truncated key file");
+    }
+    return fail(MKACC_E_ARG, std::string("key file has no section ") + name);
+}
+
+}  // namespace
+
+extern "C" {
+
+int mkkg_file_write(const char* path, uint32_t kind, const mkkg_params* p, const mkkg_section* sections,
+                    uint32_t count) {
+    if (!path || !p || (count && !sections)) return fail(MKACC_E_ARG, "null argument");
+    File fl(path, "wb");
+    if (!fl.f) return fail(MKACC_E_ARG, std::string("cannot create ") + path);
+    uint64_t w[kParamWords];
+    pack_params(*p, w);
+    bool ok = fl.put(kMagic, 8) && fl.put(&kFileVersion, 4) && fl.put(&kind, 4) && fl.put(w, sizeof(w)) &&
+              fl.put(&count, 4);
+    for (uint32_t s = 0; ok && s < count; ++s) {
+        const mkkg_section& sec = sections[s];
+        if (sec.words && !sec.data) return fail(MKACC_E_ARG, "section without data");
+        char nm[16] = {0};
+        std::strncpy(nm, sec.name, 15);
+        const uint64_t h = fnv1a(sec.data, sec.words * 4);
+        ok = fl.put(nm, 16) && fl.put(&sec.words, 8) && fl.put(sec.data, sec.words * 4) && fl.put(&h, 8);
+    }
+    if (!ok) return fail(MKACC_E_ARG, std::string("write failed: ") + path);
+    return MKACC_OK;
+}
+
+int mkkg_file_info(const char* path, uint32_t* kind, mkkg_params* p, uint32_t* count) {
+    File fl(path, "rb");
+    return read_header(fl, kind, p, count);
+}
+
+uint64_t mkkg_file_section_words(const char* path, const char* name) {
+    if (!name) return 0;
+    File fl(path, "rb");
+    uint64_t w = 0;
+    return seek_section(fl, name, &w) ? 0 : w;
+}
+
+int mkkg_file_read_section(const char* path, const char* name, uint32_t* out, uint64_t words) {
+    if (!name || (words && !out)) return fail(MKACC_E_ARG, "null argument");
+    File fl(path, "rb");
+    uint64_t w = 0;
+    int rc = seek_section(fl, name, &w);
+    if (rc) return rc;
+    if (w != words) return fail(MKACC_E_ARG, std::string("section ") + name + " has a different size");
+    uint64_t h = 0;
+    if (!fl.get(out, words * 4) || !fl.get(&h, 8)) return fail(MKACC_E_ARG, "truncated key file");
+    if (h != fnv1a(out, words * 4)) return fail(MKACC_E_ARG, std::string("checksum mismatch in section ") + name);
     return MKACC_OK;
 }
 

@@ -64,6 +64,10 @@ SIGNATURES = {
     "mkkg_mntru_decrypt": (_int, [_pp, _u32p, _u32p, _u64, _u32, _u32, _sz, _u32p]),
     "mkkg_mklwe_encrypt": (_int, [_pp, _u64, _u32p, _u32p, _u32, _sz, _u32p, _u32p]),
     "mkkg_mklwe_decrypt": (_int, [_pp, _u32p, _u32p, _u32p, _u64, _u32, _u32, _sz, _u32p]),
+    "mkkg_file_write": (_int, [ctypes.c_char_p, _u32, _pp, ctypes.c_void_p, _u32]),
+    "mkkg_file_info": (_int, [ctypes.c_char_p, ctypes.POINTER(_u32), _pp, ctypes.POINTER(_u32)]),
+    "mkkg_file_section_words": (_u64, [ctypes.c_char_p, ctypes.c_char_p]),
+    "mkkg_file_read_section": (_int, [ctypes.c_char_p, ctypes.c_char_p, _u32p, _u64]),
     "mkkg_ntt_forward": (_int, [_pp, _u32p, _u32p, _sz]),
     "mkkg_ntt_inverse": (_int, [_pp, _u32p, _u32p, _sz]),
     "mkkg_last_error": (ctypes.c_char_p, []),
@@ -261,3 +265,84 @@ def ntt_inverse(p: MkkgParams, a) -> np.ndarray:
     out = np.empty_like(a)
     _check(load().mkkg_ntt_inverse(ctypes.byref(p), _p(a), _p(out), a.size // p.acc.N))
     return out
+
+
+# ---- key wire format (mkfhe_keys.h, MKKG_FILE_*) ----------------------------------------------
+
+FILE_MNTRU_SK, FILE_MKLWE_SK, FILE_BTKEY, FILE_CIPHERTEXT = 1, 2, 3, 4
+
+
+class MkkgSection(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char * 16), ("words", ctypes.c_uint64), ("data", _u32p)]
+
+
+def write_file(path: str, kind: int, p: MkkgParams, sections: dict):
+    """Write named uint32 arrays (shapes are not stored: readers know them from the kind and p)."""
+    arrs = {k: _in(v) for k, v in sections.items() if v is not None}
+    secs = (MkkgSection * len(arrs))()
+    for s, (name, a) in zip(secs, arrs.items()):
+        s.name = name.encode()
+        s.words = a.size
+        s.data = _p(a)
+    _check(load().mkkg_file_write(os.fsencode(path), kind, ctypes.byref(p), secs, len(arrs)))
+
+
+def file_info(path: str):
+    """(kind, params, section count) of a key file."""
+    kind, cnt, p = _u32(), _u32(), MkkgParams()
+    _check(load().mkkg_file_info(os.fsencode(path), ctypes.byref(kind), ctypes.byref(p), ctypes.byref(cnt)))
+    return kind.value, p, cnt.value
+
+
+def read_section(path: str, name: str, shape) -> np.ndarray | None:
+    L = load()
+    words = L.mkkg_file_section_words(os.fsencode(path), name.encode())
+    if words == 0:
+        return None
+    out = np.empty(int(np.prod(shape)), np.uint32)
+    if out.size != words:
+        raise MkaccError(-1, f"section {name}: {words} words, expected shape {shape}")
+    _check(L.mkkg_file_read_section(os.fsencode(path), name.encode(), _p(out), words))
+    return out.reshape(shape)
+
+
+def save_secret_key(path: str, p: MkkgParams, sk):
+    if isinstance(sk, MNTRUPrivateKey):
+        write_file(path, FILE_MNTRU_SK, p, {"F": sk.F, "Finv": sk.Finv})
+    else:
+        write_file(path, FILE_MKLWE_SK, p, {"s": sk.s})
+
+
+def load_secret_key(path: str):
+    """-> (params, MNTRUPrivateKey | MKLWEPrivateKey)"""
+    kind, p, _ = file_info(path)
+    k, n = p.acc.k, p.acc.n
+    if kind == FILE_MNTRU_SK:
+        return p, MNTRUPrivateKey(read_section(path, "F", (k, n, n)), read_section(path, "Finv", (k, n, n)))
+    if kind == FILE_MKLWE_SK:
+        return p, MKLWEPrivateKey(read_section(path, "s", (k, n)))
+    raise MkaccError(-1, f"{path} is not a secret-key file (kind {kind})")
+
+
+def save_btkey(path: str, p: MkkgParams, bk: UniEncBTKey):
+    write_file(path, FILE_BTKEY, p, {"crs": bk.crs, "skN": bk.skN, "skN_eval": bk.skN_eval,
+                                     "skNinv_eval": bk.skNinv_eval, "pkey": bk.pkey, "evk": bk.evk,
+                                     "ksk": bk.ksk, "ksk_a": bk.ksk_A, "ksk_b": bk.ksk_B})
+
+
+def load_btkey(path: str):
+    """-> (params, UniEncBTKey)"""
+    kind, p, _ = file_info(path)
+    if kind != FILE_BTKEY:
+        raise MkaccError(-1, f"{path} is not a bootstrapping-key file (kind {kind})")
+    k, n, N, dg, nk, dks = dims(p)
+    B = p.ks.baseKS
+    bk = UniEncBTKey(read_section(path, "crs", (dg, N)), read_section(path, "skN", (k, N)),
+                     read_section(path, "skN_eval", (k, N)), read_section(path, "skNinv_eval", (k, N)),
+                     read_section(path, "pkey", (k, dg, N)), read_section(path, "evk", (k, nk, n + 1, dg, 2, N)))
+    if p.acc.method == 2:
+        bk.ksk_A = read_section(path, "ksk_a", (k, N, B, dks, n))
+        bk.ksk_B = read_section(path, "ksk_b", (k, N, B, dks))
+    else:
+        bk.ksk = read_section(path, "ksk", (k, N * dks, n))
+    return p, bk

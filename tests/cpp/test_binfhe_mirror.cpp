@@ -81,6 +81,16 @@ static void test_cpu() {
     }
     auto c0 = cc.Encrypt(sk, 0), c1 = cc.Encrypt(sk, 1);
     EXPECT(throws<config_error>([&] { cc.EvalBinGate(NAND, c0, c1); }));  // keys not generated
+    // secret-key file round trip (mkfhe_keys.h wire format)
+    const std::string f = std::string(std::getenv("TMPDIR") ? std::getenv("TMPDIR") : "/tmp") + "/mkfhe_sk_test.mkfk";
+    cc.SaveSecretKey(f, sk);
+    auto sk2 = cc.LoadMNTRUSecretKey(f);
+    EXPECT(sk2->F() == sk->F() && sk2->Finv() == sk->Finv());
+    MNTRUPlaintext r1 = -1;
+    cc.Decrypt2(sk2, c1, &r1);
+    EXPECT(r1 == 1);
+    std::remove(f.c_str());
+    EXPECT(throws<config_error>([&] { cc.LoadMNTRUSecretKey(f); }));
     BinFHEContext cl;
     cl.GenerateBinFHEContext(STD100_MKNTRU_LWE, MKNTRU_LWE);
     auto skl = cl.MKLWE_KeyGen();

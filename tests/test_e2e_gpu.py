@@ -74,6 +74,28 @@ def test_mklwe_nand_gates_decrypt_correctly(oracle):
 
 
 @pytest.mark.gpu
+def test_keys_from_file_drive_a_fresh_context(tmp_path):
+    """Key wire format: keys saved by one context, loaded into another, gates still decrypt."""
+    from mkfhe_amd import keys as K
+    from mkfhe_amd.binfhe import NAND
+    cc = _ctx("STD100_MKNTRU", 0, 505)
+    sk = cc.MNTRU_KeyGen()
+    cc.MKBTKeyGen(sk)
+    cc.ctGateGen(sk, NAND)
+    f_bk, f_sk = str(tmp_path / "bt.mkfk"), str(tmp_path / "sk.mkfk")
+    cc.SaveBTKey(f_bk)
+    K.save_secret_key(f_sk, cc.params, sk)
+    cc2 = _ctx("STD100_MKNTRU", 0, 606)
+    cc2.LoadBTKey(f_bk)
+    _, sk2 = K.load_secret_key(f_sk)
+    cc2.ctNAND = cc.ctNAND
+    rng = np.random.default_rng(11)
+    m1, m2 = rng.integers(0, 2, 64), rng.integers(0, 2, 64)
+    out = cc2.EvalBinGate(NAND, cc2.Encrypt(sk2, m1), cc2.Encrypt(sk2, m2))
+    assert np.array_equal(cc2.DecryptGate(sk2, out), 1 - (m1 & m2))
+
+
+@pytest.mark.gpu
 def test_mkntru_four_parties_decrypt_correctly():
     """k = 4 (STD100_MKNTRU_2): the per-party accumulator loop depth of config 3."""
     from mkfhe_amd.binfhe import NAND

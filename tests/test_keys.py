@@ -255,3 +255,53 @@ def test_error_behaviour(lib):
         cc.EvalBinGate(3, cc.Encrypt(sk, 0), cc.Encrypt(sk, 1))   # no MKBTKeyGen yet
     with pytest.raises(ConfigError):
         cc.GenerateBinFHEContext("STD100_MKNTRU", 1 + 5)
+
+
+def test_keys_header_symbols_bound_and_exported(lib):
+    """Every function include/mkfhe_keys.h declares is exported and bound in mkfhe_amd/keys.py."""
+    import re
+    from conftest import ROOT
+    txt = open(os.path.join(ROOT, "include", "mkfhe_keys.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    names = set(re.findall(r"\b(mkkg_[a-z0-9_]+)\s*\(", txt))
+    assert len(names) >= 26
+    assert names == set(K.SIGNATURES)
+    for n in names:
+        assert hasattr(lib, n), n
+    assert lib.mkkg_abi_version() == 1
+
+
+def test_key_files_roundtrip(mntru_keys, tmp_path):
+    """Key wire format: save -> load is the identity, params travel along."""
+    p, sk, bk = mntru_keys
+    f_sk, f_bk = str(tmp_path / "sk.mkfk"), str(tmp_path / "bt.mkfk")
+    K.save_secret_key(f_sk, p, sk)
+    K.save_btkey(f_bk, p, bk)
+    p2, sk2 = K.load_secret_key(f_sk)
+    assert np.array_equal(sk2.F, sk.F) and np.array_equal(sk2.Finv, sk.Finv)
+    assert (p2.acc.k, p2.acc.n, p2.acc.Q, p2.acc.root, p2.ks.qKS, p2.sigma) == \
+        (p.acc.k, p.acc.n, p.acc.Q, p.acc.root, p.ks.qKS, p.sigma)
+    p3, bk2 = K.load_btkey(f_bk)
+    for f in ("crs", "skN", "skN_eval", "skNinv_eval", "pkey", "evk", "ksk"):
+        assert np.array_equal(getattr(bk2, f), getattr(bk, f)), f
+    assert bk2.ksk_A is None
+    kind, _, count = K.file_info(f_bk)
+    assert kind == K.FILE_BTKEY and count == 7
+
+
+def test_key_file_rejects_corruption(lib, tmp_path):
+    p = K.paramset("STD100_MKNTRU_LWE", 2)
+    sk = K.mklwe_keygen(p, 77)
+    f = str(tmp_path / "s.mkfk")
+    K.save_secret_key(f, p, sk)
+    assert np.array_equal(K.load_secret_key(f)[1].s, sk.s)
+    raw = bytearray(open(f, "rb").read())
+    raw[-20] ^= 1                                  # a data byte of the last section
+    open(f, "wb").write(bytes(raw))
+    with pytest.raises(Exception, match="checksum"):
+        K.load_secret_key(f)
+    open(f, "wb").write(b"NOTAKEY!" + bytes(raw[8:]))
+    with pytest.raises(Exception, match="MKFHEKEY"):
+        K.load_secret_key(f)
+    with pytest.raises(Exception):
+        K.load_btkey(str(tmp_path / "missing.mkfk"))
