@@ -205,6 +205,14 @@ struct KeyGroup {
 // which is the same for all k parties: the first party computes it and stores
 // it to the gate's scratch, later parties load it back.
 enum DMode { D_COMPUTE = 0, D_STORE = 1, D_LOAD = 2 };
+// The store/reload of d_i (MKACC_D_SCRATCH=1) is 1% faster at k = 2 but moves
+// 2*dg*N*4 bytes per gate-step through HBM (192 MB per launch at STD128_MKNTRU,
+// B = 4096: 2.7x the algorithmic traffic, PMC profiles/round1_v14_pmc.txt);
+// recomputing it per party keeps HBM traffic near the algorithmic bytes.
+#ifndef MKACC_D_SCRATCH
+#define MKACC_D_SCRATCH 0
+#endif
+constexpr bool kDScratch = MKACC_D_SCRATCH != 0;
 
 template <int DG, int METHOD, bool FIRST, bool START, int DM>
 __device__ __forceinline__ void mac_digit(const uint32_t (&g)[kRegs], int i, uint32_t u, uint64_t (&uj)[kRegs],
@@ -422,7 +430,7 @@ __global__ __launch_bounds__(kThreads, 2) void mk_step_kernel(StepArgs a) {
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) sv[r] = 0;
     uint32_t keep[kRegs];
-    if constexpr (METHOD == XZW && !FIRST) {
+    if constexpr (METHOD == XZW && !FIRST && kDScratch) {
         // d_i is the same for all parties: the first pass computes and stores
         // it, the later ones load it (k == 1: the single pass computes it)
         if (k == 1) {
