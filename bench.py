@@ -34,9 +34,10 @@ METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 # measured on this pool (tools/ubench_intops.hip, profiles/round1_ubench_intops.txt)
 PEAK_SHOUP_MULMOD_TPS = 7.744e12     # 27-bit Shoup mod-mul / s, whole chip
 PEAK_HBM_GBS = 8000.0                # MI355X_MICROARCH.md (spec)
+Q50 = 1125899906826241               # config 5 stress modulus
 
 
-def algorithmic_counts(k: int, n: int, dg: int, nk: int, N: int = 2048, B: int = 1):
+def algorithmic_counts(k: int, n: int, dg: int, nk: int, N: int = 2048, B: int = 1, word: int = 4):
     """Per-launch algorithmic work of one accumulator step over B gates.
 
     mod-muls: (k+1)(dg+1) NTTs x N/2 log2 N butterflies (no N^-1 scaling: it is
@@ -49,8 +50,8 @@ def algorithmic_counts(k: int, n: int, dg: int, nk: int, N: int = 2048, B: int =
     ntt = (k + 1) * (dg + 1) * (N // 2) * logn
     comb = 2 * dg * N if nk == 2 else 0
     mulmods = B * (ntt + k * N + comb + (2 * k + 1) * dg * N)
-    key_bytes = nk * dg * 2 * N * 4 + k * dg * N * 4
-    bytes_ = key_bytes + B * (2 * k * N * 4 + 4)
+    key_bytes = (nk * dg * 2 * N + k * dg * N) * word
+    bytes_ = key_bytes + B * (2 * k * N * word + 4)
     return mulmods, bytes_
 
 
@@ -74,6 +75,9 @@ def parse():
     ap.add_argument("--stage", choices=["gate", "evalacc"], default="gate")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--q-bits", type=int, default=0, choices=[0, 50],
+                    help="50: config 5 stress -- the paramset's shape with the 50-bit Q = 1125899906826241 and "
+                         "B_g = 2^10 in 64-bit words (EvalAcc on the 64-bit word path)")
     ap.add_argument("--n-override", type=int, default=0,
                     help="profiling aid: shorten the LWE dimension (fewer accumulator steps); not a bench config")
     return ap.parse_args()
@@ -133,7 +137,13 @@ def main():
     p = mk.paramset(args.paramset)
     if args.n_override:
         p.n = args.n_override
+    if args.q_bits == 50:   # SURVEY.md s8 config 5 stress (s6: reference CPU 0.568 s / EvalAcc at k=2, n=560)
+        p.Q, p.baseG, p.digitsG, p.root = Q50, 1 << 10, 0, 0
+        args.stage = "evalacc"   # the 64-bit word path covers the accumulator
     eng = mk.MKAccumulatorEngine(p, device=local)
+    p = eng.params
+    wide = eng.wide
+    word = 8 if p.Q > (1 << 32) else 4
     B = args.batch
     lwe = p.method != mk.MKNTRU
     qKS, baseKS = p.q, 32                     # modKS = mod and baseKS = 32 in every MK set (binfhecontext.cpp:129-144)
@@ -143,7 +153,7 @@ def main():
     evk_n = int(np.prod(eng.evk_shape))
     pkey_n = int(np.prod(eng.pkey_shape))
     keys = shard.broadcast_keys(evk_n + pkey_n, p.Q, seed=12345, device=dev)
-    keys_h = keys.cpu().numpy().view(np.uint32)
+    keys_h = keys.cpu().numpy().view(np.uint64 if word == 8 else np.uint32)
     eng.upload_keys(keys_h[:evk_n], keys_h[evk_n:])
     del keys, keys_h
     if args.stage == "gate":
@@ -162,6 +172,8 @@ def main():
     rng = np.random.Generator(np.random.PCG64(1000 + rank))
 
     def dev_u32(a):
+        if a.dtype == np.uint64:
+            return torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(dev)
         return torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint32).view(np.int32)).to(dev)
 
     stream = torch.cuda.ExternalStream(eng.stream_handle())
@@ -210,7 +222,8 @@ def main():
     if args.stage == "gate":
         assert int(d_oa.max().item()) < qKS and int(d_oa.min().item()) >= 0
     else:
-        assert int(d_out.max().item()) < p.Q and int(d_out.min().item()) >= 0
+        hi = d_out.view(torch.int64) if word == 8 else d_out
+        assert int(hi.max().item()) < p.Q and int(hi.min().item()) >= 0
 
     # ---- dominant kernel (the accumulator step) timed live with HIP events on
     # the engine stream: one EvalAcc pass = k*n step launches (+2 tiny kernels)
@@ -228,7 +241,7 @@ def main():
 
     dg = p.digitsG - 1
     nk = 1 if lwe else 2
-    mm, by = algorithmic_counts(p.k, p.n, dg, nk, p.N, B)
+    mm, by = algorithmic_counts(p.k, p.n, dg, nk, p.N, B, word)
     stage_txt = ("NAND gates: head + BootstrapGateCore (EvalAcc) + extraction/ModSwitch/"
                  f"{'KeySwitch' if lwe else 'KeySwitch2'}") if args.stage == "gate" else "EvalAcc (blind rotation) only"
     result = {
@@ -242,20 +255,23 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u32 (27-bit residues mod Q)",
+        "dtype": "u64 (50-bit residues mod Q)" if word == 8 else "u32 (27-bit residues mod Q)",
         "data": "synthetic: uniform keys, key-switching keys and ciphertexts (seeded)",
         "config": {"workload": f"{args.paramset} {p.k}-party {'MK-LWE' if lwe else 'MK-NTRU'} {stage_txt} "
-                               f"(k={p.k}, n={p.n}, N={p.N}, dg={dg})",
+                               f"(k={p.k}, n={p.n}, N={p.N}, dg={dg}"
+                               + (f", Q={p.Q} in 64-bit words, B_g=2^{p.baseG.bit_length() - 1})" if wide else ")"),
                    "paramset": args.paramset, "stage": args.stage, "batch_per_gpu": B, "global_batch": world * B,
                    "parallelism": f"gate-sharded x{world}"},
         "roofline": {"bound": "hbm", "achieved": by / per_launch_s / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": by / per_launch_s / 1e9 / PEAK_HBM_GBS,
-                     "traffic": measured_traffic(args.paramset) if not args.n_override else None,
-                     "kernel": "mk_step_kernel", "per_launch_us": per_launch_s * 1e6,
+                     "traffic": measured_traffic(args.paramset) if not (args.n_override or wide) else None,
+                     "kernel": "wide::step_kernel" if wide else "mk_step_kernel",
+                     "per_launch_us": per_launch_s * 1e6,
                      "bytes_per_launch": by},
-        "roofline_valu": {"bound": "valu-int", "achieved": mm / per_launch_s / 1e12,
-                          "peak": PEAK_SHOUP_MULMOD_TPS / 1e12, "unit": "T mod-mul/s",
-                          "frac": mm / per_launch_s / PEAK_SHOUP_MULMOD_TPS, "mulmods_per_launch": mm},
+        # the VALU peak is the measured 32-bit Shoup rate: not a bound for 64-bit words
+        "roofline_valu": None if wide else {
+            "bound": "valu-int", "achieved": mm / per_launch_s / 1e12, "peak": PEAK_SHOUP_MULMOD_TPS / 1e12,
+            "unit": "T mod-mul/s", "frac": mm / per_launch_s / PEAK_SHOUP_MULMOD_TPS, "mulmods_per_launch": mm},
     }
     if rank == 0 and world == 1 and args.cpu_baseline:
         thr = args.cpu_threads or min(16, os.cpu_count() or 1)

@@ -55,7 +55,8 @@ typedef struct mkacc_params {
     uint32_t k;        /* number of parties (numUser) */
     uint32_t n;        /* LWE / NTRU dimension (latticeParam) */
     uint32_t N;        /* ring dimension; the engine supports N = 2048 */
-    uint64_t Q;        /* ring modulus; the engine supports 2^26 < Q < 2^28, Q = 1 mod 2N */
+    uint64_t Q;        /* ring modulus, prime, Q = 1 mod 2N, 2^26 < Q < 2^62: Q < 2^27 runs the 32-bit
+                          register-resident kernel, larger Q the 64-bit word path (EvalAcc only) */
     uint64_t q;        /* ciphertext modulus (mod); XZW computes c = floor(ct*2N/q) */
     uint32_t baseG;    /* gadget base B_g, power of two */
     uint32_t digitsG;  /* 0 = derive ceil(log Q / log B_g) as the reference does */
@@ -99,6 +100,13 @@ int mkacc_upload_keys_u64(mkacc_ctx* ctx, const uint64_t* evk, const uint64_t* p
  * Equivalent to calling the reference EvalAcc once per gate.
  */
 int mkacc_eval_batch(mkacc_ctx* ctx, const uint32_t* ct, const uint32_t* acc_in, uint32_t* acc_out, size_t B);
+/* Same with 64-bit accumulator words (NATIVE_SIZE=64, NativeInteger of 64 bits):
+ * required when Q >= 2^32; valid for every context. */
+int mkacc_eval_batch_u64(mkacc_ctx* ctx, const uint32_t* ct, const uint64_t* acc_in, uint64_t* acc_out, size_t B);
+/* 1 if the context runs the 64-bit word path (mkfhe_amd/csrc/mkacc_wide.hpp): then
+ * mkacc_eval_batch_device takes uint64_t accumulators and the gate calls are
+ * unsupported. */
+int mkacc_is_wide(const mkacc_ctx* ctx);
 
 /* Same with DEVICE pointers on the context's device; enqueued on the context
  * stream and returns without waiting (use mkacc_sync).  Used by bench.py so
@@ -160,6 +168,10 @@ int mkacc_ntt_inverse(mkacc_ctx* ctx, const uint32_t* in, uint32_t* out, size_t 
 /* UniEncAccumulator::SignedDigitDecompose(poly) (mk-acc.cpp:54-80) on `count`
  * COEFF polys: out [count][dg][N]. */
 int mkacc_sdd(mkacc_ctx* ctx, const uint32_t* in, uint32_t* out, size_t count);
+/* 64-bit-word forms of the three primitives (any context). */
+int mkacc_ntt_forward_u64(mkacc_ctx* ctx, const uint64_t* in, uint64_t* out, size_t count);
+int mkacc_ntt_inverse_u64(mkacc_ctx* ctx, const uint64_t* in, uint64_t* out, size_t count);
+int mkacc_sdd_u64(mkacc_ctx* ctx, const uint64_t* in, uint64_t* out, size_t count);
 
 /* Per-thread text of the last error ("" if none). */
 const char* mkacc_last_error(void);

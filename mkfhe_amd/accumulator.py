@@ -114,17 +114,28 @@ class MKAccumulatorEngine:
         self._key_token = (id(evk), id(pkey))
 
     # -- evaluation -------------------------------------------------------------
+    @property
+    def wide(self) -> bool:
+        """True if the context runs the 64-bit word path (Q >= 2^27)."""
+        return bool(_lib.load().mkacc_is_wide(self._h))
+
     def eval_batch(self, ct: np.ndarray, acc: np.ndarray) -> np.ndarray:
-        """EvalAcc on B gates: ct [B][k][n], acc [B][k][N] EVAL -> new acc."""
+        """EvalAcc on B gates: ct [B][k][n], acc [B][k][N] EVAL -> new acc.
+        uint64 accumulators (or Q >= 2^32) go through mkacc_eval_batch_u64."""
         ct32 = np.ascontiguousarray(ct, dtype=np.uint32)
-        acc32 = np.ascontiguousarray(acc, dtype=np.uint32)
+        use64 = acc.dtype == np.uint64 or self.Q >= (1 << 32)
+        accw = np.ascontiguousarray(acc, dtype=np.uint64 if use64 else np.uint32)
         if ct32.ndim != 3 or ct32.shape[1:] != (self.k, self.n):
             raise MkaccError(_lib.MKACC_E_ARG, f"ct must be [B][{self.k}][{self.n}]")
         B = ct32.shape[0]
-        if acc32.shape != (B, self.k, self.N):
+        if accw.shape != (B, self.k, self.N):
             raise MkaccError(_lib.MKACC_E_ARG, f"acc must be [B][{self.k}][{self.N}]")
-        out = np.empty_like(acc32)
-        check(_lib.load().mkacc_eval_batch(self._h, _u32(ct32), _u32(acc32), _u32(out), B))
+        out = np.empty_like(accw)
+        if use64:
+            check(_lib.load().mkacc_eval_batch_u64(self._h, _u32(ct32), accw.ctypes.data_as(_u64p),
+                                                   out.ctypes.data_as(_u64p), B))
+        else:
+            check(_lib.load().mkacc_eval_batch(self._h, _u32(ct32), _u32(accw), _u32(out), B))
         return out
 
     def eval_batch_device(self, d_ct, d_acc_in, d_acc_out, B: int):
@@ -204,23 +215,29 @@ class MKAccumulatorEngine:
         return oa if self.method == MKNTRU else (oa, ob)
 
     # -- primitives -------------------------------------------------------------
-    def _prim(self, fn, a: np.ndarray, out_mul: int):
+    def _prim(self, name: str, a: np.ndarray, out_mul: int):
+        L = _lib.load()
+        if a.dtype == np.uint64 or self.wide:   # 64-bit word entry points
+            x = np.ascontiguousarray(a, dtype=np.uint64).reshape(-1, self.N)
+            out = np.empty((x.shape[0] * out_mul, self.N), dtype=np.uint64)
+            check(getattr(L, name + "_u64")(self._h, x.ctypes.data_as(_u64p), out.ctypes.data_as(_u64p), x.shape[0]))
+            return out
         x = np.ascontiguousarray(a, dtype=np.uint32).reshape(-1, self.N)
         out = np.empty((x.shape[0] * out_mul, self.N), dtype=np.uint32)
-        check(fn(self._h, _u32(x), _u32(out), x.shape[0]))
+        check(getattr(L, name)(self._h, _u32(x), _u32(out), x.shape[0]))
         return out
 
     def ntt_forward(self, a: np.ndarray) -> np.ndarray:
         """NativePoly::SetFormat(EVALUATION) on rows of a."""
-        return self._prim(_lib.load().mkacc_ntt_forward, a, 1)
+        return self._prim("mkacc_ntt_forward", a, 1)
 
     def ntt_inverse(self, a: np.ndarray) -> np.ndarray:
         """NativePoly::SetFormat(COEFFICIENT) on rows of a."""
-        return self._prim(_lib.load().mkacc_ntt_inverse, a, 1)
+        return self._prim("mkacc_ntt_inverse", a, 1)
 
     def sdd(self, a: np.ndarray) -> np.ndarray:
         """SignedDigitDecompose (mk-acc.cpp:54-80): rows -> [rows][dg][N]."""
-        out = self._prim(_lib.load().mkacc_sdd, a, self.dg)
+        out = self._prim("mkacc_sdd", a, self.dg)
         return out.reshape(-1, self.dg, self.N)
 
 

@@ -583,6 +583,7 @@ StepFn step_fn(int dg, int method, bool first);
 }  // namespace
 
 #include "mkacc_gate.hpp"
+#include "mkacc_wide.hpp"
 
 namespace {
 
@@ -638,6 +639,22 @@ struct mkacc_ctx {
     uint32_t* d_bh = nullptr;      // [B] MK-LWE rotation b
     uint32_t* d_gin = nullptr;     // host API staging of gate inputs
     uint32_t* d_gout = nullptr;
+    // 64-bit word path (mkacc_wide.hpp), used when Q does not fit the 27-bit kernel
+    bool wide = false;
+    wide::Mod64 wm{};
+    wide::Sdd64 wsd{};
+    uint64_t wninv = 0, wninvp = 0;
+    ulonglong2* d_wtwf = nullptr;  // forward table {w, w'} (reference order)
+    ulonglong2* d_wtwi = nullptr;
+    ulonglong2* d_wpsi = nullptr;  // psi^e, e < 2N
+    uint64_t* d_wkeys = nullptr;   // [k][n+1][nk][dg][2][N] EVAL
+    uint64_t* d_wpkey = nullptr;   // [k][dg][N]
+    size_t wws_B = 0, wio_B = 0;
+    uint64_t* d_wacc0 = nullptr;
+    uint64_t* d_wacc1 = nullptr;
+    uint32_t* d_wcvals = nullptr;
+    uint32_t* d_wct = nullptr;     // host-pointer API staging
+    uint64_t* d_wio = nullptr;
     std::mutex mu;
 };
 
@@ -929,6 +946,200 @@ int prim_launch(mkacc_ctx* c, const uint32_t* in, uint32_t* out, size_t count, s
     return MKACC_OK;
 }
 
+// ---- 64-bit word path (mkacc_wide.hpp) --------------------------------------------
+
+int wide_setup(mkacc_ctx* c) {
+    using u128 = unsigned __int128;
+    const uint64_t Q = c->p.Q;
+    const uint32_t L = 64u - (uint32_t)__builtin_clzll(Q);
+    c->wm = wide::Mod64{Q, (uint64_t)(((u128)1 << (2 * L)) / Q), L};
+    const uint32_t b = (uint32_t)__builtin_ctz(c->p.baseG);
+    uint64_t C = 0;
+    for (uint32_t i = 0; i < c->p.digitsG; ++i) C += (1ull << (b - 1)) << (b * i);
+    c->wsd = wide::Sdd64{Q >> 1, C, C - Q, 1ull << (b - 1), b};
+    auto comp = [Q](uint64_t w) { return (uint64_t)(((u128)w << 64) / Q); };
+    c->wninv = modinv(kN, Q);
+    c->wninvp = comp(c->wninv);
+    std::vector<ulonglong2> tf(kN), ti(kN), pw(2 * kN);
+    const uint64_t psi = c->p.root, psii = modinv(psi, Q);
+    uint64_t x = 1, xi = 1;
+    for (uint32_t i = 0; i < (uint32_t)kN; ++i) {
+        const uint32_t r = bit_reverse(i, kLogN);
+        tf[r] = make_ulonglong2(x, comp(x));
+        ti[r] = make_ulonglong2(xi, comp(xi));
+        x = mulmod(x, psi, Q);
+        xi = mulmod(xi, psii, Q);
+    }
+    uint64_t e = 1;
+    for (uint32_t i = 0; i < 2u * kN; ++i) {
+        pw[i] = make_ulonglong2(e, comp(e));
+        e = mulmod(e, psi, Q);
+    }
+    HIP_TRY(hipMalloc(&c->d_wtwf, kN * sizeof(ulonglong2)));
+    HIP_TRY(hipMalloc(&c->d_wtwi, kN * sizeof(ulonglong2)));
+    HIP_TRY(hipMalloc(&c->d_wpsi, 2 * kN * sizeof(ulonglong2)));
+    HIP_TRY(hipMemcpy(c->d_wtwf, tf.data(), kN * sizeof(ulonglong2), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c->d_wtwi, ti.data(), kN * sizeof(ulonglong2), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c->d_wpsi, pw.data(), 2 * kN * sizeof(ulonglong2), hipMemcpyHostToDevice));
+    return MKACC_OK;
+}
+
+// reference [k][nk][n+1][dg][2][N] -> device [k][n+1][nk][dg][2][N] (same EVAL order, no scaling)
+template <typename W>
+int wide_upload_keys(mkacc_ctx* c, const W* evk, const W* pkey) {
+    if (!evk || !pkey) return fail(MKACC_E_ARG, "null key pointer");
+    const uint64_t Q = c->p.Q;
+    const uint32_t k = c->p.k, n = c->p.n, nk = c->nk, dg = c->dg;
+    const size_t blk = (size_t)dg * 2 * kN;
+    std::vector<uint64_t> host((size_t)k * (n + 1) * nk * blk);
+    for (uint32_t u = 0; u < k; ++u)
+        for (uint32_t j = 0; j < nk; ++j)
+            for (uint32_t i = 0; i <= n; ++i) {
+                const W* src = evk + (((size_t)u * nk + j) * (n + 1) + i) * blk;
+                uint64_t* dst = host.data() + (((size_t)u * (n + 1) + i) * nk + j) * blk;
+                for (size_t s = 0; s < blk; ++s) {
+                    if ((uint64_t)src[s] >= Q) return fail(MKACC_E_RANGE, "evk word not a canonical residue mod Q");
+                    dst[s] = (uint64_t)src[s];
+                }
+            }
+    const size_t pw = (size_t)k * dg * kN;
+    std::vector<uint64_t> hp(pw);
+    for (size_t s = 0; s < pw; ++s) {
+        if ((uint64_t)pkey[s] >= Q) return fail(MKACC_E_RANGE, "pkey word not a canonical residue mod Q");
+        hp[s] = (uint64_t)pkey[s];
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    if (!c->d_wkeys) HIP_TRY(hipMalloc(&c->d_wkeys, host.size() * 8));
+    if (!c->d_wpkey) HIP_TRY(hipMalloc(&c->d_wpkey, pw * 8));
+    HIP_TRY(hipMemcpy(c->d_wkeys, host.data(), host.size() * 8, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c->d_wpkey, hp.data(), pw * 8, hipMemcpyHostToDevice));
+    c->have_keys = true;
+    return MKACC_OK;
+}
+
+int wide_ensure_ws(mkacc_ctx* c, size_t B) {
+    if (B <= c->wws_B) return MKACC_OK;
+    for (void* p : {(void*)c->d_wacc0, (void*)c->d_wacc1, (void*)c->d_wcvals})
+        if (p) HIP_TRY(hipFree(p));
+    c->d_wacc0 = c->d_wacc1 = nullptr;
+    c->d_wcvals = nullptr;
+    c->wws_B = 0;
+    const size_t accw = B * c->p.k * (size_t)kN;
+    HIP_TRY(hipMalloc(&c->d_wacc0, accw * 8));
+    HIP_TRY(hipMalloc(&c->d_wacc1, accw * 8));
+    HIP_TRY(hipMalloc(&c->d_wcvals, B * c->p.k * (size_t)c->p.n * 4));
+    c->wws_B = B;
+    return MKACC_OK;
+}
+
+// k*n wide steps over a batch on device buffers (d_in may alias d_out)
+int wide_launch_batch(mkacc_ctx* c, const uint32_t* d_ct, const uint64_t* d_in, uint64_t* d_out, size_t B) {
+    if (!c->have_keys) return fail(MKACC_E_NOKEYS, "Bootstrapping keys have not been generated/uploaded");
+    if (B == 0) return MKACC_OK;
+    int rc = wide_ensure_ws(c, B);
+    if (rc) return rc;
+    const uint32_t k = c->p.k, n = c->p.n;
+    const size_t tot = B * (size_t)k * n, accb = B * (size_t)k * kN * 8;
+    hipLaunchKernelGGL(prep_c_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, c->stream, d_ct, c->d_wcvals,
+                       (uint32_t)B, k * n, (uint32_t)c->method_class, (uint32_t)c->p.q);
+    HIP_TRY(hipMemcpyAsync(c->d_wacc0, d_in, accb, hipMemcpyDeviceToDevice, c->stream));
+    uint64_t* cur = c->d_wacc0;
+    uint64_t* nxt = c->d_wacc1;
+    const size_t blk = (size_t)c->dg * 2 * kN;
+    auto key = [&](uint32_t u, uint32_t i, uint32_t j) {
+        return c->d_wkeys + (((size_t)u * (n + 1) + i) * c->nk + j) * blk;
+    };
+    for (uint32_t u = 0; u < k; ++u)
+        for (uint32_t i = 0; i < n; ++i) {
+            const bool first = (u == 0 && i == 0);
+            wide::StepArgs a;
+            a.acc_in = cur;
+            a.acc_out = nxt;
+            a.cvals = c->d_wcvals + ((size_t)u * n + i) * B;
+            a.key1 = key(u, i, 0);
+            a.key2 = c->nk == 2 ? key(u, i, 1) : a.key1;
+            a.keys = key(0, n, 0);
+            a.pkey = c->d_wpkey;
+            a.twf = c->d_wtwf;
+            a.twi = c->d_wtwi;
+            a.psi = c->d_wpsi;
+            a.k = k;
+            a.index = u;
+            a.dg = c->dg;
+            a.ninv = c->wninv;
+            a.ninvp = c->wninvp;
+            a.m = c->wm;
+            a.sd = c->wsd;
+            void (*fn)(wide::StepArgs);
+            if (c->method_class == XZW) fn = first ? wide::step_kernel<XZW, true> : wide::step_kernel<XZW, false>;
+            else fn = first ? wide::step_kernel<XZW_B, true> : wide::step_kernel<XZW_B, false>;
+            hipLaunchKernelGGL(fn, dim3((unsigned)B), dim3(wide::kThreads), 0, c->stream, a);
+            std::swap(cur, nxt);
+        }
+    HIP_TRY(hipMemcpyAsync(d_out, cur, accb, hipMemcpyDeviceToDevice, c->stream));
+    HIP_TRY(hipGetLastError());
+    return MKACC_OK;
+}
+
+// host-pointer batch through the wide path
+int wide_eval_host(mkacc_ctx* c, const uint32_t* ct, const uint64_t* acc_in, uint64_t* acc_out, size_t B) {
+    const size_t ctw = B * c->p.k * (size_t)c->p.n, accw = B * c->p.k * (size_t)kN;
+    HIP_TRY(hipSetDevice(c->device));
+    if (B > c->wio_B) {
+        if (c->d_wct) HIP_TRY(hipFree(c->d_wct));
+        if (c->d_wio) HIP_TRY(hipFree(c->d_wio));
+        c->d_wct = nullptr;
+        c->d_wio = nullptr;
+        c->wio_B = 0;
+        HIP_TRY(hipMalloc(&c->d_wct, ctw * 4));
+        HIP_TRY(hipMalloc(&c->d_wio, accw * 8));
+        c->wio_B = B;
+    }
+    HIP_TRY(hipMemcpyAsync(c->d_wct, ct, ctw * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->d_wio, acc_in, accw * 8, hipMemcpyHostToDevice, c->stream));
+    int rc = wide_launch_batch(c, c->d_wct, c->d_wio, c->d_wio, B);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(acc_out, c->d_wio, accw * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return MKACC_OK;
+}
+
+int wide_prim(mkacc_ctx* c, const uint64_t* in, uint64_t* out, size_t count, int which) {
+    if (count == 0) return MKACC_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    const uint64_t Q = c->p.Q;
+    for (size_t s = 0; s < count * kN; ++s)
+        if (in[s] >= Q) return fail(MKACC_E_RANGE, "input word not a canonical residue mod Q");
+    const size_t out_mul = which == 2 ? c->dg : 1;
+    uint64_t *din = nullptr, *dout = nullptr;
+    HIP_TRY(hipMalloc(&din, count * kN * 8));
+    HIP_TRY(hipMalloc(&dout, count * kN * 8 * out_mul));
+    HIP_TRY(hipMemcpyAsync(din, in, count * kN * 8, hipMemcpyHostToDevice, c->stream));
+    if (which == 0)
+        hipLaunchKernelGGL(wide::ntt_fwd_kernel, dim3((unsigned)count), dim3(wide::kThreads), 0, c->stream, din, dout,
+                           c->d_wtwf, Q);
+    else if (which == 1)
+        hipLaunchKernelGGL(wide::ntt_inv_kernel, dim3((unsigned)count), dim3(wide::kThreads), 0, c->stream, din, dout,
+                           c->d_wtwi, Q, c->wninv, c->wninvp);
+    else
+        hipLaunchKernelGGL(wide::sdd_kernel, dim3((unsigned)((count * kN + 255) / 256)), dim3(256), 0, c->stream, din,
+                           dout, (uint32_t)count, c->dg, c->wsd, Q);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(out, dout, count * kN * 8 * out_mul, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipFree(din));
+    HIP_TRY(hipFree(dout));
+    return MKACC_OK;
+}
+
+int check_batch_inputs(const mkacc_ctx* c, const uint32_t* ct, size_t B) {
+    const size_t ctw = B * c->p.k * (size_t)c->p.n;
+    const uint64_t lim = c->method_class == XZW ? c->p.q : 2ull * kN + 1;  // XZW_B: c <= 2N (2N -> 0)
+    for (size_t s = 0; s < ctw; ++s)
+        if (ct[s] >= lim) return fail(MKACC_E_RANGE, "ciphertext word out of range");
+    return MKACC_OK;
+}
+
 }  // namespace
 
 // ---- C ABI ------------------------------------------------------------------------
@@ -964,7 +1175,8 @@ int mkacc_create(const mkacc_params* pin, int device, mkacc_ctx** out) {
     mkacc_params p = *pin;
     if (p.method > MKACC_METHOD_MKNTRU_LWE) return fail(MKACC_E_ARG, "method is invalid");
     if (p.N != (uint32_t)kN) return fail(MKACC_E_UNSUPPORTED, "engine supports ring dimension N = 2048 only");
-    if (!(p.Q > (1ull << 26) && p.Q < (1ull << 27))) return fail(MKACC_E_UNSUPPORTED, "engine supports 2^26 < Q < 2^27");
+    if (!(p.Q > (1ull << 26) && p.Q < (1ull << 62)))
+        return fail(MKACC_E_UNSUPPORTED, "engine supports 2^26 < Q < 2^62");
     if ((p.Q - 1) % (2ull * p.N) != 0 || !is_prime(p.Q)) return fail(MKACC_E_ARG, "Q must be a prime = 1 mod 2N");
     if (p.k == 0 || p.k > 64 || p.n == 0) return fail(MKACC_E_ARG, "bad k or n");
     if (p.baseG < 2 || (p.baseG & (p.baseG - 1))) return fail(MKACC_E_ARG, "Gadget base should be a power of two.");
@@ -972,13 +1184,21 @@ int mkacc_create(const mkacc_params* pin, int device, mkacc_ctx** out) {
         return fail(MKACC_E_ARG, "bad ciphertext modulus q");
     if (p.digitsG == 0) p.digitsG = digits_g(p.Q, p.baseG);
     if (p.root == 0) p.root = root_of_unity(2ull * p.N, p.Q);
+    if (p.digitsG < 2) return fail(MKACC_E_ARG, "digitsG must be at least 2");
     const uint32_t dg = p.digitsG - 1;
-    if (dg < 2 || dg > 5) return fail(MKACC_E_UNSUPPORTED, "engine supports 2..5 used gadget digits");
-    if ((uint32_t)__builtin_ctz(p.baseG) * p.digitsG > 32)
-        return fail(MKACC_E_UNSUPPORTED, "engine supports log2(baseG) * digitsG <= 32");
-    if ((uint32_t)__builtin_ctz(p.baseG) * (dg - 1) > (dg <= 3 ? 16u : 20u) ||
-        (dg > 3 && 2u * __builtin_ctz(p.baseG) + 20u > 32u))
-        return fail(MKACC_E_UNSUPPORTED, "engine packs gadget digits 2..dg into 16 (dg <= 3) or 20 bits");
+    const uint32_t gb = (uint32_t)__builtin_ctz(p.baseG);
+    // the 27-bit register-resident kernel, or the 64-bit LDS-tile path (mkacc_wide.hpp)
+    std::string why;
+    if (!(p.Q < (1ull << 27))) why = "Q >= 2^27";
+    else if (dg < 2 || dg > 5) why = "dg outside 2..5";
+    else if (gb * p.digitsG > 32) why = "log2(baseG) * digitsG > 32";
+    else if (gb * (dg - 1) > (dg <= 3 ? 16u : 20u) || (dg > 3 && 2u * gb + 20u > 32u))
+        why = "digits 2..dg do not pack into 16 (dg <= 3) or 20 bits";
+    const char* eng = std::getenv("MKACC_ENGINE");
+    if (eng && !std::strcmp(eng, "wide")) why = "MKACC_ENGINE=wide";
+    const bool wide = !why.empty();
+    if (wide && (dg > 8 || gb * p.digitsG > 63))
+        return fail(MKACC_E_UNSUPPORTED, "engine supports dg <= 8 and log2(baseG) * digitsG <= 63 (" + why + ")");
     if (!is_primitive_root(p.root, 2ull * p.N, p.Q)) return fail(MKACC_E_ARG, "root is not a primitive 2N-th root");
 
     auto c = std::make_unique<mkacc_ctx>();
@@ -987,6 +1207,18 @@ int mkacc_create(const mkacc_params* pin, int device, mkacc_ctx** out) {
     c->method_class = p.method == MKACC_METHOD_MKNTRU ? XZW : XZW_B;
     c->dg = dg;
     c->nk = c->method_class == XZW ? 2 : 1;
+    c->wide = wide;
+    if (wide) {
+        HIP_TRY(hipSetDevice(device));
+        HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        const int rc = wide_setup(c.get());
+        if (rc) {
+            mkacc_destroy(c.release());
+            return rc;
+        }
+        *out = c.release();
+        return MKACC_OK;
+    }
     c->mod.Q = (uint32_t)p.Q;
     c->mod.mu = (uint32_t)((1ull << 58) / p.Q);
     c->mod.r32 = (uint32_t)((1ull << 32) % p.Q);
@@ -1057,7 +1289,9 @@ void mkacc_destroy(mkacc_ctx* c) {
     for (void* p : {(void*)c->d_twf, (void*)c->d_twi, (void*)c->d_img, (void*)c->d_keys, (void*)c->d_pkey,
                     (void*)c->d_acc0, (void*)c->d_acc1, (void*)c->d_cvals, (void*)c->d_deff, (void*)c->d_ct,
                     (void*)c->d_io, (void*)c->d_ksk, (void*)c->d_lweA, (void*)c->d_lweB, (void*)c->d_tv,
-                    (void*)c->d_digits, (void*)c->d_bh, (void*)c->d_gin, (void*)c->d_gout})
+                    (void*)c->d_digits, (void*)c->d_bh, (void*)c->d_gin, (void*)c->d_gout, (void*)c->d_wtwf,
+                    (void*)c->d_wtwi, (void*)c->d_wpsi, (void*)c->d_wkeys, (void*)c->d_wpkey, (void*)c->d_wacc0,
+                    (void*)c->d_wacc1, (void*)c->d_wcvals, (void*)c->d_wct, (void*)c->d_wio})
         if (p) (void)hipFree(p);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -1077,23 +1311,56 @@ size_t mkacc_pkey_words(const mkacc_ctx* c) { return c ? (size_t)c->p.k * c->dg 
 int mkacc_upload_keys(mkacc_ctx* c, const uint32_t* evk, const uint32_t* pkey) {
     if (!c) return fail(MKACC_E_ARG, "null context");
     std::lock_guard<std::mutex> g(c->mu);
+    if (c->wide) return wide_upload_keys<uint32_t>(c, evk, pkey);
     return upload_keys_impl<uint32_t>(c, evk, pkey);
 }
 int mkacc_upload_keys_u64(mkacc_ctx* c, const uint64_t* evk, const uint64_t* pkey) {
     if (!c) return fail(MKACC_E_ARG, "null context");
     std::lock_guard<std::mutex> g(c->mu);
+    if (c->wide) return wide_upload_keys<uint64_t>(c, evk, pkey);
     return upload_keys_impl<uint64_t>(c, evk, pkey);
+}
+
+int mkacc_is_wide(const mkacc_ctx* c) { return c && c->wide ? 1 : 0; }
+
+int mkacc_eval_batch_u64(mkacc_ctx* c, const uint32_t* ct, const uint64_t* acc_in, uint64_t* acc_out, size_t B) {
+    if (!c || !ct || !acc_in || !acc_out) return fail(MKACC_E_ARG, "null argument");
+    if (!c->have_keys) return fail(MKACC_E_NOKEYS, "Bootstrapping keys have not been generated. Please call MKBTKeyGen before calling bootstrapping.");
+    if (B == 0) return MKACC_OK;
+    const size_t accw = B * c->p.k * (size_t)kN;
+    for (size_t s = 0; s < accw; ++s)
+        if (acc_in[s] >= c->p.Q) return fail(MKACC_E_RANGE, "accumulator word not a canonical residue mod Q");
+    if (!c->wide) {   // 27-bit kernel: narrow, run, widen
+        std::vector<uint32_t> a32(acc_in, acc_in + accw);
+        const int rc = mkacc_eval_batch(c, ct, a32.data(), a32.data(), B);
+        if (rc) return rc;
+        for (size_t s = 0; s < accw; ++s) acc_out[s] = a32[s];
+        return MKACC_OK;
+    }
+    std::lock_guard<std::mutex> g(c->mu);
+    const int rc = check_batch_inputs(c, ct, B);
+    if (rc) return rc;
+    return wide_eval_host(c, ct, acc_in, acc_out, B);
 }
 
 int mkacc_eval_batch(mkacc_ctx* c, const uint32_t* ct, const uint32_t* acc_in, uint32_t* acc_out, size_t B) {
     if (!c || !ct || !acc_in || !acc_out) return fail(MKACC_E_ARG, "null argument");
+    if (c->wide) {
+        if (c->p.Q > 0xFFFFFFFFull)
+            return fail(MKACC_E_UNSUPPORTED, "Q >= 2^32 does not fit 32-bit words: use mkacc_eval_batch_u64");
+        const size_t accw = B * c->p.k * (size_t)kN;
+        std::vector<uint64_t> a64(acc_in, acc_in + accw);
+        const int rc = mkacc_eval_batch_u64(c, ct, a64.data(), a64.data(), B);
+        if (rc) return rc;
+        for (size_t s = 0; s < accw; ++s) acc_out[s] = (uint32_t)a64[s];
+        return MKACC_OK;
+    }
     std::lock_guard<std::mutex> g(c->mu);
     if (!c->have_keys) return fail(MKACC_E_NOKEYS, "Bootstrapping keys have not been generated. Please call MKBTKeyGen before calling bootstrapping.");
     if (B == 0) return MKACC_OK;
     const size_t ctw = B * c->p.k * (size_t)c->p.n, accw = B * c->p.k * (size_t)kN;
-    const uint64_t lim = c->method_class == XZW ? c->p.q : 2ull * kN + 1;  // XZW_B: c <= 2N (2N -> 0)
-    for (size_t s = 0; s < ctw; ++s)
-        if (ct[s] >= lim) return fail(MKACC_E_RANGE, "ciphertext word out of range");
+    int rc0 = check_batch_inputs(c, ct, B);
+    if (rc0) return rc0;
     for (size_t s = 0; s < accw; ++s)
         if (acc_in[s] >= c->p.Q) return fail(MKACC_E_RANGE, "accumulator word not a canonical residue mod Q");
     HIP_TRY(hipSetDevice(c->device));
@@ -1119,6 +1386,9 @@ int mkacc_eval_batch_device(mkacc_ctx* c, const uint32_t* d_ct, const uint32_t* 
     if (!c || !d_ct || !d_in || !d_out) return fail(MKACC_E_ARG, "null argument");
     std::lock_guard<std::mutex> g(c->mu);
     HIP_TRY(hipSetDevice(c->device));
+    if (c->wide)   // 64-bit words: d_in / d_out hold [B][k][N] uint64_t
+        return wide_launch_batch(c, d_ct, reinterpret_cast<const uint64_t*>(d_in), reinterpret_cast<uint64_t*>(d_out),
+                                 B);
     return launch_batch(c, d_ct, d_in, d_out, B);
 }
 
@@ -1143,6 +1413,7 @@ int check_ks(mkacc_ctx* c, const mkacc_ks_params* ks) {
 int mkacc_upload_ksk_mntru(mkacc_ctx* c, const mkacc_ks_params* ks, const uint32_t* ksk) {
     if (!c || !ksk) return fail(MKACC_E_ARG, "null argument");
     std::lock_guard<std::mutex> g(c->mu);
+    if (c->wide) return fail(MKACC_E_UNSUPPORTED, "the 64-bit word path covers EvalAcc only; NAND gates need Q < 2^27");
     if (c->method_class != XZW) return fail(MKACC_E_ARG, "KeySwitch2 keys belong to the MKNTRU method");
     int rc = check_ks(c, ks);
     if (rc) return rc;
@@ -1172,6 +1443,7 @@ int mkacc_upload_ksk_mntru(mkacc_ctx* c, const mkacc_ks_params* ks, const uint32
 int mkacc_upload_ksk_mklwe(mkacc_ctx* c, const mkacc_ks_params* ks, const uint32_t* A, const uint32_t* B) {
     if (!c || !A || !B) return fail(MKACC_E_ARG, "null argument");
     std::lock_guard<std::mutex> g(c->mu);
+    if (c->wide) return fail(MKACC_E_UNSUPPORTED, "the 64-bit word path covers EvalAcc only; NAND gates need Q < 2^27");
     if (c->method_class != XZW_B) return fail(MKACC_E_ARG, "MK-LWE KeySwitch keys belong to the MKNTRU_LWE method");
     int rc = check_ks(c, ks);
     if (rc) return rc;
@@ -1245,6 +1517,7 @@ int mkacc_eval_nand_mntru(mkacc_ctx* c, const uint32_t* ct_nand, const uint32_t*
                           uint32_t* out, size_t B) {
     if (!c || !ct_nand || !ct1 || !ct2 || !out) return fail(MKACC_E_ARG, "null argument");
     std::lock_guard<std::mutex> g(c->mu);
+    if (c->wide) return fail(MKACC_E_UNSUPPORTED, "the 64-bit word path covers EvalAcc only; NAND gates need Q < 2^27");
     if (c->method_class != XZW) return fail(MKACC_E_ARG, "method is not MKNTRU");
     if (ct1 == ct2) return fail(MKACC_E_ARG, "Input ciphertexts should be independant");
     if (B == 0) return MKACC_OK;
@@ -1255,6 +1528,7 @@ int mkacc_eval_nand_mklwe(mkacc_ctx* c, const uint32_t* a1, const uint32_t* b1, 
                           const uint32_t* b2, uint32_t* out_a, uint32_t* out_b, size_t B) {
     if (!c || !a1 || !b1 || !a2 || !b2 || !out_a || !out_b) return fail(MKACC_E_ARG, "null argument");
     std::lock_guard<std::mutex> g(c->mu);
+    if (c->wide) return fail(MKACC_E_UNSUPPORTED, "the 64-bit word path covers EvalAcc only; NAND gates need Q < 2^27");
     if (c->method_class != XZW_B) return fail(MKACC_E_ARG, "method is not MKNTRU_LWE / MKNTRU_B");
     if (a1 == a2) return fail(MKACC_E_ARG, "Input ciphertexts should be independant");
     if (B == 0) return MKACC_OK;
@@ -1265,6 +1539,7 @@ int mkacc_eval_nand_device(mkacc_ctx* c, const uint32_t* d_ct_nand, const uint32
                            const uint32_t* d_a2, const uint32_t* d_b2, uint32_t* d_out_a, uint32_t* d_out_b,
                            size_t B) {
     if (!c || !d_a1 || !d_a2 || !d_out_a) return fail(MKACC_E_ARG, "null argument");
+    if (c->wide) return fail(MKACC_E_UNSUPPORTED, "the 64-bit word path covers EvalAcc only; NAND gates need Q < 2^27");
     std::lock_guard<std::mutex> g(c->mu);
     if (c->method_class == XZW && !d_ct_nand) return fail(MKACC_E_ARG, "null ctNAND");
     if (c->method_class == XZW_B && (!d_b1 || !d_b2 || !d_out_b)) return fail(MKACC_E_ARG, "null b");
@@ -1275,6 +1550,7 @@ int mkacc_eval_nand_device(mkacc_ctx* c, const uint32_t* d_ct_nand, const uint32
 int mkacc_gate_tail(mkacc_ctx* c, const uint32_t* acc, uint32_t* out_a, uint32_t* out_b, size_t B) {
     if (!c || !acc || !out_a || (c->method_class == XZW_B && !out_b)) return fail(MKACC_E_ARG, "null argument");
     std::lock_guard<std::mutex> g(c->mu);
+    if (c->wide) return fail(MKACC_E_UNSUPPORTED, "the 64-bit word path covers EvalAcc only; NAND gates need Q < 2^27");
     if (!c->have_ksk) return fail(MKACC_E_NOKEYS, "Key-switching keys have not been uploaded");
     if (B == 0) return MKACC_OK;
     const size_t npoly = B * c->p.k, kno = (size_t)c->p.k * c->ks.n_out;
@@ -1310,17 +1586,49 @@ void* mkacc_stream(mkacc_ctx* c) { return c ? (void*)c->stream : nullptr; }
 int mkacc_ntt_forward(mkacc_ctx* c, const uint32_t* in, uint32_t* out, size_t count) {
     if (!c) return fail(MKACC_E_ARG, "null context");
     std::lock_guard<std::mutex> g(c->mu);
+    if (c->wide) return fail(MKACC_E_UNSUPPORTED, "64-bit word context: use the _u64 primitive");
     return prim_launch(c, in, out, count, 1, 0);
 }
 int mkacc_ntt_inverse(mkacc_ctx* c, const uint32_t* in, uint32_t* out, size_t count) {
     if (!c) return fail(MKACC_E_ARG, "null context");
     std::lock_guard<std::mutex> g(c->mu);
+    if (c->wide) return fail(MKACC_E_UNSUPPORTED, "64-bit word context: use the _u64 primitive");
     return prim_launch(c, in, out, count, 1, 1);
 }
 int mkacc_sdd(mkacc_ctx* c, const uint32_t* in, uint32_t* out, size_t count) {
     if (!c) return fail(MKACC_E_ARG, "null context");
     std::lock_guard<std::mutex> g(c->mu);
+    if (c->wide) return fail(MKACC_E_UNSUPPORTED, "64-bit word context: use the _u64 primitive");
     return prim_launch(c, in, out, count, c->dg, 2);
+}
+
+namespace {
+// 64-bit primitives: the wide kernels, or the 27-bit ones through narrowed words
+int prim_u64(mkacc_ctx* c, const uint64_t* in, uint64_t* out, size_t count, int which) {
+    if (!c || !in || !out) return fail(MKACC_E_ARG, "null argument");
+    std::lock_guard<std::mutex> g(c->mu);
+    if (c->wide) return wide_prim(c, in, out, count, which);
+    const size_t w = count * kN, out_mul = which == 2 ? c->dg : 1;
+    std::vector<uint32_t> i32(w), o32(w * out_mul);
+    for (size_t s = 0; s < w; ++s) {
+        if (in[s] >= c->p.Q) return fail(MKACC_E_RANGE, "input word not a canonical residue mod Q");
+        i32[s] = (uint32_t)in[s];
+    }
+    const int rc = prim_launch(c, i32.data(), o32.data(), count, out_mul, which);
+    if (rc) return rc;
+    for (size_t s = 0; s < o32.size(); ++s) out[s] = o32[s];
+    return MKACC_OK;
+}
+}  // namespace
+
+int mkacc_ntt_forward_u64(mkacc_ctx* c, const uint64_t* in, uint64_t* out, size_t count) {
+    return prim_u64(c, in, out, count, 0);
+}
+int mkacc_ntt_inverse_u64(mkacc_ctx* c, const uint64_t* in, uint64_t* out, size_t count) {
+    return prim_u64(c, in, out, count, 1);
+}
+int mkacc_sdd_u64(mkacc_ctx* c, const uint64_t* in, uint64_t* out, size_t count) {
+    return prim_u64(c, in, out, count, 2);
 }
 
 }  // extern "C"

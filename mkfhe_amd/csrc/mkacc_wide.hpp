@@ -1,0 +1,278 @@
+// mkacc_wide.hpp -- the 64-bit-word accumulator path: EvalAcc for a ring
+// modulus 2^27 <= Q < 2^62 (the reference at NATIVE_SIZE=64, where
+// MAX_MODULUS_SIZE is 60; SURVEY.md s8 config 5 stress: Q = 1125899906826241,
+// B_g = 2^10).  Included by mkacc_engine.hip.
+//
+// A residue no longer fits a 32-bit lane word, so the register-resident
+// one-wave-per-gate design of the 27-bit kernel (mkacc_device.hpp) does not
+// carry over: here one 256-thread workgroup owns one gate, each thread holds
+// 8 EVAL slots (j = t + 256 e, coalesced key/accumulator streams), and every
+// transform runs in a 16 KiB LDS tile (radix-2 stages, one barrier each).
+// Products are 64 x 64 -> 128-bit: Shoup with precomputed companions for the
+// fixed operands (twiddles, monomial powers psi^e, N^-1) and Barrett
+// (HAC 14.42) for the data x key products.  Every result is a canonical
+// residue, so the same reorderings as the 27-bit kernel are bit-exact.
+#pragma once
+
+namespace {
+
+namespace wide {
+
+constexpr int kThreads = 256;
+constexpr int kPer = kN / kThreads;   // 8 slots per thread
+
+struct Mod64 {
+    uint64_t Q;
+    uint64_t mu;    // floor(2^(2L) / Q)
+    uint32_t L;     // 2^(L-1) <= Q < 2^L
+};
+
+__device__ __forceinline__ uint64_t add(uint64_t a, uint64_t b, uint64_t Q) {
+    const uint64_t s = a + b;
+    return s >= Q ? s - Q : s;
+}
+__device__ __forceinline__ uint64_t sub(uint64_t a, uint64_t b, uint64_t Q) {
+    return a >= b ? a - b : a + Q - b;
+}
+// x * w mod Q, wp = floor(w 2^64 / Q) (Shoup; any 64-bit x)
+__device__ __forceinline__ uint64_t mul_shoup(uint64_t x, uint64_t w, uint64_t wp, uint64_t Q) {
+    const uint64_t q = __umul64hi(x, wp);
+    const uint64_t r = x * w - q * Q;   // [0, 2Q)
+    return r >= Q ? r - Q : r;
+}
+// a * b mod Q for a, b < Q (Barrett, HAC 14.42 with base 2)
+__device__ __forceinline__ uint64_t mulmod(uint64_t a, uint64_t b, const Mod64& m) {
+    const unsigned __int128 x = (unsigned __int128)a * b;
+    const uint64_t q1 = (uint64_t)(x >> (m.L - 1));
+    const uint64_t q2 = (uint64_t)(((unsigned __int128)q1 * m.mu) >> (m.L + 1));
+    uint64_t r = (uint64_t)x - q2 * m.Q;   // [0, 3Q)
+    r = r >= m.Q ? r - m.Q : r;
+    return r >= m.Q ? r - m.Q : r;
+}
+
+struct Sdd64 {
+    uint64_t qhalf;   // Q >> 1
+    uint64_t cpos;    // C = sum_{i < digitsG} 2^(b-1) 2^(b i)
+    uint64_t cneg;    // C - Q (mod 2^64)
+    uint64_t half;    // 2^(b-1)
+    uint32_t gbits;   // b
+};
+// offset word D = centred(t) + C; balanced digit i = bfe(D, b i, b) - 2^(b-1)
+// (closed form of mk-acc.cpp:54-80, proof in mkacc_device.hpp; b * digitsG <= 63)
+__device__ __forceinline__ uint64_t sdd_offset(uint64_t t, const Sdd64& s) {
+    return t + (t < s.qhalf ? s.cpos : s.cneg);
+}
+// digit i (1..dg) as the reference emits it: r < 0 ? r + Q : r
+__device__ __forceinline__ uint64_t sdd_digit(uint64_t D, uint32_t i, const Sdd64& s, uint64_t Q) {
+    const uint64_t f = (D >> (s.gbits * i)) & ((s.half << 1) - 1);
+    return f >= s.half ? f - s.half : f + Q - s.half;
+}
+
+// NTT of the LDS tile a[N], reference order (transformnat-impl.h:300-354):
+// stage m: butterfly (j, j+t) with table[m + i], t = N / 2m.  tw = {w, w'}.
+__device__ __forceinline__ void ntt_fwd(uint64_t* a, const ulonglong2* __restrict__ tw, uint64_t Q) {
+    uint32_t logt = kLogN - 1;
+    for (uint32_t m = 1; m < (uint32_t)kN; m <<= 1, --logt) {
+        const uint32_t t = 1u << logt;
+#pragma unroll
+        for (int r = 0; r < kN / 2 / kThreads; ++r) {
+            const uint32_t b = threadIdx.x + r * kThreads;
+            const uint32_t i = b >> logt, j = (i << (logt + 1)) + (b & (t - 1));
+            const ulonglong2 w = tw[m + i];
+            const uint64_t U = a[j], V = mul_shoup(a[j + t], w.x, w.y, Q);
+            a[j] = add(U, V, Q);
+            a[j + t] = sub(U, V, Q);
+        }
+        __syncthreads();
+    }
+}
+// Inverse GS without the N^-1 factor (transformnat-impl.h:492-552 up to the scaling)
+__device__ __forceinline__ void ntt_inv_noscale(uint64_t* a, const ulonglong2* __restrict__ tw, uint64_t Q) {
+    uint32_t logt = 0;
+    for (uint32_t m = kN >> 1; m >= 1; m >>= 1, ++logt) {
+        const uint32_t t = 1u << logt;
+#pragma unroll
+        for (int r = 0; r < kN / 2 / kThreads; ++r) {
+            const uint32_t b = threadIdx.x + r * kThreads;
+            const uint32_t i = b >> logt, j = (i << (logt + 1)) + (b & (t - 1));
+            const ulonglong2 w = tw[m + i];
+            const uint64_t U = a[j], V = a[j + t];
+            a[j] = add(U, V, Q);
+            a[j + t] = mul_shoup(sub(U, V, Q), w.x, w.y, Q);
+        }
+        __syncthreads();
+    }
+}
+
+struct StepArgs {
+    const uint64_t* acc_in;    // [B][k][N] EVAL (reference order)
+    uint64_t* acc_out;
+    const uint32_t* cvals;     // [B] exponents c of this step, in [0, 2N)
+    const uint64_t* key1;      // ev1 = (*ek)[u][0][i] : [dg][2][N]
+    const uint64_t* key2;      // ev2 = (*ek)[u][1][i] (XZW)
+    const uint64_t* keys;      // evs = (*ek)[0][0][n]
+    const uint64_t* pkey;      // [k][dg][N]
+    const ulonglong2* twf;     // forward table {w, w'}
+    const ulonglong2* twi;     // inverse table
+    const ulonglong2* psi;     // psi^e, e in [0, 2N), with companions
+    uint32_t k, index, dg;
+    uint64_t ninv, ninvp;
+    Mod64 m;
+    Sdd64 sd;
+};
+
+// X^e at EVAL slot j: psi^(e (2 brv(j) + 1) mod 2N)  (transformnat-impl.h:705-760)
+__device__ __forceinline__ ulonglong2 mono(const ulonglong2* psi, uint32_t e, uint32_t oj) {
+    return psi[(e * oj) & (2u * kN - 1u)];
+}
+
+// d_i / f_i of AddToAccXZW{0,} for one slot (xzw.cpp:322-325, 375-378; xzw_B.cpp:311-314, 368-371)
+template <int METHOD, bool FIRST>
+__device__ __forceinline__ uint64_t key_eff(uint64_t k1, uint64_t k2, uint64_t ks, ulonglong2 tp, ulonglong2 tn,
+                                            uint64_t Q) {
+    if (METHOD == XZW) {
+        if (FIRST) {
+            const uint64_t t1 = sub(mul_shoup(k1, tp.x, tp.y, Q), k1, Q);
+            const uint64_t t2 = sub(mul_shoup(k2, tn.x, tn.y, Q), k2, Q);
+            return add(add(ks, t1, Q), t2, Q);
+        }
+        return sub(k1, mul_shoup(k2, tn.x, tn.y, Q), Q);   // ev1 - ev2 X^-c
+    }
+    if (FIRST) return add(ks, sub(mul_shoup(k1, tp.x, tp.y, Q), k1, Q), Q);
+    return k1;
+}
+
+// One accumulator step of one gate per workgroup (same algebra as mk_step_kernel):
+//   FIRST: acc <- HbProd(acc);  else acc <- acc + HbProd(acc (X^c - 1))
+template <int METHOD, bool FIRST>
+__global__ __launch_bounds__(kThreads) void step_kernel(StepArgs a) {
+    __shared__ uint64_t tile[kN];
+    const uint32_t gate = blockIdx.x, t = threadIdx.x;
+    const uint64_t Q = a.m.Q;
+    const uint32_t c = a.cvals[gate], cneg = (2u * kN - c) & (2u * kN - 1u);
+    const uint32_t k = a.k, index = a.index, dg = a.dg;
+    uint32_t oj[kPer];
+#pragma unroll
+    for (int e = 0; e < kPer; ++e) oj[e] = 2u * (__brev(t + kThreads * e) >> (32 - kLogN)) + 1u;
+    const size_t key_f = (size_t)kN;   // f_i follows d_i inside [dg][2][N]
+    uint64_t sv[kPer], keep[kPer];
+#pragma unroll
+    for (int e = 0; e < kPer; ++e) sv[e] = 0;
+
+    for (uint32_t tt = 1; tt <= k; ++tt) {
+        const uint32_t u = index + tt < k ? index + tt : index + tt - k;
+        const uint64_t* accu = a.acc_in + ((size_t)gate * k + u) * kN;
+        uint64_t a0[kPer], D[kPer], uj[kPer];
+#pragma unroll
+        for (int e = 0; e < kPer; ++e) {
+            const uint32_t j = t + kThreads * e;
+            a0[e] = accu[j];
+            uint64_t x = a0[e];
+            if (!FIRST) {   // acctemp = acc * (X^c - 1)   (xzw.cpp:336-338)
+                const ulonglong2 w = mono(a.psi, c, oj[e]);
+                x = sub(mul_shoup(x, w.x, w.y, Q), x, Q);
+            }
+            tile[j] = x;
+            uj[e] = FIRST ? 0 : a0[e];
+        }
+        __syncthreads();
+        ntt_inv_noscale(tile, a.twi, Q);
+#pragma unroll
+        for (int e = 0; e < kPer; ++e)
+            D[e] = sdd_offset(mul_shoup(tile[t + kThreads * e], a.ninv, a.ninvp, Q), a.sd);
+        for (uint32_t i = 0; i < dg; ++i) {
+            __syncthreads();
+#pragma unroll
+            for (int e = 0; e < kPer; ++e) tile[t + kThreads * e] = sdd_digit(D[e], i + 1, a.sd, Q);
+            __syncthreads();
+            ntt_fwd(tile, a.twf, Q);
+            const size_t ko = (size_t)i * 2 * kN;
+            const uint64_t* P = a.pkey + ((size_t)u * dg + i) * kN;
+#pragma unroll
+            for (int e = 0; e < kPer; ++e) {
+                const uint32_t j = t + kThreads * e;
+                const uint64_t g = tile[j];
+                const ulonglong2 tp = FIRST ? mono(a.psi, c, oj[e]) : ulonglong2{0, 0};
+                const ulonglong2 tn = METHOD == XZW ? mono(a.psi, cneg, oj[e]) : ulonglong2{0, 0};
+                const uint64_t d = key_eff<METHOD, FIRST>(a.key1[ko + j], METHOD == XZW ? a.key2[ko + j] : 0,
+                                                          FIRST ? a.keys[ko + j] : 0, tp, tn, Q);
+                uj[e] = add(uj[e], mulmod(g, d, a.m), Q);                 // <g^-1(c), d_i>
+                sv[e] = add(sv[e], mulmod(g, P[j], a.m), Q);              // <g^-1(c), P[u]_i>
+            }
+        }
+        if (tt < k) {
+            uint64_t* out = a.acc_out + ((size_t)gate * k + u) * kN;
+#pragma unroll
+            for (int e = 0; e < kPer; ++e) out[t + kThreads * e] = uj[e];
+        } else {
+#pragma unroll
+            for (int e = 0; e < kPer; ++e) keep[e] = uj[e];
+        }
+    }
+
+    // second half of HbProd: iNTT(sumV) -> SDD -> NTT -> acc[index] += <., f>  (xzw.cpp:272-289)
+    uint64_t D[kPer];
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < kPer; ++e) tile[t + kThreads * e] = sv[e];
+    __syncthreads();
+    ntt_inv_noscale(tile, a.twi, Q);
+#pragma unroll
+    for (int e = 0; e < kPer; ++e) D[e] = sdd_offset(mul_shoup(tile[t + kThreads * e], a.ninv, a.ninvp, Q), a.sd);
+    for (uint32_t i = 0; i < dg; ++i) {
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < kPer; ++e) tile[t + kThreads * e] = sdd_digit(D[e], i + 1, a.sd, Q);
+        __syncthreads();
+        ntt_fwd(tile, a.twf, Q);
+        const size_t ko = (size_t)i * 2 * kN + key_f;
+#pragma unroll
+        for (int e = 0; e < kPer; ++e) {
+            const uint32_t j = t + kThreads * e;
+            const ulonglong2 tp = FIRST ? mono(a.psi, c, oj[e]) : ulonglong2{0, 0};
+            const ulonglong2 tn = METHOD == XZW ? mono(a.psi, cneg, oj[e]) : ulonglong2{0, 0};
+            const uint64_t f = key_eff<METHOD, FIRST>(a.key1[ko + j], METHOD == XZW ? a.key2[ko + j] : 0,
+                                                      FIRST ? a.keys[ko + j] : 0, tp, tn, Q);
+            keep[e] = add(keep[e], mulmod(tile[j], f, a.m), Q);
+        }
+    }
+    uint64_t* out = a.acc_out + ((size_t)gate * k + index) * kN;
+#pragma unroll
+    for (int e = 0; e < kPer; ++e) out[t + kThreads * e] = keep[e];
+}
+
+// primitive kernels for parity tests: one polynomial per workgroup
+__global__ __launch_bounds__(kThreads) void ntt_fwd_kernel(const uint64_t* __restrict__ in, uint64_t* __restrict__ out,
+                                                            const ulonglong2* __restrict__ tw, uint64_t Q) {
+    __shared__ uint64_t tile[kN];
+    const size_t base = (size_t)blockIdx.x * kN;
+    for (int e = 0; e < kPer; ++e) tile[threadIdx.x + kThreads * e] = in[base + threadIdx.x + kThreads * e];
+    __syncthreads();
+    ntt_fwd(tile, tw, Q);
+    for (int e = 0; e < kPer; ++e) out[base + threadIdx.x + kThreads * e] = tile[threadIdx.x + kThreads * e];
+}
+__global__ __launch_bounds__(kThreads) void ntt_inv_kernel(const uint64_t* __restrict__ in, uint64_t* __restrict__ out,
+                                                            const ulonglong2* __restrict__ tw, uint64_t Q,
+                                                            uint64_t ninv, uint64_t ninvp) {
+    __shared__ uint64_t tile[kN];
+    const size_t base = (size_t)blockIdx.x * kN;
+    for (int e = 0; e < kPer; ++e) tile[threadIdx.x + kThreads * e] = in[base + threadIdx.x + kThreads * e];
+    __syncthreads();
+    ntt_inv_noscale(tile, tw, Q);
+    for (int e = 0; e < kPer; ++e) {
+        const uint32_t j = threadIdx.x + kThreads * e;
+        out[base + j] = mul_shoup(tile[j], ninv, ninvp, Q);
+    }
+}
+__global__ void sdd_kernel(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, uint32_t count, uint32_t dg,
+                           Sdd64 sd, uint64_t Q) {
+    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (size_t)count * kN) return;
+    const size_t p = idx / kN, j = idx % kN;
+    const uint64_t D = sdd_offset(in[idx], sd);
+    for (uint32_t i = 0; i < dg; ++i) out[(p * dg + i) * kN + j] = sdd_digit(D, i + 1, sd, Q);
+}
+
+}  // namespace wide
+
+}  // namespace

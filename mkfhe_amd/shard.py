@@ -20,26 +20,33 @@ def shard_range(total: int, rank: int, world: int) -> tuple[int, int]:
     return start, start + q + (1 if rank < r else 0)
 
 
+def word_dtype(Q: int):
+    """Storage word of residues mod Q: uint32 up to 2^32, else uint64 (NATIVE_SIZE=64)."""
+    return np.uint32 if Q <= (1 << 32) else np.uint64
+
+
 def uniform_residues(nwords: int, Q: int, seed: int) -> np.ndarray:
-    """Synthetic key material: uniform residues mod Q (uint32)."""
-    return np.random.Generator(np.random.PCG64(seed)).integers(0, Q, size=nwords, dtype=np.uint32)
+    """Synthetic key material: uniform residues mod Q (uint32, or uint64 for Q > 2^32)."""
+    return np.random.Generator(np.random.PCG64(seed)).integers(0, Q, size=nwords, dtype=word_dtype(Q))
 
 
 def broadcast_keys(nwords: int, Q: int, seed: int, device: str = "cpu"):
     """Rank 0 draws `nwords` key words and broadcasts them once to every rank.
 
-    Returns a torch int32 tensor (bit pattern of the uint32 words) on `device`.
-    Single-process runs skip the collective.
+    Returns a torch int32 (int64 for Q > 2^32) tensor holding the bit pattern
+    of the words on `device`.  Single-process runs skip the collective.
     """
     import torch
     import torch.distributed as dist
 
     multi = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
     rank = dist.get_rank() if multi else 0
+    wide = word_dtype(Q) == np.uint64
     if rank == 0:
-        t = torch.from_numpy(uniform_residues(nwords, Q, seed).view(np.int32)).to(device)
+        w = uniform_residues(nwords, Q, seed)
+        t = torch.from_numpy(w.view(np.int64 if wide else np.int32)).to(device)
     else:
-        t = torch.empty(nwords, dtype=torch.int32, device=device)
+        t = torch.empty(nwords, dtype=torch.int64 if wide else torch.int32, device=device)
     if multi:
         dist.broadcast(t, src=0)
     return t
@@ -50,8 +57,9 @@ def mntru_test_vector(eng) -> np.ndarray:
     acc[0] = NTT(Rx) with Rx[j] = Q - (Q/8 + 1) for j < N/2 else Q/8 + 1; acc[u>0] = 0."""
     Q, N = eng.Q, eng.N
     q2p = Q // 8 + 1
-    rx = np.where(np.arange(N) < N // 2, Q - q2p, q2p).astype(np.uint32)
-    acc = np.zeros((eng.k, N), dtype=np.uint32)
+    dt = word_dtype(Q)
+    rx = np.where(np.arange(N) < N // 2, Q - q2p, q2p).astype(dt)
+    acc = np.zeros((eng.k, N), dtype=dt)
     acc[0] = eng.ntt_forward(rx[None])[0]
     return acc
 

@@ -1,0 +1,96 @@
+"""The 64-bit word path (mkfhe_amd/csrc/mkacc_wide.hpp): EvalAcc for
+2^27 <= Q < 2^62, i.e. the reference at NATIVE_SIZE=64 with a wide modulus
+(SURVEY.md s8 config 5 stress: Q = 1125899906826241, B_g = 2^10, dg = 4).
+Bit-exact against the CPU oracle, whose 64-bit arithmetic is u128-exact.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import Q_MK, make_case
+
+N = 2048
+Q50 = 1125899906826241          # SURVEY.md s0 item 2 / s6 ("cfg5 stress")
+PSI50 = 1080667890455           # its minimal primitive 4096-th root, printed by the reference probe
+
+
+def test_oracle_wide_constants(oracle):
+    """Pins the oracle's number theory at 50 bits on the reference's own output."""
+    assert oracle.is_prime(Q50) and (Q50 - 1) % (2 * N) == 0 and Q50 < (1 << 50)
+    assert oracle.root_of_unity(2 * N, Q50) == PSI50
+    assert oracle.digits_g(Q50, 1 << 10) == 5
+
+
+def test_oracle_wide_ntt_roundtrip(oracle):
+    a = oracle.fill_uniform(N, Q50, 9)
+    e = oracle.ntt_forward(a, Q50, PSI50)
+    assert np.array_equal(oracle.ntt_inverse(e, Q50, PSI50), a)
+    # negacyclic product of X and X^(N-1) is -1
+    x = np.zeros(N, np.uint64); x[1] = 1
+    y = np.zeros(N, np.uint64); y[N - 1] = 1
+    prod = (oracle.ntt_forward(x, Q50, PSI50).astype(object) * oracle.ntt_forward(y, Q50, PSI50).astype(object)) % Q50
+    z = oracle.ntt_inverse(np.array(prod, dtype=np.uint64), Q50, PSI50)
+    assert z[0] == Q50 - 1 and not z[1:].any()
+
+
+def _eng(mk, method, k, n, Q, q, baseG):
+    return mk.MKAccumulatorEngine(mk.make_params(method, k, n, N, Q, q, baseG))
+
+
+@pytest.mark.gpu
+def test_wide_context_and_primitives(mk_gpu, oracle):
+    mk = mk_gpu
+    eng = _eng(mk, mk.MKNTRU, 2, 4, Q50, 45181, 1 << 10)
+    assert eng.wide and eng.dg == 4 and eng.params.root == PSI50
+    a = oracle.fill_uniform(3 * N, Q50, 21).reshape(3, N)
+    f = eng.ntt_forward(a)
+    assert f.dtype == np.uint64
+    assert np.array_equal(f, np.stack([oracle.ntt_forward(x, Q50, PSI50) for x in a]))
+    assert np.array_equal(eng.ntt_inverse(f), a)
+    d = eng.sdd(a)
+    assert np.array_equal(d, np.stack([oracle.sdd(x, Q50, 1 << 10, 4) for x in a]))
+    # the gate API is the 27-bit kernel's
+    with pytest.raises(mk.MkaccError) as e:
+        eng.upload_ksk_mntru(np.zeros((2, N * 4, 4), np.uint32), 45181, 32, 4)
+    assert e.value.code == -2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method,k,n,baseG,B", [
+    ("XZW", 2, 5, 1 << 10, 3),     # config 5 stress shape (dg = 4)
+    ("XZW", 3, 3, 1 << 17, 2),     # dg = 2, three parties
+    ("XZW_B", 2, 4, 1 << 10, 3),
+    ("XZW_B", 1, 4, 1 << 13, 2),   # dg = 3, one party
+])
+def test_wide_evalacc_bitexact(mk_gpu, oracle, method, k, n, baseG, B):
+    mk = mk_gpu
+    m = oracle.XZW if method == "XZW" else oracle.XZW_B
+    orc, evk, pkey, ct, acc = make_case(oracle, m, k, n, 45181, baseG, B, seed=k * 7 + n, Q=Q50)
+    exp = orc.evalacc(evk, pkey, ct, acc)
+    eng = _eng(mk, mk.MKNTRU if method == "XZW" else mk.MKNTRU_LWE, k, n, Q50, 45181, baseG)
+    assert eng.wide
+    eng.upload_keys(evk.astype(np.uint64), pkey.astype(np.uint64))
+    got = eng.eval_batch(ct.astype(np.uint32), acc.astype(np.uint64))
+    assert got.dtype == np.uint64
+    assert np.array_equal(got, exp), int(np.count_nonzero(got != exp))
+
+
+@pytest.mark.gpu
+def test_wide_path_matches_fast_path_at_27_bits(mk_gpu, oracle):
+    """MKACC_ENGINE=wide forces the 64-bit path on a 27-bit Q: both engines agree bit for bit."""
+    mk = mk_gpu
+    orc, evk, pkey, ct, acc = make_case(oracle, oracle.XZW, 2, 6, 45181, 1 << 7, 5, seed=44)
+    fast = _eng(mk, mk.MKNTRU, 2, 6, Q_MK, 45181, 1 << 7)
+    fast.upload_keys(evk.astype(np.uint32), pkey.astype(np.uint32))
+    want = fast.eval_batch(ct.astype(np.uint32), acc.astype(np.uint32))
+    os.environ["MKACC_ENGINE"] = "wide"
+    try:
+        wide = _eng(mk, mk.MKNTRU, 2, 6, Q_MK, 45181, 1 << 7)
+    finally:
+        del os.environ["MKACC_ENGINE"]
+    assert wide.wide and not fast.wide
+    wide.upload_keys(evk.astype(np.uint32), pkey.astype(np.uint32))
+    got = wide.eval_batch(ct.astype(np.uint32), acc.astype(np.uint32))
+    assert np.array_equal(got, want)
+    assert np.array_equal(got.astype(np.uint64), orc.evalacc(evk, pkey, ct, acc))
