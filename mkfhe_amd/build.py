@@ -60,10 +60,12 @@ def build(force: bool = False, verbose: bool = False) -> str:
     cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-fvisibility-inlines-hidden", "-Wl,-Bsymbolic",
            "-Wno-unused-result", "-Wno-pass-failed", "-I", os.path.join(ROOT, "include"),
-           "-o", OUT + ".tmp"] + SOURCES
+           "-Rpass-analysis=kernel-resource-usage", "-o", OUT + ".tmp"] + SOURCES
     if verbose:
         print(" ".join(cmd))
-    subprocess.check_call(cmd)
+    # per-kernel VGPR / spill / occupancy report next to the library
+    with open(os.path.join(os.path.dirname(OUT), "resource_usage.txt"), "w") as rep:
+        subprocess.check_call(cmd, stderr=rep)
     os.replace(OUT + ".tmp", OUT)
     return OUT
 

@@ -393,8 +393,10 @@ __device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_
 // mod Q, so the reordering (parties in the order index+1, ..., index) is
 // bit-exact.
 template <int DG, int METHOD, bool FIRST>
+__device__ __forceinline__ void step_body(const StepCtx& s, uint32_t k, uint32_t index);
+
+template <int DG, int METHOD, bool FIRST>
 __global__ __launch_bounds__(kThreads, 2) void mk_step_kernel(StepArgs a) {
-    constexpr int kDigitUnroll = DG == 2 ? 2 : 1;
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     load_image(smem, a.img);
     const uint32_t l = threadIdx.x & 63u;
@@ -403,10 +405,9 @@ __global__ __launch_bounds__(kThreads, 2) void mk_step_kernel(StepArgs a) {
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t gate = blockIdx.x * kWavesPerBlock + wv;
     if (gate >= a.B) return;
-    const uint32_t Q = a.m.Q;
     const uint32_t c = __builtin_amdgcn_readfirstlane(a.cvals[gate]);
     const uint32_t cneg = (2u * kN - c) & (2u * kN - 1u);
-    const uint32_t k = a.k, index = a.index;
+    const uint32_t k = a.k;
     const uint32_t polyB = kN * 4u;
     const StepCtx s{tables(smem, a.img),
                     smem + kLdsTabWords + wv * kLdsWords,
@@ -425,7 +426,17 @@ __global__ __launch_bounds__(kThreads, 2) void mk_step_kernel(StepArgs a) {
                     make_rsrc(a.keys, DG * 2 * polyB),
                     make_rsrc(a.pkey, k * DG * polyB),
                     make_rsrc(a.deff + (size_t)gate * DG * kN, DG * polyB)};
+    step_body<DG, METHOD, FIRST>(s, k, a.index);
+}
 
+template <int DG, int METHOD, bool FIRST>
+__device__ __forceinline__ void step_body(const StepCtx& s, uint32_t k, uint32_t index) {
+    // no digit unrolling: at DG = 2 unrolling the f-part loop spilled ~250 VGPRs
+    // (-Rpass-analysis=kernel-resource-usage, mkfhe_amd/lib/resource_usage.txt)
+    constexpr int kDigitUnroll = 1;
+    const uint32_t Q = s.m.Q;
+    const uint32_t l = s.l;
+    const uint32_t polyB = kN * 4u;
     uint64_t sv[kRegs];
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) sv[r] = 0;

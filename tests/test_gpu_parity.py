@@ -75,6 +75,9 @@ CASES = [
     ("XZW_B", 2, 3, 32749, 1 << 7, 2),    # dg=3
     ("XZW", 1, 6, 45181, 1 << 9, 2),      # single party
     ("XZW", 5, 2, 45181, 1 << 9, 5),      # odd party count, odd batch
+    ("XZW", 16, 2, 45181, 1 << 5, 2),     # STD128_MKNTRU_4 shape: 16 parties, dg=5
+    ("XZW_B", 16, 2, 32749, 1 << 7, 3),   # STD128_MKNTRU_LWE_4 shape: 16 parties, dg=3
+    ("XZW", 8, 3, 45181, 1 << 6, 2),      # STD128_MKNTRU_3 shape (config 4): 8 parties, dg=4
 ]
 
 
