@@ -1,0 +1,149 @@
+#!/usr/bin/env python3
+"""Generate tests/golden/*.json (committed fixtures; run here, never on the GPU box).
+
+  python tests/golden/make_golden.py
+
+reference_kats.json
+    Known-answer vectors held by the reference's own unit tests for the
+    primitives on this path, copied as data with their file:line (the
+    reference has no MK/accumulator test), plus the MK ring
+    constants the reference probe printed.
+evalacc_full.json
+    Full-size EvalAcc fixtures: for each BASELINE configuration shape, seeded
+    synthetic keys / ciphertexts (oracle fill_uniform, SplitMix64) and the
+    MNTRU test-vector accumulator, run through the CPU oracle; stored as the
+    SHA-256 of the little-endian uint64 output plus sample coefficients.
+    The GPU tests regenerate the inputs from the seeds and compare digests.
+gates_realkeys.json
+    NAND gates with real keys (seeded NTL-free key generation,
+    mkfhe_amd/keys.py), evaluated by the oracle: digest of the output
+    ciphertexts and their decryptions.
+"""
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+import pyoracle  # noqa: E402
+
+N = 2048
+Q_MK = 134176769
+Q50 = 1125899906826241
+
+REFERENCE_KATS = {
+    "first_prime": [
+        {"bits": 30, "m": 2048, "q": 1073750017, "src": "src/core/unittest/UnitTestNbTheory.cpp:170-175"},
+        {"bits": 49, "m": 4096, "q": 562949953548289, "src": "src/core/unittest/UnitTestNbTheory.cpp:178-185"},
+    ],
+    "switch_format_forward": {"q": 73, "root": 22, "in": [2, 1, 3, 2], "out": [69, 65, 44, 49],
+                              "src": "src/core/unittest/UnitTestPolyElements.cpp:388-399"},
+    "switch_format_inverse": {"q": 73, "root": 22, "in": [2, 3, 1, 2], "out": [2, 3, 50, 3],
+                              "src": "src/core/unittest/UnitTestPolyElements.cpp:401-411"},
+    "transpose": {"q": 73, "root": 22, "in": [31, 21, 15, 34], "out": [31, 39, 58, 52],
+                  "src": "src/core/unittest/UnitTestPolyElements.cpp:540-571"},
+    "automorphism": {"q": 73, "k": 3, "in": [56, 1, 37, 2], "out": [56, 2, 36, 1],
+                     "src": "src/core/unittest/UnitTestPolyElements.cpp:512-521"},
+    "crt_mult": {"q": 113, "m": 8, "a": [1, 2, 4, 1], "out": [94, 109, 11, 18],
+                 "src": "src/core/unittest/UnitTestTransform.cpp:58-93"},
+    "mk_ring": {"Q": Q_MK, "psi": 100530, "src": "binfhecontext.cpp:157-158 + reference probe, SURVEY.md s0"},
+    "cfg5_ring": {"Q": Q50, "psi": 1080667890455, "src": "reference probe at NATIVE_SIZE=64, SURVEY.md s0 item 2"},
+}
+
+# name, method, k, n, q, baseG, Q, B  (the BASELINE.json configuration shapes)
+EVALACC_CASES = [
+    ("STD100_MKNTRU", pyoracle.XZW, 2, 560, 45181, 1 << 9, Q_MK, 2),
+    ("STD128_MKNTRU", pyoracle.XZW, 2, 765, 45181, 1 << 7, Q_MK, 2),
+    ("STD100_MKNTRU_LWE", pyoracle.XZW_B, 2, 500, 32749, 1 << 9, Q_MK, 2),
+    ("STD100_MKNTRU_LWE_2", pyoracle.XZW_B, 4, 500, 32749, 1 << 9, Q_MK, 2),
+    ("STD128_MKNTRU_3", pyoracle.XZW, 8, 765, 45181, 1 << 6, Q_MK, 1),
+    ("CFG5_Q50_STD100_SHAPE", pyoracle.XZW, 2, 560, 45181, 1 << 10, Q50, 2),
+]
+
+
+def digest(a) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a, dtype="<u8").tobytes()).hexdigest()
+
+
+def evalacc_inputs(method, k, n, q, baseG, Q, B, seed):
+    """Seeded inputs, identical to what tests/test_golden.py rebuilds."""
+    orc = pyoracle.Oracle(method, k, n, N, Q, q, baseG)
+    evk = pyoracle.fill_uniform(int(np.prod(orc.evk_shape)), Q, seed + 1).reshape(orc.evk_shape)
+    pkey = pyoracle.fill_uniform(int(np.prod(orc.pkey_shape)), Q, seed + 2).reshape(orc.pkey_shape)
+    bound = q if method == pyoracle.XZW else 2 * N
+    ct = pyoracle.fill_uniform(B * k * n, bound, seed + 3).reshape(B, k, n)
+    acc = np.broadcast_to(orc.mntru_testvector(4), (B, k, N)).copy()
+    return orc, evk, pkey, ct, acc
+
+
+def make_evalacc():
+    out = []
+    for i, (name, method, k, n, q, baseG, Q, B) in enumerate(EVALACC_CASES):
+        seed = 7000 + 100 * i
+        orc, evk, pkey, ct, acc = evalacc_inputs(method, k, n, q, baseG, Q, B, seed)
+        res = orc.evalacc_batch(evk, pkey, ct, acc, min(8, os.cpu_count() or 1))
+        out.append({"name": name, "method": "XZW" if method == pyoracle.XZW else "XZW_B", "k": k, "n": n,
+                    "q": q, "baseG": baseG, "Q": Q, "B": B, "seed": seed, "sha256": digest(res),
+                    "sample": [int(x) for x in res[0, 0, :8]] + [int(x) for x in res[-1, -1, -8:]]})
+        print(name, out[-1]["sha256"][:16], flush=True)
+    return out
+
+
+def make_gates():
+    from mkfhe_amd import keys as K
+    out = []
+    m1 = np.array([0, 0, 1, 1]); m2 = np.array([0, 1, 0, 1])
+    for ps, method in (("STD128_MKNTRU", 0), ("STD100_MKNTRU_LWE", 2)):
+        p = K.paramset(ps, method)
+        k, n, _, dg, nk, dks = K.dims(p)
+        seed = 9100 if method == 0 else 9200
+        if method == 0:
+            sk = K.mntru_keygen(p, seed)
+            bk = K.bt_keygen(p, sk, seed=seed + 1)
+            ctn = K.mntru_ctgate(p, sk, seed + 2)
+            c1, c2 = K.mntru_encrypt(p, sk, m1, seed=seed + 3), K.mntru_encrypt(p, sk, m2, seed=seed + 4)
+            orc = pyoracle.Oracle(pyoracle.XZW, k, n, N, p.acc.Q, p.acc.q, p.acc.baseG)
+            heads = np.stack([pyoracle.mntru_head(ctn, c1[i], c2[i], p.acc.q) for i in range(4)])
+            acc0 = np.broadcast_to(orc.mntru_testvector(4), (4, k, N)).copy()
+            acc = orc.evalacc_batch(bk.evk, bk.pkey, heads, acc0, 4)
+            res = np.stack([orc.mntru_tail_ksk1(acc[i], bk.ksk, p.ks.qKS, p.ks.baseKS, n) for i in range(4)])
+            dec = K.mntru_decrypt(p, sk, res.astype(np.uint32), mod=p.ks.qKS)
+            inputs = {"ct_nand": digest(ctn), "ct1": digest(c1), "ct2": digest(c2)}
+        else:
+            sk = K.mklwe_keygen(p, seed)
+            bk = K.bt_keygen(p, sk, seed=seed + 1)
+            a1, b1 = K.mklwe_encrypt(p, sk, m1, seed=seed + 3)
+            a2, b2 = K.mklwe_encrypt(p, sk, m2, seed=seed + 4)
+            orc = pyoracle.Oracle(pyoracle.XZW_B, k, n, N, p.acc.Q, 2 * N, p.acc.baseG)
+            cs, accs = zip(*[orc.mklwe_head(a1[i], b1[i], a2[i], b2[i], p.acc.q) for i in range(4)])
+            acc = orc.evalacc_batch(bk.evk, bk.pkey, np.stack(cs), np.stack(accs), 4)
+            A, Bk = bk.ksk_A.astype(np.uint64), bk.ksk_B.astype(np.uint64)
+            outs = [orc.mklwe_tail(acc[i], A, Bk, p.ks.qKS, p.ks.baseKS, n) for i in range(4)]
+            res = np.concatenate([np.stack([o[0] for o in outs]).reshape(4, -1),
+                                  np.array([[o[1]] for o in outs], dtype=np.uint64)], axis=1)
+            dec = K.mklwe_decrypt(p, sk, np.stack([o[0] for o in outs]).astype(np.uint32),
+                                  np.array([o[1] for o in outs], dtype=np.uint32), mod=p.ks.qKS)
+            inputs = {"a1": digest(a1), "b1": digest(b1), "a2": digest(a2), "b2": digest(b2)}
+        assert np.array_equal(dec, 1 - (m1 & m2)), (ps, dec)
+        out.append({"paramset": ps, "method": method, "seed": seed, "m1": m1.tolist(), "m2": m2.tolist(),
+                    "keys": {"evk": digest(bk.evk), "pkey": digest(bk.pkey)}, "inputs": inputs,
+                    "sha256": digest(res), "decrypted": dec.tolist()})
+        print(ps, out[-1]["sha256"][:16], flush=True)
+    return out
+
+
+def main():
+    pyoracle.build()
+    json.dump(REFERENCE_KATS, open(os.path.join(HERE, "reference_kats.json"), "w"), indent=1)
+    json.dump(make_gates(), open(os.path.join(HERE, "gates_realkeys.json"), "w"), indent=1)
+    json.dump(make_evalacc(), open(os.path.join(HERE, "evalacc_full.json"), "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
