@@ -68,37 +68,79 @@ __device__ __forceinline__ uint64_t sdd_digit(uint64_t D, uint32_t i, const Sdd6
     return f >= s.half ? f - s.half : f + Q - s.half;
 }
 
+// CT / GS butterflies (canonical in, canonical out)
+__device__ __forceinline__ void ct(uint64_t& a, uint64_t& b, ulonglong2 w, uint64_t Q) {
+    const uint64_t U = a, V = mul_shoup(b, w.x, w.y, Q);
+    a = add(U, V, Q);
+    b = sub(U, V, Q);
+}
+__device__ __forceinline__ void gs(uint64_t& a, uint64_t& b, ulonglong2 w, uint64_t Q) {
+    const uint64_t U = a, V = b;
+    a = add(U, V, Q);
+    b = mul_shoup(sub(U, V, Q), w.x, w.y, Q);
+}
+
 // NTT of the LDS tile a[N], reference order (transformnat-impl.h:300-354):
 // stage m: butterfly (j, j+t) with table[m + i], t = N / 2m.  tw = {w, w'}.
+// Stages are taken two at a time (radix-4 groups j0 + {0, t/2, t, 3t/2}: one
+// barrier per pair), the last stage alone.
 __device__ __forceinline__ void ntt_fwd(uint64_t* a, const ulonglong2* __restrict__ tw, uint64_t Q) {
-    uint32_t logt = kLogN - 1;
-    for (uint32_t m = 1; m < (uint32_t)kN; m <<= 1, --logt) {
+    uint32_t m = 1, logt = kLogN - 1;                 // stage s: m = 2^s, t = 2^logt
+    for (; logt >= 2; m <<= 2, logt -= 2) {          // stages (s, s+1), t >= 4
+        const uint32_t h = 1u << (logt - 1);          // t / 2 = groups per block
+#pragma unroll
+        for (int r = 0; r < kN / 4 / kThreads; ++r) {
+            const uint32_t g = threadIdx.x + r * kThreads;
+            const uint32_t i = g >> (logt - 1), j0 = (i << (logt + 1)) + (g & (h - 1));
+            uint64_t x0 = a[j0], x1 = a[j0 + h], x2 = a[j0 + 2 * h], x3 = a[j0 + 3 * h];
+            const ulonglong2 w1 = tw[m + i];
+            ct(x0, x2, w1, Q);
+            ct(x1, x3, w1, Q);
+            ct(x0, x1, tw[2 * m + 2 * i], Q);
+            ct(x2, x3, tw[2 * m + 2 * i + 1], Q);
+            a[j0] = x0; a[j0 + h] = x1; a[j0 + 2 * h] = x2; a[j0 + 3 * h] = x3;
+        }
+        __syncthreads();
+    }
+    // remaining stages with t = 2 then t = 1 (N = 2^11: one pair above leaves t = 1 only)
+    for (; m < (uint32_t)kN; m <<= 1, --logt) {
         const uint32_t t = 1u << logt;
 #pragma unroll
         for (int r = 0; r < kN / 2 / kThreads; ++r) {
             const uint32_t b = threadIdx.x + r * kThreads;
             const uint32_t i = b >> logt, j = (i << (logt + 1)) + (b & (t - 1));
-            const ulonglong2 w = tw[m + i];
-            const uint64_t U = a[j], V = mul_shoup(a[j + t], w.x, w.y, Q);
-            a[j] = add(U, V, Q);
-            a[j + t] = sub(U, V, Q);
+            ct(a[j], a[j + t], tw[m + i], Q);
         }
         __syncthreads();
     }
 }
-// Inverse GS without the N^-1 factor (transformnat-impl.h:492-552 up to the scaling)
+// Inverse GS without the N^-1 factor (transformnat-impl.h:492-552 up to the
+// scaling): stage pairs (t, 2t) as radix-4 groups j0 + {0, t, 2t, 3t}.
 __device__ __forceinline__ void ntt_inv_noscale(uint64_t* a, const ulonglong2* __restrict__ tw, uint64_t Q) {
-    uint32_t logt = 0;
-    for (uint32_t m = kN >> 1; m >= 1; m >>= 1, ++logt) {
+    uint32_t m = kN >> 1, logt = 0;                   // stage: m blocks, t = 2^logt
+    for (; m >= 2; m >>= 2, logt += 2) {
+        const uint32_t t = 1u << logt;
+#pragma unroll
+        for (int r = 0; r < kN / 4 / kThreads; ++r) {
+            const uint32_t g = threadIdx.x + r * kThreads;
+            const uint32_t b = g >> logt, j0 = (b << (logt + 2)) + (g & (t - 1));
+            uint64_t x0 = a[j0], x1 = a[j0 + t], x2 = a[j0 + 2 * t], x3 = a[j0 + 3 * t];
+            gs(x0, x1, tw[m + 2 * b], Q);
+            gs(x2, x3, tw[m + 2 * b + 1], Q);
+            const ulonglong2 w2 = tw[(m >> 1) + b];
+            gs(x0, x2, w2, Q);
+            gs(x1, x3, w2, Q);
+            a[j0] = x0; a[j0 + t] = x1; a[j0 + 2 * t] = x2; a[j0 + 3 * t] = x3;
+        }
+        __syncthreads();
+    }
+    for (; m >= 1; m >>= 1, ++logt) {
         const uint32_t t = 1u << logt;
 #pragma unroll
         for (int r = 0; r < kN / 2 / kThreads; ++r) {
             const uint32_t b = threadIdx.x + r * kThreads;
             const uint32_t i = b >> logt, j = (i << (logt + 1)) + (b & (t - 1));
-            const ulonglong2 w = tw[m + i];
-            const uint64_t U = a[j], V = a[j + t];
-            a[j] = add(U, V, Q);
-            a[j + t] = mul_shoup(sub(U, V, Q), w.x, w.y, Q);
+            gs(a[j], a[j + t], tw[m + i], Q);
         }
         __syncthreads();
     }
