@@ -963,7 +963,9 @@ int wide_setup(mkacc_ctx* c) {
     using u128 = unsigned __int128;
     const uint64_t Q = c->p.Q;
     const uint32_t L = 64u - (uint32_t)__builtin_clzll(Q);
-    c->wm = wide::Mod64{Q, (uint64_t)(((u128)1 << (2 * L)) / Q), L};
+    uint64_t qi = Q;                       // Q^-1 mod 2^64 by Newton (Q odd)
+    for (int it = 0; it < 6; ++it) qi *= 2 - Q * qi;
+    c->wm = wide::Mod64{Q, (uint64_t)(((u128)1 << (2 * L)) / Q), L, 0 - qi};
     const uint32_t b = (uint32_t)__builtin_ctz(c->p.baseG);
     uint64_t C = 0;
     for (uint32_t i = 0; i < c->p.digitsG; ++i) C += (1ull << (b - 1)) << (b * i);
@@ -995,11 +997,14 @@ int wide_setup(mkacc_ctx* c) {
     return MKACC_OK;
 }
 
-// reference [k][nk][n+1][dg][2][N] -> device [k][n+1][nk][dg][2][N] (same EVAL order, no scaling)
+// reference [k][nk][n+1][dg][2][N] -> device [k][n+1][nk][dg][2][N] (same EVAL
+// order), every word in Montgomery form K * 2^64 mod Q (wide::montmul)
 template <typename W>
 int wide_upload_keys(mkacc_ctx* c, const W* evk, const W* pkey) {
     if (!evk || !pkey) return fail(MKACC_E_ARG, "null key pointer");
     const uint64_t Q = c->p.Q;
+    const uint64_t R = (uint64_t)(((unsigned __int128)1 << 64) % Q);
+    auto mont = [Q, R](uint64_t x) { return (uint64_t)((unsigned __int128)x * R % Q); };
     const uint32_t k = c->p.k, n = c->p.n, nk = c->nk, dg = c->dg;
     const size_t blk = (size_t)dg * 2 * kN;
     std::vector<uint64_t> host((size_t)k * (n + 1) * nk * blk);
@@ -1010,14 +1015,14 @@ int wide_upload_keys(mkacc_ctx* c, const W* evk, const W* pkey) {
                 uint64_t* dst = host.data() + (((size_t)u * (n + 1) + i) * nk + j) * blk;
                 for (size_t s = 0; s < blk; ++s) {
                     if ((uint64_t)src[s] >= Q) return fail(MKACC_E_RANGE, "evk word not a canonical residue mod Q");
-                    dst[s] = (uint64_t)src[s];
+                    dst[s] = mont((uint64_t)src[s]);
                 }
             }
     const size_t pw = (size_t)k * dg * kN;
     std::vector<uint64_t> hp(pw);
     for (size_t s = 0; s < pw; ++s) {
         if ((uint64_t)pkey[s] >= Q) return fail(MKACC_E_RANGE, "pkey word not a canonical residue mod Q");
-        hp[s] = (uint64_t)pkey[s];
+        hp[s] = mont((uint64_t)pkey[s]);
     }
     HIP_TRY(hipSetDevice(c->device));
     if (!c->d_wkeys) HIP_TRY(hipMalloc(&c->d_wkeys, host.size() * 8));

@@ -7,10 +7,11 @@
 // one-wave-per-gate design of the 27-bit kernel (mkacc_device.hpp) does not
 // carry over: here one 256-thread workgroup owns one gate, each thread holds
 // 8 EVAL slots (j = t + 256 e, coalesced key/accumulator streams), and every
-// transform runs in a 16 KiB LDS tile (radix-2 stages, one barrier each).
+// transform runs in a 16 KiB LDS tile (two stages per barrier).
 // Products are 64 x 64 -> 128-bit: Shoup with precomputed companions for the
-// fixed operands (twiddles, monomial powers psi^e, N^-1) and Barrett
-// (HAC 14.42) for the data x key products.  Every result is a canonical
+// fixed operands (twiddles, monomial powers psi^e, N^-1) and Montgomery for
+// the data x key products (keys stored as K * 2^64 mod Q at upload; the key
+// combinations are linear, so d_i, f_i stay in that form).  Every result is a canonical
 // residue, so the same reorderings as the 27-bit kernel are bit-exact.
 #pragma once
 
@@ -25,6 +26,7 @@ struct Mod64 {
     uint64_t Q;
     uint64_t mu;    // floor(2^(2L) / Q)
     uint32_t L;     // 2^(L-1) <= Q < 2^L
+    uint64_t qp;    // -Q^-1 mod 2^64 (Montgomery, R = 2^64)
 };
 
 __device__ __forceinline__ uint64_t add(uint64_t a, uint64_t b, uint64_t Q) {
@@ -47,6 +49,17 @@ __device__ __forceinline__ uint64_t mulmod(uint64_t a, uint64_t b, const Mod64& 
     const uint64_t q2 = (uint64_t)(((unsigned __int128)q1 * m.mu) >> (m.L + 1));
     uint64_t r = (uint64_t)x - q2 * m.Q;   // [0, 3Q)
     r = r >= m.Q ? r - m.Q : r;
+    return r >= m.Q ? r - m.Q : r;
+}
+
+// a * b * 2^-64 mod Q for a < Q, b < Q (Montgomery reduction of the 128-bit
+// product): the keys are stored as K * 2^64 mod Q, so montmul(g, K') = g * K.
+// t + m Q is divisible by 2^64, its low word is 0 iff t's is, and the quotient
+// is below 2Q.
+__device__ __forceinline__ uint64_t montmul(uint64_t a, uint64_t b, const Mod64& m) {
+    const uint64_t lo = a * b, hi = __umul64hi(a, b);
+    const uint64_t mq = lo * m.qp;
+    const uint64_t r = hi + __umul64hi(mq, m.Q) + (lo != 0);
     return r >= m.Q ? r - m.Q : r;
 }
 
@@ -238,8 +251,8 @@ __global__ __launch_bounds__(kThreads) void step_kernel(StepArgs a) {
                 const ulonglong2 tn = METHOD == XZW ? mono(a.psi, cneg, oj[e]) : ulonglong2{0, 0};
                 const uint64_t d = key_eff<METHOD, FIRST>(a.key1[ko + j], METHOD == XZW ? a.key2[ko + j] : 0,
                                                           FIRST ? a.keys[ko + j] : 0, tp, tn, Q);
-                uj[e] = add(uj[e], mulmod(g, d, a.m), Q);                 // <g^-1(c), d_i>
-                sv[e] = add(sv[e], mulmod(g, P[j], a.m), Q);              // <g^-1(c), P[u]_i>
+                uj[e] = add(uj[e], montmul(g, d, a.m), Q);                // <g^-1(c), d_i>
+                sv[e] = add(sv[e], montmul(g, P[j], a.m), Q);             // <g^-1(c), P[u]_i>
             }
         }
         if (tt < k) {
@@ -275,7 +288,7 @@ __global__ __launch_bounds__(kThreads) void step_kernel(StepArgs a) {
             const ulonglong2 tn = METHOD == XZW ? mono(a.psi, cneg, oj[e]) : ulonglong2{0, 0};
             const uint64_t f = key_eff<METHOD, FIRST>(a.key1[ko + j], METHOD == XZW ? a.key2[ko + j] : 0,
                                                       FIRST ? a.keys[ko + j] : 0, tp, tn, Q);
-            keep[e] = add(keep[e], mulmod(tile[j], f, a.m), Q);
+            keep[e] = add(keep[e], montmul(tile[j], f, a.m), Q);
         }
     }
     uint64_t* out = a.acc_out + ((size_t)gate * k + index) * kN;
