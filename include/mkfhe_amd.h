@@ -55,7 +55,7 @@ typedef struct mkacc_params {
     uint32_t k;        /* number of parties (numUser) */
     uint32_t n;        /* LWE / NTRU dimension (latticeParam) */
     uint32_t N;        /* ring dimension; the engine supports N = 2048 */
-    uint64_t Q;        /* ring modulus, prime, Q = 1 mod 2N, 2^26 < Q < 2^62: Q < 2^27 runs the 32-bit
+    uint64_t Q;        /* ring modulus, prime, Q = 1 mod 2N, 2^26 < Q < 2^61: Q < 2^27 runs the 32-bit
                           register-resident kernel, larger Q the 64-bit word path (EvalAcc only) */
     uint64_t q;        /* ciphertext modulus (mod); XZW computes c = floor(ct*2N/q) */
     uint32_t baseG;    /* gadget base B_g, power of two */

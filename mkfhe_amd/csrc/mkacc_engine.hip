@@ -1191,8 +1191,10 @@ int mkacc_create(const mkacc_params* pin, int device, mkacc_ctx** out) {
     mkacc_params p = *pin;
     if (p.method > MKACC_METHOD_MKNTRU_LWE) return fail(MKACC_E_ARG, "method is invalid");
     if (p.N != (uint32_t)kN) return fail(MKACC_E_UNSUPPORTED, "engine supports ring dimension N = 2048 only");
-    if (!(p.Q > (1ull << 26) && p.Q < (1ull << 62)))
-        return fail(MKACC_E_UNSUPPORTED, "engine supports 2^26 < Q < 2^62");
+    // Q < 2^61: the 64-bit path's lazy butterflies keep words below 6Q < 2^64
+    // (the reference's NATIVE_SIZE=64 limit MAX_MODULUS_SIZE is 60 bits)
+    if (!(p.Q > (1ull << 26) && p.Q < (1ull << 61)))
+        return fail(MKACC_E_UNSUPPORTED, "engine supports 2^26 < Q < 2^61");
     if ((p.Q - 1) % (2ull * p.N) != 0 || !is_prime(p.Q)) return fail(MKACC_E_ARG, "Q must be a prime = 1 mod 2N");
     if (p.k == 0 || p.k > 64 || p.n == 0) return fail(MKACC_E_ARG, "bad k or n");
     if (p.baseG < 2 || (p.baseG & (p.baseG - 1))) return fail(MKACC_E_ARG, "Gadget base should be a power of two.");

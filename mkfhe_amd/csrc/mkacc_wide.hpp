@@ -1,5 +1,5 @@
 // mkacc_wide.hpp -- the 64-bit-word accumulator path: EvalAcc for a ring
-// modulus 2^27 <= Q < 2^62 (the reference at NATIVE_SIZE=64, where
+// modulus 2^27 <= Q < 2^61 (the reference at NATIVE_SIZE=64, where
 // MAX_MODULUS_SIZE is 60; SURVEY.md s8 config 5 stress: Q = 1125899906826241,
 // B_g = 2^10).  Included by mkacc_engine.hip.
 //
@@ -9,9 +9,10 @@
 // 8 EVAL slots (j = t + 256 e, coalesced key/accumulator streams), and every
 // transform runs in a 16 KiB LDS tile (two stages per barrier).
 // Products are 64 x 64 -> 128-bit: Shoup with precomputed companions for the
-// fixed operands (twiddles, monomial powers psi^e, N^-1) and Montgomery for
+// fixed operands (twiddles, monomial powers psi^e, N^-1; built from 32-bit
+// limb multiply-adds, lazy butterflies) and Montgomery for
 // the data x key products (keys stored as K * 2^64 mod Q at upload; the key
-// combinations are linear, so d_i, f_i stay in that form).  Every result is a canonical
+// combinations are linear, so d_i, f_i stay in that form).  Every stored result is a canonical
 // residue, so the same reorderings as the 27-bit kernel are bit-exact.
 #pragma once
 
@@ -36,11 +37,32 @@ __device__ __forceinline__ uint64_t add(uint64_t a, uint64_t b, uint64_t Q) {
 __device__ __forceinline__ uint64_t sub(uint64_t a, uint64_t b, uint64_t Q) {
     return a >= b ? a - b : a + Q - b;
 }
-// x * w mod Q, wp = floor(w 2^64 / Q) (Shoup; any 64-bit x)
+// Shoup product from 32-bit limbs with a truncated quotient.  For any 64-bit x,
+// w < Q and wp = floor(w 2^64 / Q): q~ = xh*ph + hi(xh*pl) + hi(xl*ph + lo(xh*pl))
+// drops only the xl*pl partial product and one low carry, so q~ = q - delta with
+// q = floor(x wp / 2^64) and delta in {0, 1}; exact Shoup gives x w - q Q in
+// [0, 2Q), hence T = x w - q~ Q lies in [0, 3Q).  T is formed as the low 64 bits
+// of x w + q~ (2^64 - Q): two full products for the low word, four low-word
+// products (one v_mad_u64_u32 each) for the high word.  11 multiply-adds in all,
+// against ~4 wide products plus corrections for the 128-bit form.
+__device__ __forceinline__ uint32_t lo32(uint64_t x) { return (uint32_t)x; }
+__device__ __forceinline__ uint32_t hi32(uint64_t x) { return (uint32_t)(x >> 32); }
+__device__ __forceinline__ uint64_t shoup3(uint64_t x, uint64_t w, uint64_t wp, uint64_t nQ) {
+    const uint32_t xl = lo32(x), xh = hi32(x);
+    const uint64_t t1 = mad64(xh, lo32(wp), 0);
+    const uint64_t s = mad64(xl, hi32(wp), lo32(t1));
+    const uint64_t q = mad64(xh, hi32(wp), hi32(t1)) + hi32(s);
+    const uint64_t A = mad64(lo32(q), lo32(nQ), mad64(xl, lo32(w), 0));
+    uint64_t h = mad64_pin<false>(xh, lo32(w), hi32(A));
+    h = mad64_pin<false>(xl, hi32(w), h);
+    h = mad64_pin<true>(hi32(q), lo32(nQ), h);
+    h = mad64_pin<true>(lo32(q), hi32(nQ), h);
+    return ((uint64_t)lo32(h) << 32) | lo32(A);
+}
+__device__ __forceinline__ uint64_t csub(uint64_t x, uint64_t m) { return x >= m ? x - m : x; }
+// x * w mod Q, canonical (any 64-bit x)
 __device__ __forceinline__ uint64_t mul_shoup(uint64_t x, uint64_t w, uint64_t wp, uint64_t Q) {
-    const uint64_t q = __umul64hi(x, wp);
-    const uint64_t r = x * w - q * Q;   // [0, 2Q)
-    return r >= Q ? r - Q : r;
+    return csub(csub(shoup3(x, w, wp, 0 - Q), Q), Q);
 }
 // a * b mod Q for a, b < Q (Barrett, HAC 14.42 with base 2)
 __device__ __forceinline__ uint64_t mulmod(uint64_t a, uint64_t b, const Mod64& m) {
@@ -52,10 +74,10 @@ __device__ __forceinline__ uint64_t mulmod(uint64_t a, uint64_t b, const Mod64& 
     return r >= m.Q ? r - m.Q : r;
 }
 
-// a * b * 2^-64 mod Q for a < Q, b < Q (Montgomery reduction of the 128-bit
+// a * b * 2^-64 mod Q for a < 6Q, b < Q (Montgomery reduction of the 128-bit
 // product): the keys are stored as K * 2^64 mod Q, so montmul(g, K') = g * K.
 // t + m Q is divisible by 2^64, its low word is 0 iff t's is, and the quotient
-// is below 2Q.
+// is below Q + 6Q^2 / 2^64 < 2Q (Q < 2^61), so one subtraction makes it canonical.
 __device__ __forceinline__ uint64_t montmul(uint64_t a, uint64_t b, const Mod64& m) {
     const uint64_t lo = a * b, hi = __umul64hi(a, b);
     const uint64_t mq = lo * m.qp;
@@ -81,16 +103,29 @@ __device__ __forceinline__ uint64_t sdd_digit(uint64_t D, uint32_t i, const Sdd6
     return f >= s.half ? f - s.half : f + Q - s.half;
 }
 
-// CT / GS butterflies (canonical in, canonical out)
-__device__ __forceinline__ void ct(uint64_t& a, uint64_t& b, ulonglong2 w, uint64_t Q) {
-    const uint64_t U = a, V = mul_shoup(b, w.x, w.y, Q);
-    a = add(U, V, Q);
-    b = sub(U, V, Q);
+// Lazy CT / GS butterflies (Q < 2^61, so 6Q < 2^64).  Forward: values stay
+// in [0, 6Q) -- a is brought under 3Q, T = shoup3(b) < 3Q, outputs X + T and
+// X + 3Q - T.  Inverse: values stay in [0, 3Q) -- a + b reduced once by 3Q,
+// b' = shoup3(a - b + 3Q) < 3Q.  One 64-bit conditional subtraction per
+// butterfly instead of three; results are reduced where they are consumed
+// (montmul accepts g < 6Q, mul_shoup any word, canon6 for the primitives).
+struct Lazy {
+    uint64_t Q3, nQ;
+};
+__device__ __forceinline__ void ct(uint64_t& a, uint64_t& b, ulonglong2 w, const Lazy& z) {
+    const uint64_t X = csub(a, z.Q3);
+    const uint64_t T = shoup3(b, w.x, w.y, z.nQ);
+    a = X + T;
+    b = X + z.Q3 - T;
 }
-__device__ __forceinline__ void gs(uint64_t& a, uint64_t& b, ulonglong2 w, uint64_t Q) {
-    const uint64_t U = a, V = b;
-    a = add(U, V, Q);
-    b = mul_shoup(sub(U, V, Q), w.x, w.y, Q);
+__device__ __forceinline__ void gs(uint64_t& a, uint64_t& b, ulonglong2 w, const Lazy& z) {
+    const uint64_t d = a + z.Q3 - b;
+    a = csub(a + b, z.Q3);
+    b = shoup3(d, w.x, w.y, z.nQ);
+}
+// [0, 6Q) -> [0, Q)
+__device__ __forceinline__ uint64_t canon6(uint64_t x, uint64_t Q) {
+    return csub(csub(csub(x, 3 * Q), Q), Q);
 }
 
 // NTT of the LDS tile a[N], reference order (transformnat-impl.h:300-354):
@@ -98,6 +133,7 @@ __device__ __forceinline__ void gs(uint64_t& a, uint64_t& b, ulonglong2 w, uint6
 // Stages are taken two at a time (radix-4 groups j0 + {0, t/2, t, 3t/2}: one
 // barrier per pair), the last stage alone.
 __device__ __forceinline__ void ntt_fwd(uint64_t* a, const ulonglong2* __restrict__ tw, uint64_t Q) {
+    const Lazy z{3 * Q, 0 - Q};
     uint32_t m = 1, logt = kLogN - 1;                 // stage s: m = 2^s, t = 2^logt
     for (; logt >= 2; m <<= 2, logt -= 2) {          // stages (s, s+1), t >= 4
         const uint32_t h = 1u << (logt - 1);          // t / 2 = groups per block
@@ -107,10 +143,10 @@ __device__ __forceinline__ void ntt_fwd(uint64_t* a, const ulonglong2* __restric
             const uint32_t i = g >> (logt - 1), j0 = (i << (logt + 1)) + (g & (h - 1));
             uint64_t x0 = a[j0], x1 = a[j0 + h], x2 = a[j0 + 2 * h], x3 = a[j0 + 3 * h];
             const ulonglong2 w1 = tw[m + i];
-            ct(x0, x2, w1, Q);
-            ct(x1, x3, w1, Q);
-            ct(x0, x1, tw[2 * m + 2 * i], Q);
-            ct(x2, x3, tw[2 * m + 2 * i + 1], Q);
+            ct(x0, x2, w1, z);
+            ct(x1, x3, w1, z);
+            ct(x0, x1, tw[2 * m + 2 * i], z);
+            ct(x2, x3, tw[2 * m + 2 * i + 1], z);
             a[j0] = x0; a[j0 + h] = x1; a[j0 + 2 * h] = x2; a[j0 + 3 * h] = x3;
         }
         __syncthreads();
@@ -122,7 +158,7 @@ __device__ __forceinline__ void ntt_fwd(uint64_t* a, const ulonglong2* __restric
         for (int r = 0; r < kN / 2 / kThreads; ++r) {
             const uint32_t b = threadIdx.x + r * kThreads;
             const uint32_t i = b >> logt, j = (i << (logt + 1)) + (b & (t - 1));
-            ct(a[j], a[j + t], tw[m + i], Q);
+            ct(a[j], a[j + t], tw[m + i], z);
         }
         __syncthreads();
     }
@@ -130,6 +166,7 @@ __device__ __forceinline__ void ntt_fwd(uint64_t* a, const ulonglong2* __restric
 // Inverse GS without the N^-1 factor (transformnat-impl.h:492-552 up to the
 // scaling): stage pairs (t, 2t) as radix-4 groups j0 + {0, t, 2t, 3t}.
 __device__ __forceinline__ void ntt_inv_noscale(uint64_t* a, const ulonglong2* __restrict__ tw, uint64_t Q) {
+    const Lazy z{3 * Q, 0 - Q};
     uint32_t m = kN >> 1, logt = 0;                   // stage: m blocks, t = 2^logt
     for (; m >= 2; m >>= 2, logt += 2) {
         const uint32_t t = 1u << logt;
@@ -138,11 +175,11 @@ __device__ __forceinline__ void ntt_inv_noscale(uint64_t* a, const ulonglong2* _
             const uint32_t g = threadIdx.x + r * kThreads;
             const uint32_t b = g >> logt, j0 = (b << (logt + 2)) + (g & (t - 1));
             uint64_t x0 = a[j0], x1 = a[j0 + t], x2 = a[j0 + 2 * t], x3 = a[j0 + 3 * t];
-            gs(x0, x1, tw[m + 2 * b], Q);
-            gs(x2, x3, tw[m + 2 * b + 1], Q);
+            gs(x0, x1, tw[m + 2 * b], z);
+            gs(x2, x3, tw[m + 2 * b + 1], z);
             const ulonglong2 w2 = tw[(m >> 1) + b];
-            gs(x0, x2, w2, Q);
-            gs(x1, x3, w2, Q);
+            gs(x0, x2, w2, z);
+            gs(x1, x3, w2, z);
             a[j0] = x0; a[j0 + t] = x1; a[j0 + 2 * t] = x2; a[j0 + 3 * t] = x3;
         }
         __syncthreads();
@@ -153,7 +190,7 @@ __device__ __forceinline__ void ntt_inv_noscale(uint64_t* a, const ulonglong2* _
         for (int r = 0; r < kN / 2 / kThreads; ++r) {
             const uint32_t b = threadIdx.x + r * kThreads;
             const uint32_t i = b >> logt, j = (i << (logt + 1)) + (b & (t - 1));
-            gs(a[j], a[j + t], tw[m + i], Q);
+            gs(a[j], a[j + t], tw[m + i], z);
         }
         __syncthreads();
     }
@@ -304,7 +341,7 @@ __global__ __launch_bounds__(kThreads) void ntt_fwd_kernel(const uint64_t* __res
     for (int e = 0; e < kPer; ++e) tile[threadIdx.x + kThreads * e] = in[base + threadIdx.x + kThreads * e];
     __syncthreads();
     ntt_fwd(tile, tw, Q);
-    for (int e = 0; e < kPer; ++e) out[base + threadIdx.x + kThreads * e] = tile[threadIdx.x + kThreads * e];
+    for (int e = 0; e < kPer; ++e) out[base + threadIdx.x + kThreads * e] = canon6(tile[threadIdx.x + kThreads * e], Q);
 }
 __global__ __launch_bounds__(kThreads) void ntt_inv_kernel(const uint64_t* __restrict__ in, uint64_t* __restrict__ out,
                                                             const ulonglong2* __restrict__ tw, uint64_t Q,

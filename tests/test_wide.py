@@ -1,5 +1,5 @@
 """The 64-bit word path (mkfhe_amd/csrc/mkacc_wide.hpp): EvalAcc for
-2^27 <= Q < 2^62, i.e. the reference at NATIVE_SIZE=64 with a wide modulus
+2^27 <= Q < 2^61, i.e. the reference at NATIVE_SIZE=64 with a wide modulus
 (SURVEY.md s8 config 5 stress: Q = 1125899906826241, B_g = 2^10, dg = 4).
 Bit-exact against the CPU oracle, whose 64-bit arithmetic is u128-exact.
 """
