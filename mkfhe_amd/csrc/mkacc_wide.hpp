@@ -236,46 +236,54 @@ __device__ __forceinline__ uint64_t key_eff(uint64_t k1, uint64_t k2, uint64_t k
 
 // One accumulator step of one gate per workgroup (same algebra as mk_step_kernel):
 //   FIRST: acc <- HbProd(acc);  else acc <- acc + HbProd(acc (X^c - 1))
+// Four workgroups per CU (<= 128 VGPRs): the offset words D of the digit
+// decomposition live in a second LDS tile (each thread touches only its own
+// slots, so it needs no barrier) and the EVAL exponents 2 brv(j) + 1 are
+// recomputed where they are used.
+__device__ __forceinline__ uint32_t odd_exp(uint32_t j) { return 2u * (__brev(j) >> (32 - kLogN)) + 1u; }
+
 template <int METHOD, bool FIRST>
-__global__ __launch_bounds__(kThreads) void step_kernel(StepArgs a) {
+__global__ __launch_bounds__(kThreads, 4) void step_kernel(StepArgs a) {
     __shared__ uint64_t tile[kN];
+    __shared__ uint64_t dtile[kN];
     const uint32_t gate = blockIdx.x, t = threadIdx.x;
     const uint64_t Q = a.m.Q;
     const uint32_t c = a.cvals[gate], cneg = (2u * kN - c) & (2u * kN - 1u);
     const uint32_t k = a.k, index = a.index, dg = a.dg;
-    uint32_t oj[kPer];
-#pragma unroll
-    for (int e = 0; e < kPer; ++e) oj[e] = 2u * (__brev(t + kThreads * e) >> (32 - kLogN)) + 1u;
     const size_t key_f = (size_t)kN;   // f_i follows d_i inside [dg][2][N]
-    uint64_t sv[kPer], keep[kPer];
+    uint64_t sv[kPer];
 #pragma unroll
     for (int e = 0; e < kPer; ++e) sv[e] = 0;
 
     for (uint32_t tt = 1; tt <= k; ++tt) {
         const uint32_t u = index + tt < k ? index + tt : index + tt - k;
         const uint64_t* accu = a.acc_in + ((size_t)gate * k + u) * kN;
-        uint64_t a0[kPer], D[kPer], uj[kPer];
+        uint64_t uj[kPer];
 #pragma unroll
         for (int e = 0; e < kPer; ++e) {
             const uint32_t j = t + kThreads * e;
-            a0[e] = accu[j];
-            uint64_t x = a0[e];
+            uint64_t x = accu[j];
+            uj[e] = FIRST ? 0 : x;
             if (!FIRST) {   // acctemp = acc * (X^c - 1)   (xzw.cpp:336-338)
-                const ulonglong2 w = mono(a.psi, c, oj[e]);
+                const ulonglong2 w = mono(a.psi, c, odd_exp(j));
                 x = sub(mul_shoup(x, w.x, w.y, Q), x, Q);
             }
             tile[j] = x;
-            uj[e] = FIRST ? 0 : a0[e];
         }
         __syncthreads();
         ntt_inv_noscale(tile, a.twi, Q);
 #pragma unroll
-        for (int e = 0; e < kPer; ++e)
-            D[e] = sdd_offset(mul_shoup(tile[t + kThreads * e], a.ninv, a.ninvp, Q), a.sd);
+        for (int e = 0; e < kPer; ++e) {
+            const uint32_t j = t + kThreads * e;
+            dtile[j] = sdd_offset(mul_shoup(tile[j], a.ninv, a.ninvp, Q), a.sd);
+        }
         for (uint32_t i = 0; i < dg; ++i) {
             __syncthreads();
 #pragma unroll
-            for (int e = 0; e < kPer; ++e) tile[t + kThreads * e] = sdd_digit(D[e], i + 1, a.sd, Q);
+            for (int e = 0; e < kPer; ++e) {
+                const uint32_t j = t + kThreads * e;
+                tile[j] = sdd_digit(dtile[j], i + 1, a.sd, Q);
+            }
             __syncthreads();
             ntt_fwd(tile, a.twf, Q);
             const size_t ko = (size_t)i * 2 * kN;
@@ -283,52 +291,56 @@ __global__ __launch_bounds__(kThreads) void step_kernel(StepArgs a) {
 #pragma unroll
             for (int e = 0; e < kPer; ++e) {
                 const uint32_t j = t + kThreads * e;
-                const uint64_t g = tile[j];
-                const ulonglong2 tp = FIRST ? mono(a.psi, c, oj[e]) : ulonglong2{0, 0};
-                const ulonglong2 tn = METHOD == XZW ? mono(a.psi, cneg, oj[e]) : ulonglong2{0, 0};
+                const uint64_t g = tile[j];   // [0, 6Q): montmul's range
+                const ulonglong2 tp = FIRST ? mono(a.psi, c, odd_exp(j)) : ulonglong2{0, 0};
+                const ulonglong2 tn = METHOD == XZW ? mono(a.psi, cneg, odd_exp(j)) : ulonglong2{0, 0};
                 const uint64_t d = key_eff<METHOD, FIRST>(a.key1[ko + j], METHOD == XZW ? a.key2[ko + j] : 0,
                                                           FIRST ? a.keys[ko + j] : 0, tp, tn, Q);
                 uj[e] = add(uj[e], montmul(g, d, a.m), Q);                // <g^-1(c), d_i>
                 sv[e] = add(sv[e], montmul(g, P[j], a.m), Q);             // <g^-1(c), P[u]_i>
             }
         }
-        if (tt < k) {
-            uint64_t* out = a.acc_out + ((size_t)gate * k + u) * kN;
+        // acc[index] is stored here too and read back by this thread for the f-part
+        uint64_t* out = a.acc_out + ((size_t)gate * k + u) * kN;
 #pragma unroll
-            for (int e = 0; e < kPer; ++e) out[t + kThreads * e] = uj[e];
-        } else {
-#pragma unroll
-            for (int e = 0; e < kPer; ++e) keep[e] = uj[e];
-        }
+        for (int e = 0; e < kPer; ++e) out[t + kThreads * e] = uj[e];
     }
 
     // second half of HbProd: iNTT(sumV) -> SDD -> NTT -> acc[index] += <., f>  (xzw.cpp:272-289)
-    uint64_t D[kPer];
     __syncthreads();
 #pragma unroll
     for (int e = 0; e < kPer; ++e) tile[t + kThreads * e] = sv[e];
     __syncthreads();
     ntt_inv_noscale(tile, a.twi, Q);
 #pragma unroll
-    for (int e = 0; e < kPer; ++e) D[e] = sdd_offset(mul_shoup(tile[t + kThreads * e], a.ninv, a.ninvp, Q), a.sd);
+    for (int e = 0; e < kPer; ++e) {
+        const uint32_t j = t + kThreads * e;
+        dtile[j] = sdd_offset(mul_shoup(tile[j], a.ninv, a.ninvp, Q), a.sd);
+    }
+    uint64_t* out = a.acc_out + ((size_t)gate * k + index) * kN;
+    uint64_t keep[kPer];
+#pragma unroll
+    for (int e = 0; e < kPer; ++e) keep[e] = out[t + kThreads * e];
     for (uint32_t i = 0; i < dg; ++i) {
         __syncthreads();
 #pragma unroll
-        for (int e = 0; e < kPer; ++e) tile[t + kThreads * e] = sdd_digit(D[e], i + 1, a.sd, Q);
+        for (int e = 0; e < kPer; ++e) {
+            const uint32_t j = t + kThreads * e;
+            tile[j] = sdd_digit(dtile[j], i + 1, a.sd, Q);
+        }
         __syncthreads();
         ntt_fwd(tile, a.twf, Q);
         const size_t ko = (size_t)i * 2 * kN + key_f;
 #pragma unroll
         for (int e = 0; e < kPer; ++e) {
             const uint32_t j = t + kThreads * e;
-            const ulonglong2 tp = FIRST ? mono(a.psi, c, oj[e]) : ulonglong2{0, 0};
-            const ulonglong2 tn = METHOD == XZW ? mono(a.psi, cneg, oj[e]) : ulonglong2{0, 0};
+            const ulonglong2 tp = FIRST ? mono(a.psi, c, odd_exp(j)) : ulonglong2{0, 0};
+            const ulonglong2 tn = METHOD == XZW ? mono(a.psi, cneg, odd_exp(j)) : ulonglong2{0, 0};
             const uint64_t f = key_eff<METHOD, FIRST>(a.key1[ko + j], METHOD == XZW ? a.key2[ko + j] : 0,
                                                       FIRST ? a.keys[ko + j] : 0, tp, tn, Q);
             keep[e] = add(keep[e], montmul(tile[j], f, a.m), Q);
         }
     }
-    uint64_t* out = a.acc_out + ((size_t)gate * k + index) * kN;
 #pragma unroll
     for (int e = 0; e < kPer; ++e) out[t + kThreads * e] = keep[e];
 }
