@@ -94,3 +94,61 @@ def test_wide_path_matches_fast_path_at_27_bits(mk_gpu, oracle):
     got = wide.eval_batch(ct.astype(np.uint32), acc.astype(np.uint32))
     assert np.array_equal(got, want)
     assert np.array_equal(got.astype(np.uint64), orc.evalacc(evk, pkey, ct, acc))
+
+
+# Top of the supported range (Q < 2^61: the lazy butterflies keep words below
+# 6Q < 2^64).  Largest primes = 1 mod 2N below 2^61 and below 2^60 (the
+# reference's NATIVE_SIZE=64 MAX_MODULUS_SIZE); digits must satisfy
+# log2(B_g) * digitsG <= 63.
+Q61 = 2305843009213616129
+Q60 = 1152921504606830593
+
+
+def test_oracle_top_of_range_ntt_roundtrip(oracle):
+    for Q in (Q61, Q60):
+        assert oracle.is_prime(Q) and (Q - 1) % (2 * N) == 0
+        psi = oracle.root_of_unity(2 * N, Q)
+        a = oracle.fill_uniform(N, Q, 5)
+        a[:8] = Q - 1
+        assert np.array_equal(oracle.ntt_inverse(oracle.ntt_forward(a, Q, psi), Q, psi), a)
+
+
+@pytest.mark.gpu
+def test_wide_primitives_top_of_range(mk_gpu, oracle):
+    """NTT / iNTT / SDD at a 61-bit Q: the lazy ranges' worst case (words up to 6Q)."""
+    mk = mk_gpu
+    eng = _eng(mk, mk.MKNTRU, 2, 3, Q61, 45181, 1 << 21)
+    assert eng.wide and eng.dg == 2
+    psi = oracle.root_of_unity(2 * N, Q61)
+    assert eng.params.root == psi
+    a = oracle.fill_uniform(4 * N, Q61, 31).reshape(4, N)
+    a[0] = Q61 - 1                      # all-maximal residues
+    a[1, ::2] = 0
+    f = eng.ntt_forward(a)
+    assert np.array_equal(f, np.stack([oracle.ntt_forward(x, Q61, psi) for x in a]))
+    assert np.array_equal(eng.ntt_inverse(f), a)
+    assert np.array_equal(eng.sdd(a), np.stack([oracle.sdd(x, Q61, 1 << 21, 2) for x in a]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method", ["XZW", "XZW_B"])
+def test_wide_evalacc_60bit(mk_gpu, oracle, method):
+    """EvalAcc at the reference's largest NATIVE_SIZE=64 modulus size (60 bits)."""
+    mk = mk_gpu
+    m = oracle.XZW if method == "XZW" else oracle.XZW_B
+    orc, evk, pkey, ct, acc = make_case(oracle, m, 2, 3, 45181, 1 << 20, 2, seed=60, Q=Q60)
+    exp = orc.evalacc(evk, pkey, ct, acc)
+    eng = _eng(mk, mk.MKNTRU if method == "XZW" else mk.MKNTRU_LWE, 2, 3, Q60, 45181, 1 << 20)
+    assert eng.wide
+    eng.upload_keys(evk.astype(np.uint64), pkey.astype(np.uint64))
+    got = eng.eval_batch(ct.astype(np.uint32), acc.astype(np.uint64))
+    assert np.array_equal(got, exp), int(np.count_nonzero(got != exp))
+
+
+@pytest.mark.gpu
+def test_wide_rejects_q_at_2_61(mk_gpu):
+    mk = mk_gpu
+    # the range check comes before the primality check
+    with pytest.raises(mk.MkaccError) as e:
+        _eng(mk, mk.MKNTRU, 2, 3, (1 << 61) + 1, 45181, 1 << 21)
+    assert e.value.code == -2
