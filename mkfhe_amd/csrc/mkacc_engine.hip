@@ -213,6 +213,11 @@ enum DMode { D_COMPUTE = 0, D_STORE = 1, D_LOAD = 2 };
 #define MKACC_D_SCRATCH 0
 #endif
 constexpr bool kDScratch = MKACC_D_SCRATCH != 0;
+// f-part of the index pass as two key sums and one monomial product per slot
+#ifndef MKACC_SPLIT_F
+#define MKACC_SPLIT_F 1
+#endif
+constexpr bool kSplitF = MKACC_SPLIT_F != 0;
 
 template <int DG, int METHOD, bool FIRST, bool START, int DM>
 __device__ __forceinline__ void mac_digit(const uint32_t (&g)[kRegs], int i, uint32_t u, uint64_t (&uj)[kRegs],
@@ -286,6 +291,49 @@ __device__ __forceinline__ void mac_index(const uint32_t (&h)[kRegs], int i, uin
             w[r] = mad64(h[r], feff, w[r]);
         }
         sched_fence();
+    }
+}
+
+// XZW steps after the first: f_i = ev1'_i - ev2'_i X^-c (xzw.cpp:322-325) is
+// linear in the keys, so  sum_i h_i f_i = sum_i h_i ev1'_i - X^-c sum_i h_i ev2'_i:
+// two lazy sums per slot here and ONE monomial product per slot after the
+// last digit (mac_index_finish) instead of one per slot and digit.
+template <int DG>
+__device__ __forceinline__ void mac_index_split(const uint32_t (&h)[kRegs], int i, uint64_t (&w)[kRegs],
+                                                uint64_t (&w2)[kRegs], __amdgpu_buffer_rsrc_t rk1,
+                                                __amdgpu_buffer_rsrc_t rk2, uint32_t vo) {
+    const uint32_t polyB = kN * 4u;
+    const uint32_t koff = (uint32_t)(2 * i + 1) * polyB;
+    constexpr int kPrefetch = Prefetch<DG>::value;
+    KeyGroup kg[kPrefetch + 1];
+    auto issue = [&](KeyGroup& t, int gq) {
+        const uint32_t go = gq * 1024u;
+        t.k1 = bload4(rk1, vo, koff + go);
+        t.k2 = bload4(rk2, vo, koff + go);
+    };
+#pragma unroll
+    for (int j = 0; j < kPrefetch; ++j) issue(kg[j], j);
+#pragma unroll
+    for (int gq = 0; gq < 8; ++gq) {
+        if (gq + kPrefetch < 8) issue(kg[(gq + kPrefetch) % (kPrefetch + 1)], gq + kPrefetch);
+        const KeyGroup& t = kg[gq % (kPrefetch + 1)];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int r = 4 * gq + e;
+            w[r] = mad64(h[r], t.k1[e], w[r]);
+            w2[r] = mad64(h[r], t.k2[e], w2[r]);
+        }
+        sched_fence();
+    }
+}
+// w - X^-c * w2 per slot, as a lazy sum below 2^58 (w2 < DG * 4Q * Q <= 16 Q^2)
+__device__ __forceinline__ void mac_index_finish(uint64_t (&w)[kRegs], const uint64_t (&w2)[kRegs],
+                                                 const uint2* psi, const Mono& mn, const Mod& m) {
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) {
+        const uint32_t t = mul_shoup_lazy(reduce58(w2[r], m), mn.at(psi, r), m.Q);   // [0, 2Q)
+        w[r] += 2u * m.Q - t;
+        if ((r & 7) == 7) sched_fence();
     }
 }
 
@@ -472,6 +520,12 @@ __device__ __forceinline__ void step_body(const StepCtx& s, uint32_t k, uint32_t
     uint64_t w[kRegs];
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) w[r] = keep[r];
+    constexpr bool kSplit = METHOD == XZW && !FIRST && kSplitF;
+    uint64_t w2[kSplit ? kRegs : 1];
+    if constexpr (kSplit) {
+#pragma unroll
+        for (int r = 0; r < kRegs; ++r) w2[r] = 0;
+    }
 #pragma unroll kDigitUnroll
     for (int i = 0; i < DG; ++i) {
         if (i > 0) {
@@ -480,8 +534,12 @@ __device__ __forceinline__ void step_body(const StepCtx& s, uint32_t k, uint32_t
         }
         ntt_fwd(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, l, Q);
         digit_range<DG>(x, Q);
-        mac_index<DG, METHOD, FIRST>(x, i, w, s.rk1, s.rk2, s.rks, s.tb.psi, s.mp, s.mn, s.vo, Q);
+        if constexpr (kSplit)
+            mac_index_split<DG>(x, i, w, w2, s.rk1, s.rk2, s.vo);
+        else
+            mac_index<DG, METHOD, FIRST>(x, i, w, s.rk1, s.rk2, s.rks, s.tb.psi, s.mp, s.mn, s.vo, Q);
     }
+    if constexpr (kSplit) mac_index_finish(w, w2, s.tb.psi, s.mn, s.m);
     const uint32_t ioff = index * polyB;
 #pragma unroll
     for (int gq = 0; gq < 8; ++gq) {
