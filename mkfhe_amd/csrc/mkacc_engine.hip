@@ -163,8 +163,9 @@ __device__ __forceinline__ uint32_t key_eff(uint32_t k1, uint32_t k2, uint32_t k
             const uint32_t t2 = sub_mod(mul_shoup(k2, tn.x, tn.y, Q), k2, Q);
             return add_mod(add_mod(ks, t1, Q), t2, Q);
         }
-        // ev1 - ev2*(X^-c - 1) - ev2  ==  ev1 - ev2*X^-c   (xzw.cpp:322-325)
-        uint32_t d = k1 + 2u * Q - mul_shoup_lazy(k2, tn, Q);    // (0, 3Q)
+        // ev1 - ev2*(X^-c - 1) - ev2  ==  ev1 - ev2*X^-c   (xzw.cpp:322-325);
+        // mn holds -X^-c here (exponent -c + N: psi^N = -1), so one add
+        uint32_t d = k1 + mul_shoup_lazy(k2, tn, Q);             // [0, 3Q)
         d = min(d, d - 2u * Q);                                  // [0, 2Q)
         return min(d, d - Q);
     } else {
@@ -326,13 +327,13 @@ __device__ __forceinline__ void mac_index_split(const uint32_t (&h)[kRegs], int 
         sched_fence();
     }
 }
-// w - X^-c * w2 per slot, as a lazy sum below 2^58 (w2 < DG * 4Q * Q <= 16 Q^2)
+// w - X^-c * w2 per slot (mn holds -X^-c), as a lazy sum below 2^58
+// (w2 < DG * 4Q * Q <= 16 Q^2)
 __device__ __forceinline__ void mac_index_finish(uint64_t (&w)[kRegs], const uint64_t (&w2)[kRegs],
                                                  const uint2* psi, const Mono& mn, const Mod& m) {
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) {
-        const uint32_t t = mul_shoup_lazy(reduce58(w2[r], m), mn.at(psi, r), m.Q);   // [0, 2Q)
-        w[r] += 2u * m.Q - t;
+        w[r] += mul_shoup_lazy(reduce58(w2[r], m), mn.at(psi, r), m.Q);   // [0, 2Q)
         if ((r & 7) == 7) sched_fence();
     }
 }
@@ -464,7 +465,8 @@ __global__ __launch_bounds__(kThreads, 2) void mk_step_kernel(StepArgs a) {
                     a.m,
                     a.sd,
                     make_mono(c, l),
-                    make_mono(cneg, l),
+                    // X^-c in the first step; -X^-c = X^(N-c) in the later XZW steps (key_eff)
+                    make_mono(FIRST || METHOD != XZW ? cneg : (cneg + kN) & (2u * kN - 1u), l),
                     l,
                     l * 16u,
                     make_rsrc(a.acc_in + (size_t)gate * k * kN, k * polyB),
