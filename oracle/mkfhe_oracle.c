@@ -40,12 +40,45 @@ uint64_t orc_powmod(uint64_t a, uint64_t e, uint64_t Q) {
     return r;
 }
 
-static inline uint64_t addmod(uint64_t a, uint64_t b, uint64_t Q) {
-    uint64_t s = a + b;
-    return s >= Q ? s - Q : s;
-}
+/* branch-free conditional corrections (random residues defeat the branch predictor) */
+static inline uint64_t csub(uint64_t r, uint64_t Q) { return r - (Q & (0 - (uint64_t)(r >= Q))); }
+static inline uint64_t addmod(uint64_t a, uint64_t b, uint64_t Q) { return csub(a + b, Q); }
 static inline uint64_t submod(uint64_t a, uint64_t b, uint64_t Q) {
-    return a >= b ? a - b : a + Q - b;
+    return a - b + (Q & (0 - (uint64_t)(a < b)));
+}
+
+/* Exact reductions used by the accumulator loops.  The reference's pointwise
+ * product is a plain 64-bit `%` (ubintnat.h:1304-1310) and its NTT uses
+ * Shoup-precomputed twiddles (ubintnat.h:1488-1494); every form returns the
+ * canonical residue, so the choice only changes the speed of the oracle.
+ *   Q < 2^32 : Barrett with mu = floor(2^64 / Q) on the 64-bit product
+ *              (q_est in {q-1, q}: one conditional subtraction);
+ *   otherwise: 128-bit product and `%`.                                      */
+typedef struct modq {
+    uint64_t Q, mu;
+    int big;
+} modq;
+
+static modq make_modq(uint64_t Q) {
+    modq m;
+    m.Q = Q;
+    m.big = Q > 0xFFFFFFFFull;
+    m.mu = m.big ? 0 : (uint64_t)((((u128)1) << 64) / Q);
+    return m;
+}
+static inline uint64_t mm(const modq* m, uint64_t a, uint64_t b) {
+    if (!m->big) {
+        const uint64_t p = a * b;
+        const uint64_t qe = (uint64_t)(((u128)p * m->mu) >> 64);
+        return csub(p - qe * m->Q, m->Q);
+    }
+    return (uint64_t)(((u128)a * b) % m->Q);
+}
+/* Shoup companion floor(w 2^64 / Q) and product a*w mod Q (any a < 2^64, Q < 2^63) */
+static inline uint64_t shoup_pre(uint64_t w, uint64_t Q) { return (uint64_t)((((u128)w) << 64) / Q); }
+static inline uint64_t shoup_mul(uint64_t a, uint64_t w, uint64_t wp, uint64_t Q) {
+    const uint64_t qe = (uint64_t)(((u128)a * wp) >> 64);
+    return csub(a * w - qe * Q, Q);
 }
 
 uint64_t orc_modinv(uint64_t a, uint64_t Q) {
@@ -101,6 +134,16 @@ uint64_t orc_first_prime(uint32_t nbits, uint64_t m) {
     return q2;
 }
 
+/* NextPrime: nbtheory-impl.h:361-369.  Smallest prime q' > q with q' = q mod m. */
+uint64_t orc_next_prime(uint64_t q, uint64_t m) {
+    uint64_t c = q + m;
+    while (!orc_is_prime(c)) {
+        if (c + m < c) return 0; /* the reference throws math_error on overflow */
+        c += m;
+    }
+    return c;
+}
+
 /* PreviousPrime: nbtheory-impl.h:369-377. */
 uint64_t orc_previous_prime(uint64_t q, uint64_t m) {
     uint64_t c = q - m;
@@ -148,6 +191,15 @@ uint32_t orc_digits_g(uint64_t Q, uint32_t baseG) {
     return (uint32_t)ceil(logQ / log((double)baseG));
 }
 
+/* Element-wise vector arithmetic of NativeVectorT (mubintvecnat.cpp:235-244
+ * ModAdd, :279-288 ModSub, :324-340 ModMul) with the same reductions the
+ * accumulator loops use (mm / addmod / submod).  op: 0 add, 1 sub, 2 mul. */
+void orc_vec_mod(int op, const uint64_t* a, const uint64_t* b, uint64_t* out, size_t n, uint64_t Q) {
+    const modq m = make_modq(Q);
+    for (size_t i = 0; i < n; ++i)
+        out[i] = op == 0 ? addmod(a[i], b[i], Q) : op == 1 ? submod(a[i], b[i], Q) : mm(&m, a[i], b[i]);
+}
+
 /* ------------------------------------------------------------------------ */
 /* NTT (transformnat-impl.h)                                                */
 /* ------------------------------------------------------------------------ */
@@ -160,7 +212,9 @@ static uint32_t brv(uint32_t x, uint32_t bits) {
 static uint32_t ilog2u(uint32_t x) { uint32_t r = 0; while ((1u << r) < x) ++r; return r; }
 
 /* Tables exactly as ChineseRemainderTransformFTTNat::PreCompute
- * (transformnat-impl.h:705-760): table[brv(i)] = psi^i, tableI[brv(i)] = psi^-i. */
+ * (transformnat-impl.h:705-760): table[brv(i)] = psi^i, tableI[brv(i)] = psi^-i,
+ * each followed by its Shoup companions: floor(w 2^64 / Q) at +N and, for
+ * Q < 2^32, floor(w 2^32 / Q) at +2N. */
 static void make_tables(uint64_t* tab, uint64_t* tabI, uint32_t N, uint64_t Q, uint64_t psi) {
     uint32_t lg = ilog2u(N);
     uint64_t x = 1, xi = 1, psiI = orc_modinv(psi, Q);
@@ -168,21 +222,75 @@ static void make_tables(uint64_t* tab, uint64_t* tabI, uint32_t N, uint64_t Q, u
         uint32_t r = brv(i, lg);
         tab[r] = x;
         tabI[r] = xi;
+        tab[N + r] = shoup_pre(x, Q);
+        tabI[N + r] = shoup_pre(xi, Q);
+        tab[2 * N + r] = Q <= 0xFFFFFFFFull ? (x << 32) / Q : 0;
+        tabI[2 * N + r] = Q <= 0xFFFFFFFFull ? (xi << 32) / Q : 0;
         x = orc_mulmod(x, psi, Q);
         xi = orc_mulmod(xi, psiI, Q);
     }
 }
 
 /* ForwardTransformToBitReverseInPlace, transformnat-impl.h:300-354. */
-static void ntt_fwd_tab(uint64_t* a, uint32_t N, uint64_t Q, const uint64_t* tab) {
+/* Q < 2^32: Shoup with the 32-bit companion floor(w 2^32 / Q) on 32x32->64
+ * products, written so that the butterfly loops vectorize (vpmuludq). */
+static inline uint64_t shoup32(uint64_t x, uint64_t w, uint64_t wp32, uint64_t Q) {
+    const uint64_t qe = ((uint64_t)(uint32_t)x * (uint32_t)wp32) >> 32;
+    return csub((uint64_t)(uint32_t)x * (uint32_t)w - (uint64_t)(uint32_t)qe * (uint32_t)Q, Q);
+}
+static void ntt_fwd_tab32(uint64_t* restrict a, uint32_t N, uint64_t Q, const uint64_t* tab) {
     uint32_t t = N;
     for (uint32_t m = 1; m < N; m <<= 1) {
         t >>= 1;
         for (uint32_t i = 0; i < m; ++i) {
-            uint64_t w = tab[m + i];
+            const uint64_t w = tab[m + i], wp = tab[2 * N + m + i];
+            uint64_t* restrict x = a + 2 * i * t;
+            uint64_t* restrict y = x + t;
+            for (uint32_t j = 0; j < t; ++j) {
+                const uint64_t U = x[j], V = shoup32(y[j], w, wp, Q);
+                x[j] = csub(U + V, Q);
+                y[j] = U - V + (Q & (0 - (uint64_t)(U < V)));
+            }
+        }
+    }
+}
+static void ntt_inv_tab32(uint64_t* restrict a, uint32_t N, uint64_t Q, const uint64_t* tabI, uint64_t Ninv) {
+    const uint64_t NinvP = (Ninv << 32) / Q;
+    for (uint32_t i = 0; i < N; i += 2) {
+        uint64_t w = tabI[(i + N) >> 1], wp = tabI[2 * N + ((i + N) >> 1)];
+        uint64_t lo = a[i], hi = a[i + 1];
+        uint64_t d = submod(lo, hi, Q);
+        lo = addmod(lo, hi, Q);
+        a[i] = shoup32(lo, Ninv, NinvP, Q);
+        a[i + 1] = shoup32(shoup32(d, w, wp, Q), Ninv, NinvP, Q);
+    }
+    for (uint32_t m = N >> 2, t = 2; m >= 1; m >>= 1, t <<= 1) {
+        for (uint32_t i = 0; i < m; ++i) {
+            const uint64_t w = tabI[i + m], wp = tabI[2 * N + i + m];
+            uint64_t* restrict x = a + 2 * i * t;
+            uint64_t* restrict y = x + t;
+            for (uint32_t j = 0; j < t; ++j) {
+                const uint64_t lo = x[j], hi = y[j];
+                x[j] = csub(lo + hi, Q);
+                y[j] = shoup32(lo - hi + (Q & (0 - (uint64_t)(lo < hi))), w, wp, Q);
+            }
+        }
+    }
+}
+
+static void ntt_fwd_tab(uint64_t* a, uint32_t N, uint64_t Q, const uint64_t* tab) {
+    if (Q <= 0xFFFFFFFFull) {
+        ntt_fwd_tab32(a, N, Q, tab);
+        return;
+    }
+    uint32_t t = N;
+    for (uint32_t m = 1; m < N; m <<= 1) {
+        t >>= 1;
+        for (uint32_t i = 0; i < m; ++i) {
+            uint64_t w = tab[m + i], wp = tab[N + m + i];
             uint32_t j1 = 2 * i * t;
             for (uint32_t j = j1; j < j1 + t; ++j) {
-                uint64_t U = a[j], V = orc_mulmod(a[j + t], w, Q);
+                uint64_t U = a[j], V = shoup_mul(a[j + t], w, wp, Q);
                 a[j] = addmod(U, V, Q);
                 a[j + t] = submod(U, V, Q);
             }
@@ -193,38 +301,43 @@ static void ntt_fwd_tab(uint64_t* a, uint32_t N, uint64_t Q, const uint64_t* tab
 /* InverseTransformFromBitReverseInPlace, transformnat-impl.h:492-552
  * (stride-1 stage first with N^-1 fused, then GS stages of growing stride). */
 static void ntt_inv_tab(uint64_t* a, uint32_t N, uint64_t Q, const uint64_t* tabI, uint64_t Ninv) {
+    if (Q <= 0xFFFFFFFFull) {
+        ntt_inv_tab32(a, N, Q, tabI, Ninv);
+        return;
+    }
+    const uint64_t NinvP = shoup_pre(Ninv, Q);
     for (uint32_t i = 0; i < N; i += 2) {
-        uint64_t w = tabI[(i + N) >> 1];
+        uint64_t w = tabI[(i + N) >> 1], wp = tabI[N + ((i + N) >> 1)];
         uint64_t lo = a[i], hi = a[i + 1];
         uint64_t d = submod(lo, hi, Q);
         lo = addmod(lo, hi, Q);
-        a[i] = orc_mulmod(lo, Ninv, Q);
-        a[i + 1] = orc_mulmod(orc_mulmod(d, w, Q), Ninv, Q);
+        a[i] = shoup_mul(lo, Ninv, NinvP, Q);
+        a[i + 1] = shoup_mul(shoup_mul(d, w, wp, Q), Ninv, NinvP, Q);
     }
     for (uint32_t m = N >> 2, t = 2; m >= 1; m >>= 1, t <<= 1) {
         for (uint32_t i = 0; i < m; ++i) {
-            uint64_t w = tabI[i + m];
+            uint64_t w = tabI[i + m], wp = tabI[N + i + m];
             uint32_t j1 = 2 * i * t;
             for (uint32_t j = j1; j < j1 + t; ++j) {
                 uint64_t lo = a[j], hi = a[j + t];
                 a[j] = addmod(lo, hi, Q);
-                a[j + t] = orc_mulmod(submod(lo, hi, Q), w, Q);
+                a[j + t] = shoup_mul(submod(lo, hi, Q), w, wp, Q);
             }
         }
     }
 }
 
 void orc_ntt_forward(uint64_t* a, uint32_t N, uint64_t Q, uint64_t psi) {
-    uint64_t* tab = (uint64_t*)malloc(sizeof(uint64_t) * N * 2);
-    make_tables(tab, tab + N, N, Q, psi);
+    uint64_t* tab = (uint64_t*)malloc(sizeof(uint64_t) * N * 6);
+    make_tables(tab, tab + 3 * N, N, Q, psi);
     ntt_fwd_tab(a, N, Q, tab);
     free(tab);
 }
 
 void orc_ntt_inverse(uint64_t* a, uint32_t N, uint64_t Q, uint64_t psi) {
-    uint64_t* tab = (uint64_t*)malloc(sizeof(uint64_t) * N * 2);
-    make_tables(tab, tab + N, N, Q, psi);
-    ntt_inv_tab(a, N, Q, tab + N, orc_modinv(N, Q));
+    uint64_t* tab = (uint64_t*)malloc(sizeof(uint64_t) * N * 6);
+    make_tables(tab, tab + 3 * N, N, Q, psi);
+    ntt_inv_tab(a, N, Q, tab + 3 * N, orc_modinv(N, Q));
     free(tab);
 }
 
@@ -284,8 +397,9 @@ struct orc_ctx {
     orc_params p;
     uint32_t dg, nk;
     uint64_t Ninv;
-    uint64_t* tab;   /* forward table [N] */
-    uint64_t* tabI;  /* inverse table [N] */
+    modq m;
+    uint64_t* tab;   /* forward table [N] + Shoup companions [2N] (make_tables) */
+    uint64_t* tabI;  /* inverse table [N] + Shoup companions [2N] */
     uint64_t* mono;  /* [2N][N] monomials X^m - 1 in EVAL (mk-cryptoparameters.cpp:51-70) */
 };
 
@@ -301,8 +415,9 @@ orc_ctx* orc_ctx_create(const orc_params* p) {
     uint32_t N = p->N;
     uint64_t Q = p->Q;
     c->Ninv = orc_modinv(N, Q);
-    c->tab = (uint64_t*)malloc(sizeof(uint64_t) * N);
-    c->tabI = (uint64_t*)malloc(sizeof(uint64_t) * N);
+    c->m = make_modq(Q);
+    c->tab = (uint64_t*)malloc(sizeof(uint64_t) * N * 3);
+    c->tabI = (uint64_t*)malloc(sizeof(uint64_t) * N * 3);
     make_tables(c->tab, c->tabI, N, Q, c->p.psi);
     c->mono = (uint64_t*)calloc((size_t)2 * N * N, sizeof(uint64_t));
     for (uint32_t i = 0; i < N; ++i) {               /* X^i - 1 */
@@ -361,8 +476,8 @@ static void hbprod(const orc_ctx* c, const uint64_t* d, const uint64_t* f, uint3
             uint64_t uj = 0, v = 0;
             for (uint32_t i = 0; i < dg; ++i) {
                 uint64_t g = dct[(size_t)i * N + s];
-                uj = addmod(uj, orc_mulmod(g, d[(size_t)i * N + s], Q), Q);
-                v = addmod(v, orc_mulmod(g, Pu[(size_t)i * N + s], Q), Q);
+                uj = addmod(uj, mm(&c->m, g, d[(size_t)i * N + s]), Q);
+                v = addmod(v, mm(&c->m, g, Pu[(size_t)i * N + s]), Q);
             }
             sumV[s] = addmod(sumV[s], v, Q);
             out[s] = uj;
@@ -375,7 +490,7 @@ static void hbprod(const orc_ctx* c, const uint64_t* d, const uint64_t* f, uint3
     for (uint32_t s = 0; s < N; ++s) {
         uint64_t w = 0;
         for (uint32_t i = 0; i < dg; ++i)
-            w = addmod(w, orc_mulmod(dct[(size_t)i * N + s], f[(size_t)i * N + s], Q), Q);
+            w = addmod(w, mm(&c->m, dct[(size_t)i * N + s], f[(size_t)i * N + s]), Q);
         out[s] = addmod(out[s], w, Q);
     }
 }
@@ -415,19 +530,19 @@ static int evalacc_one(const orc_ctx* c, const uint64_t* evk, const uint64_t* pk
                             /* AddToAccXZW0 xzw.cpp:375-378: evs + ev1*(X^c-1) + ev2*(X^-c-1) */
                             const uint64_t* es = keyp(c, evk, u, 0, n, dgt, part);
                             for (uint32_t s = 0; s < N; ++s)
-                                out[s] = addmod(addmod(es[s], orc_mulmod(e1[s], mono[s], Q), Q),
-                                                orc_mulmod(e2[s], monoN[s], Q), Q);
+                                out[s] = addmod(addmod(es[s], mm(&c->m, e1[s], mono[s]), Q),
+                                                mm(&c->m, e2[s], monoN[s]), Q);
                         } else {
                             /* AddToAccXZW xzw.cpp:322-325: ev1 - ev2*(X^-c-1) - ev2 */
                             for (uint32_t s = 0; s < N; ++s)
-                                out[s] = submod(submod(e1[s], orc_mulmod(e2[s], monoN[s], Q), Q), e2[s], Q);
+                                out[s] = submod(submod(e1[s], mm(&c->m, e2[s], monoN[s]), Q), e2[s], Q);
                         }
                     } else {
                         if (first) {
                             /* AddToAccXZW0 xzw_B.cpp:368-371: evs + ev1*(X^c-1) */
                             const uint64_t* es = keyp(c, evk, u, 0, n, dgt, part);
                             for (uint32_t s = 0; s < N; ++s)
-                                out[s] = addmod(es[s], orc_mulmod(e1[s], mono[s], Q), Q);
+                                out[s] = addmod(es[s], mm(&c->m, e1[s], mono[s]), Q);
                         } else {
                             /* AddToAccXZW xzw_B.cpp:311-314: d = ev1 */
                             memcpy(out, e1, sizeof(uint64_t) * N);
@@ -441,7 +556,7 @@ static int evalacc_one(const orc_ctx* c, const uint64_t* evk, const uint64_t* pk
                 /* acctemp = acc * (X^c - 1); HbProd(acctemp); acc += acctemp (xzw.cpp:327-344) */
                 for (uint32_t w = 0; w < k; ++w)
                     for (uint32_t s = 0; s < N; ++s)
-                        acctemp[(size_t)w * N + s] = orc_mulmod(acc[(size_t)w * N + s], mono[s], Q);
+                        acctemp[(size_t)w * N + s] = mm(&c->m, acc[(size_t)w * N + s], mono[s]);
                 hbprod(c, d, f, u, pkey, acctemp, scratch);
                 for (size_t s = 0; s < (size_t)k * N; ++s) acc[s] = addmod(acc[s], acctemp[s], Q);
             }

@@ -30,10 +30,15 @@ extern "C" {
 int      orc_is_prime(uint64_t n);
 uint64_t orc_first_prime(uint32_t nbits, uint64_t m);     /* nbtheory-impl.h:334-357 */
 uint64_t orc_previous_prime(uint64_t q, uint64_t m);      /* nbtheory-impl.h:369-377 */
+uint64_t orc_next_prime(uint64_t q, uint64_t m);          /* nbtheory-impl.h:361-369 (0 on overflow) */
 uint64_t orc_root_of_unity(uint64_t m, uint64_t Q);       /* nbtheory-impl.h:183-231 (minimal root) */
 uint64_t orc_modinv(uint64_t a, uint64_t Q);
 uint64_t orc_mulmod(uint64_t a, uint64_t b, uint64_t Q);
 uint64_t orc_powmod(uint64_t a, uint64_t e, uint64_t Q);
+
+/* ---- NativeVectorT element-wise ModAdd / ModSub / ModMul (mubintvecnat.cpp:235-350);
+ *      op 0 add, 1 sub, 2 mul; inputs canonical residues mod Q < 2^62 ---- */
+void orc_vec_mod(int op, const uint64_t* a, const uint64_t* b, uint64_t* out, size_t n, uint64_t Q);
 
 /* ---- negacyclic NTT in the reference's EVALUATION order ----
  * forward: transformnat-impl.h:300-354 (CT, bit-reversed output)

@@ -53,6 +53,9 @@ def lib():
         L = ctypes.CDLL(_LIB_PATH)
         L.orc_first_prime.restype = ctypes.c_uint64
         L.orc_first_prime.argtypes = [ctypes.c_uint32, ctypes.c_uint64]
+        L.orc_next_prime.restype = ctypes.c_uint64
+        L.orc_next_prime.argtypes = [ctypes.c_uint64, ctypes.c_uint64]
+        L.orc_vec_mod.argtypes = [ctypes.c_int, _u64p, _u64p, _u64p, ctypes.c_size_t, ctypes.c_uint64]
         L.orc_previous_prime.restype = ctypes.c_uint64
         L.orc_previous_prime.argtypes = [ctypes.c_uint64, ctypes.c_uint64]
         L.orc_root_of_unity.restype = ctypes.c_uint64
@@ -113,6 +116,19 @@ def first_prime(nbits: int, m: int) -> int:
 
 def previous_prime(q: int, m: int) -> int:
     return int(lib().orc_previous_prime(q, m))
+
+
+def next_prime(q: int, m: int) -> int:
+    return int(lib().orc_next_prime(q, m))
+
+
+def vec_mod(op: str, a, b, Q: int) -> np.ndarray:
+    """NativeVectorT ModAdd / ModSub / ModMul (op 'add' | 'sub' | 'mul')."""
+    x = np.ascontiguousarray(np.asarray(a, dtype=np.uint64))
+    y = np.ascontiguousarray(np.asarray(b, dtype=np.uint64))
+    out = np.empty_like(x)
+    lib().orc_vec_mod({"add": 0, "sub": 1, "mul": 2}[op], _p64(x), _p64(y), _p64(out), x.size, Q)
+    return out
 
 
 def root_of_unity(m: int, Q: int) -> int:

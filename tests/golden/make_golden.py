@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Generate tests/golden/*.json (committed fixtures; run here, never on the GPU box).
 
-  python tests/golden/make_golden.py
+  python tests/golden/make_golden.py [--kats-only]
 
 reference_kats.json
     Known-answer vectors held by the reference's own unit tests for the
@@ -52,6 +52,45 @@ REFERENCE_KATS = {
                      "src": "src/core/unittest/UnitTestPolyElements.cpp:512-521"},
     "crt_mult": {"q": 113, "m": 8, "a": [1, 2, 4, 1], "out": [94, 109, 11, 18],
                  "src": "src/core/unittest/UnitTestTransform.cpp:58-93"},
+    "next_prime": {"bits": 22, "m": 2048,
+                   "chain": [4208641, 4263937, 4270081, 4274177, 4294657, 4300801, 4304897, 4319233, 4323329, 4360193],
+                   "src": "src/core/unittest/UnitTestNbTheory.cpp:380-397 (test_nextQ: FirstPrime(22, 2048), then NextPrime x10)"},
+    "vec_mod_1limb": {
+        "q": 163841,
+        "a": [127753, 77706, 17133, 22582, 112132, 27625, 126773, 8924,
+              125972, 2551, 113837, 112045, 100953, 77352, 132013, 57029],
+        "b": [66773, 69572, 142134, 141115, 123182, 155822, 128147, 94818,
+              135782, 30844, 88634, 99407, 53647, 111689, 28502, 26401],
+        "add": [30685, 147278, 159267, 163697, 71473, 19606, 91079, 103742,
+                97913, 33395, 38630, 47611, 154600, 25200, 160515, 83430],
+        "sub": [60980, 8134, 38840, 45308, 152791, 35644, 162467, 77947,
+                154031, 135548, 25203, 12638, 47306, 129504, 103511, 30628],
+        "mul": [69404, 64196, 13039, 115321, 28519, 151998, 89117, 80908,
+                57386, 39364, 8355, 146135, 61336, 31598, 25961, 87680],
+        "src": "src/core/unittest/UnitTestMubintvec.cpp:276-358 (basic_vector_vector_mod_math_1_limb)"},
+    "vec_mod_2limb": {
+        "q": 4057816419532801,
+        "a": [185225172798255, 98879665709163, 3497410031351258, 4012431933509255,
+              1543020758028581, 135094568432141, 3976954337141739, 4030348521557120,
+              175940803531155, 435236277692967, 3304652649070144, 2032520019613814,
+              375749152798379, 3933203511673255, 2293434116159938, 1201413067178193],
+        "b": [698898215124963, 39832572186149, 1835473200214782, 1041547470449968,
+              1076152419903743, 433588874877196, 2336100673132075, 2990190360138614,
+              754647536064726, 702097990733190, 2102063768035483, 119786389165930,
+              3976652902630043, 3238750424196678, 2978742255253796, 2124827461185795],
+        "add": [884123387923218, 138712237895312, 1275066812033239, 996162984426422,
+                2619173177932324, 568683443309337, 2255238590741013, 2962722462162933,
+                930588339595881, 1137334268426157, 1348899997572826, 2152306408779744,
+                294585635895621, 3114137516337132, 1214359951880933, 3326240528363988],
+        "sub": [3544143377206093, 59047093523014, 1661936831136476, 2970884463059287,
+                466868338124838, 3759322113087746, 1640853664009664, 1040158161418506,
+                3479109686999230, 3790954706492578, 1202588881034661, 1912733630447884,
+                456912669701137, 694453087476577, 3372508280438943, 3134402025525199],
+        "mul": [585473140075497, 3637571624495703, 1216097920193708, 1363577444007558,
+                694070384788800, 2378590980295187, 903406520872185, 559510929662332,
+                322863634303789, 1685429502680940, 1715852907773825, 2521152917532260,
+                781959737898673, 2334258943108700, 2573793300043944, 1273980645866111],
+        "src": "src/core/unittest/UnitTestMubintvec.cpp:402-484 (basic_vector_vector_mod_math_2_limb)"},
     "mk_ring": {"Q": Q_MK, "psi": 100530, "src": "binfhecontext.cpp:157-158 + reference probe, SURVEY.md s0"},
     "cfg5_ring": {"Q": Q50, "psi": 1080667890455, "src": "reference probe at NATIVE_SIZE=64, SURVEY.md s0 item 2"},
 }
@@ -141,6 +180,8 @@ def make_gates():
 def main():
     pyoracle.build()
     json.dump(REFERENCE_KATS, open(os.path.join(HERE, "reference_kats.json"), "w"), indent=1)
+    if "--kats-only" in sys.argv:
+        return
     json.dump(make_gates(), open(os.path.join(HERE, "gates_realkeys.json"), "w"), indent=1)
     json.dump(make_evalacc(), open(os.path.join(HERE, "evalacc_full.json"), "w"), indent=1)
 

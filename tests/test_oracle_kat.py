@@ -65,3 +65,27 @@ def test_root_is_minimal_primitive(oracle):
 def test_digits_g(oracle, logB, expect):
     # mk-cryptoparameters.h:141-142; SURVEY.md Appendix A "digitsG" column
     assert oracle.digits_g(134176769, 1 << logB) == expect
+
+
+def test_next_prime_kat(oracle):
+    # src/core/unittest/UnitTestNbTheory.cpp:380-397 (test_nextQ): q = FirstPrime(22, 2048),
+    # then ten NextPrime(q, 2048) steps (nbtheory-impl.h:361-369)
+    expect = [4208641, 4263937, 4270081, 4274177, 4294657, 4300801, 4304897, 4319233, 4323329, 4360193]
+    q = oracle.first_prime(22, 2048)
+    got = []
+    for _ in range(10):
+        q = oracle.next_prime(q, 2048)
+        got.append(q)
+    assert got == expect
+
+
+@pytest.mark.parametrize("case", ["vec_mod_1limb", "vec_mod_2limb"])
+def test_vector_mod_arithmetic_kat(oracle, case):
+    # src/core/unittest/UnitTestMubintvec.cpp:276-358 (q = 163841) and :402-484
+    # (q = 4057816419532801, 52 bits: the 128-bit product path of the oracle)
+    import json
+    import os
+    from conftest import ROOT
+    kat = json.load(open(os.path.join(ROOT, "tests", "golden", "reference_kats.json")))[case]
+    for op in ("add", "sub", "mul"):
+        assert oracle.vec_mod(op, kat["a"], kat["b"], kat["q"]).tolist() == kat[op], (case, op)
