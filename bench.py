@@ -2,16 +2,29 @@
 """Throughput bench of MK NAND gate bootstrapping on MI355X.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--paramset NAME] [--batch B]
-                    [--stage gate|evalacc]
+                    [--stage gate|evalacc] [--q-bits 50]
 
 A "step" is one pass over a batch of B independent synthetic NAND gates per
 GPU with inputs resident in HBM.  --stage gate (default) runs the whole
 EvalBinGate of the reference -- gate head, BootstrapGateCore (test vector +
 EvalAcc, the blind rotation) and the tail (extraction, ModSwitch, KeySwitch2 /
-KeySwitch); --stage evalacc runs the accumulator alone.  N > 1 runs one process
-per GPU (torch.distributed.run): rank 0 draws the bootstrapping and
-key-switching keys and broadcasts them once over RCCL; gates are sharded by
-rank with no collective on the data path ("weak" scaling: B gates per GPU).
+KeySwitch); --stage evalacc runs the accumulator alone.
+
+Multi-GPU: one process per GPU.  Under torch.distributed.run the ranks come
+from the environment; `--gpus N` without WORLD_SIZE launches the N ranks
+itself (a child torch.distributed.run, before anything touches a GPU).  Rank 0
+draws the bootstrapping keys and broadcasts them once over RCCL; every rank
+uploads them straight from the received device buffer
+(mkacc_upload_keys_device).  Gates are sharded by rank with no collective on
+the data path ("weak" scaling: B gates per GPU).
+
+Proof of the timed run: after timing, every rank copies back the outputs of
+the first G gates of ITS timed batch and recomputes them with the CPU oracle
+(oracle/, the checker) from the same inputs and keys; rank 0 reports
+`parity_checked` / `parity_mismatches` summed over ranks and the run fails on a
+mismatch.  At N = 1 those G gates, one per host core, are also the CPU
+baseline (`cpu_baseline`, kind "port": this repo's restatement of the
+reference path).
 
 Rank 0 prints one JSON line (contract in the task statement); DESIGN.md s4.4
 and s5 give the roofline accounting.
@@ -19,8 +32,11 @@ and s5 give the roofline accounting.
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -35,6 +51,9 @@ METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 PEAK_SHOUP_MULMOD_TPS = 7.744e12     # 27-bit Shoup mod-mul / s, whole chip
 PEAK_HBM_GBS = 8000.0                # MI355X_MICROARCH.md (spec)
 Q50 = 1125899906826241               # config 5 stress modulus
+REF_CPU_S_PER_EVALACC = {            # reference EvalAcc, 1 core of the survey container
+    "STD100_MKNTRU": 0.274, "STD128_MKNTRU": 0.475, "STD100_MKNTRU_LWE": 0.215,
+    "STD100_MKNTRU_LWE_2": 0.721, "STD128_MKNTRU_3": 6.750, "STD100_MKNTRU_3": 2.872}
 
 
 def algorithmic_counts(k: int, n: int, dg: int, nk: int, N: int = 2048, B: int = 1, word: int = 4):
@@ -65,7 +84,7 @@ def measured_traffic(paramset: str):
     return json.load(open(f))["traffic_bytes"]
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
@@ -74,212 +93,353 @@ def parse():
     ap.add_argument("--batch", type=int, default=4096, help="gates per GPU")
     ap.add_argument("--stage", choices=["gate", "evalacc"], default="gate")
     ap.add_argument("--cpu-baseline", type=int, default=1)
-    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: every usable host core")
+    ap.add_argument("--check-gates", type=int, default=0,
+                    help="gates per rank recomputed by the oracle (0: one per host core at N=1, 2 per rank at N>1)")
     ap.add_argument("--q-bits", type=int, default=0, choices=[0, 50],
                     help="50: config 5 stress -- the paramset's shape with the 50-bit Q = 1125899906826241 and "
                          "B_g = 2^10 in 64-bit words (EvalAcc on the 64-bit word path)")
     ap.add_argument("--n-override", type=int, default=0,
                     help="profiling aid: shorten the LWE dimension (fewer accumulator steps); not a bench config")
-    return ap.parse_args()
+    ap.add_argument("--stub-engine", action="store_true",
+                    help="test aid (tests/test_bench_ranks.py): CPU stand-in engine + gloo, to exercise the rank logic")
+    return ap.parse_args(argv)
 
 
-def cpu_baseline(p, threads: int, stage: str, ks):
-    """The oracle restatement (oracle/, 'port') timed on the host cores:
-    `threads` independent gates, one per thread (bounded sample).  For the gate
-    stage the tail is the same contraction the oracle pins (tests/test_gate.py),
-    done in numpy; it is <2% of the gate."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import pyoracle
-    pyoracle.build()
-    method = pyoracle.XZW if p.method == 0 else pyoracle.XZW_B
-    orc = pyoracle.Oracle(method, p.k, p.n, p.N, p.Q, p.q, p.baseG, p.digitsG, p.root)
-    evk = pyoracle.fill_uniform(int(np.prod(orc.evk_shape)), p.Q, 101)
-    pkey = pyoracle.fill_uniform(int(np.prod(orc.pkey_shape)), p.Q, 102)
-    bound = p.q if p.method == 0 else 2 * p.N
-    ct = pyoracle.fill_uniform(threads * p.k * p.n, bound, 103).reshape(threads, p.k, p.n)
-    acc = np.broadcast_to(orc.mntru_testvector(4), (threads, p.k, p.N)).copy()
-    t0 = time.perf_counter()
-    out = orc.evalacc_batch(evk, pkey, ct, acc, threads)
-    if stage == "gate":
-        qKS, baseKS, dks = ks
-        ksk = pyoracle.fill_uniform(p.k * p.N * dks * p.n, qKS, 104).reshape(p.k, p.N * dks, p.n).astype(np.int64)
-        for g in range(threads):
-            ext = orc.extract(out[g])
-            ms = np.vectorize(lambda v: pyoracle.round_qQ(int(v), qKS, p.Q), otypes=[np.int64])(ext)
-            digits = np.stack([(ms // baseKS ** t) % baseKS for t in range(dks)], axis=-1).reshape(p.k, -1)
-            _ = np.stack([(digits[u] @ ksk[u]) % qKS for u in range(p.k)])
-    dt = time.perf_counter() - t0
-    what = "NAND gates (EvalAcc + extraction/ModSwitch/KeySwitch)" if stage == "gate" else "EvalAcc"
-    return {"value": threads / dt, "unit": "bootstraps/s", "cores": threads, "kind": "port",
-            "sample": f"{threads} {what} of {p.n}x{p.k} accumulator steps, one per thread on {threads} threads, "
-                      f"{dt:.2f} s wall, CPU {os.uname().machine} nproc={os.cpu_count()}"}
+# ---- host CPU ----------------------------------------------------------------------
+
+def cpu_info() -> dict:
+    """Usable host cores: the affinity mask, capped by the cgroup CPU quota (the
+    GPU box shows 256 CPUs but grants 16 through cpu.max)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = int(q) / int(period)
+    except (OSError, ValueError):
+        pass
+    usable = max(1, min(aff, int(quota)) if quota else aff)
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"usable": usable, "affinity": aff, "cgroup_quota": quota, "os_cpu_count": os.cpu_count(), "model": model}
 
 
-def main():
-    args = parse()
+# ---- launcher ----------------------------------------------------------------------
+
+def spawn_ranks(args, argv) -> int:
+    """`--gpus N` without a torch.distributed environment: run N ranks as a child
+    torch.distributed.run (no GPU has been touched in this process)."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+# ---- the oracle leg (checker + CPU baseline) ---------------------------------------
+
+class OracleChecker:
+    """Recomputes gates of the timed batch on the host with the CPU oracle
+    (test infrastructure, oracle/): the checker of the run and, at N = 1, the
+    CPU baseline.  Never on the measured path."""
+
+    kind = "port"
+
+    def __init__(self, p, lwe: bool):
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle
+        pyoracle.build()
+        self.po = pyoracle
+        self.p, self.lwe = p, lwe
+        m = pyoracle.XZW_B if p.method != 0 else pyoracle.XZW
+        # MK-LWE's accumulator exponents are already mod 2N (ModSwitch in the head)
+        q = 2 * p.N if lwe else p.q
+        self.orc = pyoracle.Oracle(m, p.k, p.n, p.N, p.Q, q, p.baseG, p.digitsG, p.root)
+
+    def evalacc(self, evk, pkey, ct, acc, threads):
+        return self.orc.evalacc_batch(evk, pkey, ct, acc, threads)
+
+    def gates(self, keys, ksk, inputs, threads, ks):
+        """Full NAND gates (head, EvalAcc, tail) of the gates in `inputs`."""
+        from concurrent.futures import ThreadPoolExecutor
+        po, orc, p = self.po, self.orc, self.p
+        qKS, baseKS, n_out = ks
+        evk, pkey = keys
+        G = inputs["a1"].shape[0]
+        if self.lwe:
+            heads = [orc.mklwe_head(inputs["a1"][g], inputs["b1"][g], inputs["a2"][g], inputs["b2"][g], p.q)
+                     for g in range(G)]
+            ct = np.stack([h[0] for h in heads])
+            acc0 = np.stack([h[1] for h in heads])
+        else:
+            ct = np.stack([po.mntru_head(inputs["nand"], inputs["a1"][g], inputs["a2"][g], p.q) for g in range(G)])
+            acc0 = np.broadcast_to(orc.mntru_testvector(4), (G, p.k, p.N)).copy()
+        acc = orc.evalacc_batch(evk, pkey, ct, acc0, threads)
+        if self.lwe:
+            A, Bk = ksk
+            tail = lambda g: orc.mklwe_tail(acc[g], A, Bk, qKS, baseKS, n_out)   # noqa: E731
+        else:
+            tail = lambda g: orc.mntru_tail_ksk1(acc[g], ksk, qKS, baseKS, n_out)   # noqa: E731
+        with ThreadPoolExecutor(max(1, threads)) as ex:   # ctypes releases the GIL
+            outs = list(ex.map(tail, range(G)))
+        if self.lwe:
+            return np.stack([o[0] for o in outs]), np.array([o[1] for o in outs], dtype=np.uint64)
+        return np.stack(outs), None
+
+
+# ---- one rank ----------------------------------------------------------------------
+
+def run_rank(args, env: dict, make_engine, make_checker, torch_device: str, backend: str) -> dict | None:
+    """Bench logic of one rank: key broadcast + device upload, this rank's shard
+    of synthetic gates, warmup, barrier-bracketed timing of K steps, max over
+    ranks, the oracle check of the first G gates of the timed batch, and (rank 0)
+    the JSON result.  make_engine / make_checker / torch_device / backend are
+    the only things tests/test_bench_ranks.py replaces (CPU stand-ins, gloo)."""
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local)
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world)
-    dev = f"cuda:{local}"
-
-    import mkfhe_amd as mk
     from mkfhe_amd import shard
 
-    p = mk.paramset(args.paramset)
-    if args.n_override:
-        p.n = args.n_override
-    if args.q_bits == 50:   # SURVEY.md s8 config 5 stress (s6: reference CPU 0.568 s / EvalAcc at k=2, n=560)
-        p.Q, p.baseG, p.digitsG, p.root = Q50, 1 << 10, 0, 0
-        args.stage = "evalacc"   # the 64-bit word path covers the accumulator
-    eng = mk.MKAccumulatorEngine(p, device=local)
+    world, rank = int(env.get("WORLD_SIZE", 1)), int(env.get("RANK", 0))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if world > 1:
+        dist.init_process_group(backend, rank=rank, world_size=world, timeout=datetime.timedelta(minutes=10))
+    is_cuda = torch_device.startswith("cuda")
+
+    def sync_dev():
+        if is_cuda:
+            torch.cuda.synchronize()
+
+    eng = make_engine()
     p = eng.params
     wide = eng.wide
     word = 8 if p.Q > (1 << 32) else 4
     B = args.batch
-    lwe = p.method != mk.MKNTRU
-    qKS, baseKS = p.q, 32                     # modKS = mod and baseKS = 32 in every MK set (binfhecontext.cpp:129-144)
+    lwe = p.method != 0
+    stage = "evalacc" if wide else args.stage
+    qKS, baseKS, n_out = p.q, 32, p.n          # modKS = mod, baseKS = 32 in every MK set (binfhecontext.cpp:129-144)
     dks = int(np.ceil(np.log(qKS) / np.log(baseKS)))
 
-    # ---- keys: drawn on rank 0, broadcast once over RCCL (xGMI) ----
-    evk_n = int(np.prod(eng.evk_shape))
-    pkey_n = int(np.prod(eng.pkey_shape))
-    keys = shard.broadcast_keys(evk_n + pkey_n, p.Q, seed=12345, device=dev)
-    keys_h = keys.cpu().numpy().view(np.uint64 if word == 8 else np.uint32)
-    eng.upload_keys(keys_h[:evk_n], keys_h[evk_n:])
-    del keys, keys_h
-    if args.stage == "gate":
+    # ---- keys: drawn on rank 0, broadcast once (RCCL over xGMI), uploaded from the device buffer ----
+    evk_n, pkey_n = int(np.prod(eng.evk_shape)), int(np.prod(eng.pkey_shape))
+    keys = shard.broadcast_keys(evk_n + pkey_n, p.Q, seed=12345, device=torch_device)
+    eng.upload_keys_device(keys[:evk_n], keys[evk_n:])
+    ksk = None
+    if stage == "gate":
         if lwe:
-            na = p.k * p.N * baseKS * dks * p.n
-            nb = p.k * p.N * baseKS * dks
-            ksk = shard.broadcast_keys(na + nb, qKS, seed=23456, device=dev).cpu().numpy().view(np.uint32)
-            eng.upload_ksk_mklwe(ksk[:na], ksk[na:], qKS, baseKS, p.n)
+            na, nb = p.k * p.N * baseKS * dks * n_out, p.k * p.N * baseKS * dks
+            t = shard.broadcast_keys(na + nb, qKS, seed=23456, device=torch_device).cpu().numpy().view(np.uint32)
+            ksk = (t[:na], t[na:])
+            eng.upload_ksk_mklwe(ksk[0], ksk[1], qKS, baseKS, n_out)
         else:
-            nk = p.k * p.N * dks * p.n
-            ksk = shard.broadcast_keys(nk, qKS, seed=23456, device=dev).cpu().numpy().view(np.uint32)
-            eng.upload_ksk_mntru(ksk, qKS, baseKS, p.n)
-        del ksk
+            ksk = shard.broadcast_keys(p.k * p.N * dks * n_out, qKS, seed=23456,
+                                       device=torch_device).cpu().numpy().view(np.uint32)
+            eng.upload_ksk_mntru(ksk, qKS, baseKS, n_out)
 
-    # ---- this rank's shard of synthetic gates, resident in HBM ----
+    # ---- this rank's shard of synthetic gates, resident in device memory ----
     rng = np.random.Generator(np.random.PCG64(1000 + rank))
 
-    def dev_u32(a):
+    def dev_words(a):
+        a = np.ascontiguousarray(a)
         if a.dtype == np.uint64:
-            return torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(dev)
-        return torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint32).view(np.int32)).to(dev)
+            return torch.from_numpy(a.view(np.int64)).to(torch_device)
+        return torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint32).view(np.int32)).to(torch_device)
 
-    stream = torch.cuda.ExternalStream(eng.stream_handle())
-    if args.stage == "gate":
-        kn = p.k * p.n
-        d_a1 = dev_u32(rng.integers(0, p.q, size=(B, kn)))
-        d_a2 = dev_u32(rng.integers(0, p.q, size=(B, kn)))
-        d_nand = dev_u32(rng.integers(0, p.q, size=kn))
-        d_b1 = dev_u32(rng.integers(0, p.q, size=B)) if lwe else None
-        d_b2 = dev_u32(rng.integers(0, p.q, size=B)) if lwe else None
-        d_oa = torch.empty((B, p.k * p.n), dtype=torch.int32, device=dev)
-        d_ob = torch.empty(B, dtype=torch.int32, device=dev) if lwe else None
+    kn = p.k * p.n
+    if stage == "gate":
+        h = {"a1": rng.integers(0, p.q, size=(B, p.k, p.n), dtype=np.uint32),
+             "a2": rng.integers(0, p.q, size=(B, p.k, p.n), dtype=np.uint32),
+             "nand": rng.integers(0, p.q, size=(p.k, p.n), dtype=np.uint32)}
+        if lwe:
+            h["b1"] = rng.integers(0, p.q, size=B, dtype=np.uint32)
+            h["b2"] = rng.integers(0, p.q, size=B, dtype=np.uint32)
+        d = {key: dev_words(v) for key, v in h.items()}
+        d_oa = torch.empty((B, p.k, n_out), dtype=torch.int32, device=torch_device)
+        d_ob = torch.empty(B, dtype=torch.int32, device=torch_device) if lwe else None
 
         def run_step():
-            eng.eval_nand_device(d_nand, d_a1, d_b1, d_a2, d_b2, d_oa, d_ob, B)
+            eng.eval_nand_device(d["nand"], d["a1"], d.get("b1"), d["a2"], d.get("b2"), d_oa, d_ob, B)
     else:
         ct_h, acc_h = shard.synthetic_gates(eng, B, seed=1000 + rank)
-        d_ct, d_in = dev_u32(ct_h), dev_u32(acc_h)
+        d_ct, d_in = dev_words(ct_h), dev_words(acc_h)
         d_out = torch.empty_like(d_in)
 
         def run_step():
             eng.eval_batch_device(d_ct, d_in, d_out, B)
 
+    # ---- timed region: barrier + sync on both sides, max over ranks ----
     for _ in range(args.warmup):
         run_step()
     eng.sync()
-    torch.cuda.synchronize()
+    sync_dev()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync_dev()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         run_step()
-    eng.sync()
-    torch.cuda.synchronize()
+    eng.sync()          # also raises on a device-side input-range error
+    sync_dev()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync_dev()
     wall = time.perf_counter() - t0
-    elapsed = torch.tensor([wall], dtype=torch.float64, device=dev)
+    elapsed = torch.tensor([wall], dtype=torch.float64, device=torch_device)
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     T = float(elapsed.item())
 
-    # output sanity: residues stay canonical
-    if args.stage == "gate":
-        assert int(d_oa.max().item()) < qKS and int(d_oa.min().item()) >= 0
-    else:
-        hi = d_out.view(torch.int64) if word == 8 else d_out
-        assert int(hi.max().item()) < p.Q and int(hi.min().item()) >= 0
-
-    # ---- dominant kernel (the accumulator step) timed live with HIP events on
+    # ---- dominant kernel (the accumulator step), timed live with HIP events on
     # the engine stream: one EvalAcc pass = k*n step launches (+2 tiny kernels)
-    ct_h, acc_h = shard.synthetic_gates(eng, B, seed=2000 + rank)
-    d_ct, d_in = dev_u32(ct_h), dev_u32(acc_h)
-    d_out = torch.empty_like(d_in)
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    ev0.record(stream)
-    eng.eval_batch_device(d_ct, d_in, d_out, B)
-    ev1.record(stream)
-    eng.sync()
-    kn_steps = p.k * p.n
-    per_launch_s = ev0.elapsed_time(ev1) / 1e3 / kn_steps
+    per_launch_s = None
+    if is_cuda:
+        ct2, acc2 = shard.synthetic_gates(eng, B, seed=2000 + rank)
+        e_ct, e_in = dev_words(ct2), dev_words(acc2)
+        e_out = torch.empty_like(e_in)
+        stream = torch.cuda.ExternalStream(eng.stream_handle())
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record(stream)
+        eng.eval_batch_device(e_ct, e_in, e_out, B)
+        ev1.record(stream)
+        eng.sync()
+        per_launch_s = ev0.elapsed_time(ev1) / 1e3 / (p.k * p.n)
+        del e_ct, e_in, e_out
 
-    dg = p.digitsG - 1
-    nk = 1 if lwe else 2
-    mm, by = algorithmic_counts(p.k, p.n, dg, nk, p.N, B, word)
-    stage_txt = ("NAND gates: head + BootstrapGateCore (EvalAcc) + extraction/ModSwitch/"
-                 f"{'KeySwitch' if lwe else 'KeySwitch2'}") if args.stage == "gate" else "EvalAcc (blind rotation) only"
-    result = {
-        "metric": METRIC,
-        "value": world * B * args.steps / T,
-        "unit": "bootstraps/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": 1e3 * T / args.steps,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "u64 (50-bit residues mod Q)" if word == 8 else "u32 (27-bit residues mod Q)",
-        "data": "synthetic: uniform keys, key-switching keys and ciphertexts (seeded)",
-        "config": {"workload": f"{args.paramset} {p.k}-party {'MK-LWE' if lwe else 'MK-NTRU'} {stage_txt} "
-                               f"(k={p.k}, n={p.n}, N={p.N}, dg={dg}"
-                               + (f", Q={p.Q} in 64-bit words, B_g=2^{p.baseG.bit_length() - 1})" if wide else ")"),
-                   "paramset": args.paramset, "stage": args.stage, "batch_per_gpu": B, "global_batch": world * B,
-                   "parallelism": f"gate-sharded x{world}"},
-        "roofline": {"bound": "hbm", "achieved": by / per_launch_s / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                     "frac": by / per_launch_s / 1e9 / PEAK_HBM_GBS,
-                     "traffic": measured_traffic(args.paramset) if not (args.n_override or wide) else None,
-                     "kernel": "wide::step_kernel" if wide else "mk_step_kernel",
-                     "per_launch_us": per_launch_s * 1e6,
-                     "bytes_per_launch": by},
-        # the VALU peak is the measured 32-bit Shoup rate: not a bound for 64-bit words
-        "roofline_valu": None if wide else {
-            "bound": "valu-int", "achieved": mm / per_launch_s / 1e12, "peak": PEAK_SHOUP_MULMOD_TPS / 1e12,
-            "unit": "T mod-mul/s", "frac": mm / per_launch_s / PEAK_SHOUP_MULMOD_TPS, "mulmods_per_launch": mm},
-    }
-    if rank == 0 and world == 1 and args.cpu_baseline:
-        thr = args.cpu_threads or min(16, os.cpu_count() or 1)
-        result["cpu_baseline"] = cpu_baseline(p, thr, args.stage, (qKS, baseKS, dks))
+    # ---- proof: the first G gates of this rank's timed batch against the oracle ----
+    cpu = cpu_info()
+    G = args.check_gates or (cpu["usable"] if world == 1 else 2)
+    G = max(1, min(G, B))
+    threads = args.cpu_threads or (cpu["usable"] if world == 1 else max(1, min(G, cpu["usable"] // world)))
+    chk = make_checker(p, lwe)
+    keys_h = keys.cpu().numpy().view(np.uint64 if word == 8 else np.uint32)
+    evk_h = keys_h[:evk_n].astype(np.uint64).reshape(eng.evk_shape)
+    pkey_h = keys_h[evk_n:].astype(np.uint64).reshape(eng.pkey_shape)
+    del keys
+    t_c = time.perf_counter()
+    if stage == "gate":
+        sub = {key: (v[:G] if key != "nand" else v) for key, v in h.items()}
+        ksk64 = (tuple(x.astype(np.uint64) for x in ksk) if lwe else ksk)
+        exp_a, exp_b = chk.gates((evk_h, pkey_h), ksk64, sub, threads, (qKS, baseKS, n_out))
+        dt_c = time.perf_counter() - t_c
+        got_a = d_oa[:G].cpu().numpy().view(np.uint32).astype(np.uint64)
+        bad = np.any((got_a != exp_a.reshape(got_a.shape)).reshape(G, -1), axis=1)
+        if lwe:
+            bad |= d_ob[:G].cpu().numpy().view(np.uint32).astype(np.uint64) != exp_b
+    else:
+        exp = chk.evalacc(evk_h, pkey_h, ct_h[:G].astype(np.uint64), acc_h[:G].astype(np.uint64), threads)
+        dt_c = time.perf_counter() - t_c
+        got = d_out[:G].cpu().numpy().view(np.uint64 if word == 8 else np.uint32).astype(np.uint64)
+        bad = np.any((got != exp).reshape(G, -1), axis=1)
+    counts = torch.tensor([G, int(bad.sum())], dtype=torch.int64, device=torch_device)
+    if world > 1:
+        dist.all_reduce(counts, op=dist.ReduceOp.SUM)
+    checked, mismatches = int(counts[0].item()), int(counts[1].item())
+
+    result = None
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        dg = p.digitsG - 1
+        nk = 1 if lwe else 2
+        mm, by = algorithmic_counts(p.k, p.n, dg, nk, p.N, B, word)
+        stage_txt = ("NAND gates: head + BootstrapGateCore (EvalAcc) + extraction/ModSwitch/"
+                     f"{'KeySwitch' if lwe else 'KeySwitch2'}") if stage == "gate" else "EvalAcc (blind rotation) only"
+        pl = per_launch_s or float("nan")
+        result = {
+            "metric": METRIC,
+            "value": world * B * args.steps / T,
+            "unit": "bootstraps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * T / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64 (50-bit residues mod Q)" if word == 8 else "u32 (27-bit residues mod Q)",
+            "data": "synthetic: uniform keys, key-switching keys and ciphertexts (seeded)",
+            "config": {"workload": f"{args.paramset} {p.k}-party {'MK-LWE' if lwe else 'MK-NTRU'} {stage_txt} "
+                                   f"(k={p.k}, n={p.n}, N={p.N}, dg={dg}"
+                                   + (f", Q={p.Q} in 64-bit words, B_g=2^{p.baseG.bit_length() - 1})" if wide else ")"),
+                       "paramset": args.paramset, "stage": stage, "batch_per_gpu": B, "global_batch": world * B,
+                       "parallelism": f"gate-sharded x{world}"},
+            "parity_checked": checked,
+            "parity_mismatches": mismatches,
+            "parity": (f"first {G} gates of every rank's timed batch recomputed by the CPU oracle (oracle/, "
+                       "bit-exact integer compare of every output word); the oracle's primitives are pinned by the "
+                       "reference's KATs, the EvalAcc composition is 'parity unpinned' beyond them (DESIGN.md s3)"),
+            "roofline": {"bound": "hbm", "achieved": by / pl / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": by / pl / 1e9 / PEAK_HBM_GBS,
+                         "traffic": measured_traffic(args.paramset) if not (args.n_override or wide) else None,
+                         "kernel": "wide::step_kernel" if wide else "mk_step_kernel",
+                         "per_launch_us": pl * 1e6,
+                         "bytes_per_launch": by},
+            # the VALU peak is the measured 32-bit Shoup rate: not a bound for 64-bit words
+            "roofline_valu": None if wide else {
+                "bound": "valu-int", "achieved": mm / pl / 1e12, "peak": PEAK_SHOUP_MULMOD_TPS / 1e12,
+                "unit": "T mod-mul/s", "frac": mm / pl / PEAK_SHOUP_MULMOD_TPS, "mulmods_per_launch": mm},
+        }
+        if world == 1 and args.cpu_baseline:
+            what = ("NAND gates (head + EvalAcc + extraction/ModSwitch/key switch)" if stage == "gate"
+                    else "EvalAccs")
+            ref = REF_CPU_S_PER_EVALACC.get(args.paramset) if not (wide or args.n_override) else None
+            result["cpu_baseline"] = {
+                "value": G / dt_c, "unit": "bootstraps/s", "cores": threads, "kind": chk.kind,
+                "sample": (f"the first {G} {what} of the timed batch ({p.k}x{p.n} accumulator steps each), one per "
+                           f"thread on {threads} threads, {dt_c:.2f} s wall; the same gates are the parity check"),
+                "host": cpu,
+                "reference_1core_s_per_evalacc": ref,
+                "reference_source": "SURVEY.md s6: the reference's own EvalAcc, 1 thread of the survey container",
+            }
     if world > 1:
         dist.destroy_process_group()
+    if mismatches:
+        if rank == 0:
+            print(json.dumps(result), flush=True)
+        raise SystemExit(f"parity FAILED: {mismatches} of {checked} checked gates differ from the oracle")
+    return result
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args, argv))
+    env = dict(os.environ)
+    local = int(env.get("LOCAL_RANK", "0"))
+
+    if args.stub_engine:   # CPU rehearsal of the rank logic (tests/test_bench_ranks.py)
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import bench_stub
+        res = run_rank(args, env, lambda: bench_stub.StubEngine(args), bench_stub.StubChecker, "cpu", "gloo")
+    else:
+        import torch
+        import mkfhe_amd as mk
+
+        torch.cuda.set_device(local)
+
+        def make_engine():
+            p = mk.paramset(args.paramset)
+            if args.n_override:
+                p.n = args.n_override
+            if args.q_bits == 50:   # SURVEY.md s8 config 5 stress (s6: reference CPU 0.568 s / EvalAcc at k=2, n=560)
+                p.Q, p.baseG, p.digitsG, p.root = Q50, 1 << 10, 0, 0
+            return mk.MKAccumulatorEngine(p, device=local)
+
+        res = run_rank(args, env, make_engine, OracleChecker, f"cuda:{local}", "nccl")
+    if res is not None:
+        print(json.dumps(res), flush=True)
 
 
 if __name__ == "__main__":

@@ -12,7 +12,7 @@
  * its device buffers and one HIP stream (calls on one context are serialised).
  * Every function returns MKACC_OK (0) or a negative MKACC_E* status; the text
  * of the last error on the calling thread is available from mkacc_last_error().
- * The C++ host layer (mkfhe_amd/csrc/host/) converts a status into the
+ * The C++ host layer (include/mkfhe_amd_binfhe.hpp) converts a status into the
  * reference's exception types (OPENFHE_THROW config_error / math_error,
  * reference src/core/include/utils/exception.h:162).
  *
@@ -90,6 +90,11 @@ size_t mkacc_pkey_words(const mkacc_ctx* ctx);  /* k * (digitsG-1) * N */
  */
 int mkacc_upload_keys(mkacc_ctx* ctx, const uint32_t* evk, const uint32_t* pkey);
 int mkacc_upload_keys_u64(mkacc_ctx* ctx, const uint64_t* evk, const uint64_t* pkey);
+/* Same from DEVICE memory on the context's device (word_bytes 4 or 8), e.g. the
+ * buffer a multi-GPU run received from the one-time key broadcast: the layout
+ * conversion runs on the GPU, keys never return to the host.  Synchronous;
+ * MKACC_E_RANGE (and no keys) if a word is not a canonical residue. */
+int mkacc_upload_keys_device(mkacc_ctx* ctx, const void* d_evk, const void* d_pkey, uint32_t word_bytes);
 
 /*
  * EvalAcc over a batch of B independent gates (host buffers, synchronous).
@@ -110,10 +115,13 @@ int mkacc_is_wide(const mkacc_ctx* ctx);
 
 /* Same with DEVICE pointers on the context's device; enqueued on the context
  * stream and returns without waiting (use mkacc_sync).  Used by bench.py so
- * the timed region starts with inputs resident in HBM. */
+ * the timed region starts with inputs resident in HBM.  Input words are
+ * range-checked by the kernels that read them; a violation is reported by the
+ * next mkacc_sync (MKACC_E_RANGE), and the outputs of that batch are garbage
+ * (never an out-of-bounds access: monomial exponents are masked to [0, 2N)). */
 int mkacc_eval_batch_device(mkacc_ctx* ctx, const uint32_t* d_ct, const uint32_t* d_acc_in,
                             uint32_t* d_acc_out, size_t B);
-int mkacc_sync(mkacc_ctx* ctx);
+int mkacc_sync(mkacc_ctx* ctx);   /* waits for the stream; reports device-side input-range errors */
 
 /* The context's HIP stream (hipStream_t as void*), for event timing. */
 void* mkacc_stream(mkacc_ctx* ctx);

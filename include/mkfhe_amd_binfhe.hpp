@@ -205,8 +205,11 @@ public:
     DeviceContext& operator=(const DeviceContext&) = delete;
     mkacc_ctx* get() const { return m_ctx; }
     const mkacc_params& params() const { return m_p; }
-    const void* key_token = nullptr;
-    const void* pkey_token = nullptr;
+    // What is on the device: the key OBJECT itself is held (so its address
+    // cannot be recycled for another key while it is cached) and Pkey by value
+    // (it is passed by value, and is only k*dg*N words).
+    std::shared_ptr<const UniEncACCKeyImpl> key_ref;
+    std::vector<uint32_t> pkey_words;
 
 private:
     mkacc_ctx* m_ctx = nullptr;
@@ -315,14 +318,21 @@ private:
 
 public:
     // Flatten ek [k][nk][n+1] x [dg][2] x N and Pkey [k][dg] x N into the C-ABI
-    // layout and upload them once per key object.
+    // layout and upload them once per key object and Pkey content.
     static void upload(DeviceContext& dc, ConstUniEncACCKey& ek, const std::vector<std::vector<NativePoly>>& Pkey) {
-        if (dc.key_token == ek.get() && dc.pkey_token == (const void*)Pkey.data()) return;
         const mkacc_params& p = dc.params();
         const uint32_t dg = p.digitsG - 1, nk = p.method == MKACC_METHOD_MKNTRU ? 2 : 1, N = p.N;
+        if (Pkey.size() != p.k) throw config_error("Pkey must have k parties");
+        std::vector<uint32_t> pk(mkacc_pkey_words(dc.get()));
+        for (uint32_t u = 0; u < p.k; ++u) {
+            if (Pkey[u].size() != dg) throw config_error("Pkey must have digitsG-1 polys per party");
+            for (uint32_t d = 0; d < dg; ++d)
+                for (uint32_t s = 0; s < N; ++s) pk[((size_t)u * dg + d) * N + s] = (uint32_t)Pkey[u][d][s];
+        }
+        if (dc.key_ref == ek && dc.pkey_words == pk) return;   // keys already on the device
         const auto& K = ek->GetElements();
         if (K.size() != p.k) throw config_error("accumulator key must have k parties");
-        std::vector<uint32_t> evk(mkacc_evk_words(dc.get())), pk(mkacc_pkey_words(dc.get()));
+        std::vector<uint32_t> evk(mkacc_evk_words(dc.get()));
         size_t o = 0;
         for (uint32_t u = 0; u < p.k; ++u) {
             if (K[u].size() < nk) throw config_error("accumulator key has too few key sets");
@@ -337,15 +347,10 @@ public:
                 }
             }
         }
-        if (Pkey.size() != p.k) throw config_error("Pkey must have k parties");
-        for (uint32_t u = 0; u < p.k; ++u) {
-            if (Pkey[u].size() != dg) throw config_error("Pkey must have digitsG-1 polys per party");
-            for (uint32_t d = 0; d < dg; ++d)
-                for (uint32_t s = 0; s < N; ++s) pk[((size_t)u * dg + d) * N + s] = (uint32_t)Pkey[u][d][s];
-        }
+        dc.key_ref.reset();
         check(mkacc_upload_keys(dc.get(), evk.data(), pk.data()));
-        dc.key_token = ek.get();
-        dc.pkey_token = Pkey.data();
+        dc.key_ref = ek;
+        dc.pkey_words = std::move(pk);
     }
 
 private:
@@ -937,6 +942,11 @@ private:
     void need_gate(BINGATE gate, BINFHE_METHOD family) const {
         need_context();
         if (gate != NAND) throw not_implemented_error("only NAND is supported (ctGateGen, binfhe-base-scheme.cpp:341-342)");
+        // the reference's MKNTRU_B gate feeds mod-q MNTRU words to XZW_B as monomial
+        // exponents (binfhecontext.cpp:174, binfhe-base-scheme.cpp:1127,
+        // mk-acc-xzw_B.cpp:120,290): an out-of-range GetMonomial, i.e. undefined
+        if (m_method == MKNTRU_B)
+            throw config_error("MKNTRU_B NAND gates are undefined in the reference; use MKNTRU or MKNTRU_LWE");
         const bool lwe = m_method != MKNTRU;
         if (lwe != (family != MKNTRU)) throw config_error("ciphertext type does not match the context method");
         if (!m_keys)

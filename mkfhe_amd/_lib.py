@@ -63,6 +63,7 @@ SIGNATURES = {
     "mkacc_pkey_words": (ctypes.c_size_t, [ctypes.c_void_p]),
     "mkacc_upload_keys": (ctypes.c_int, [ctypes.c_void_p, _u32p, _u32p]),
     "mkacc_upload_keys_u64": (ctypes.c_int, [ctypes.c_void_p, _u64p, _u64p]),
+    "mkacc_upload_keys_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]),
     "mkacc_eval_batch": (ctypes.c_int, [ctypes.c_void_p, _u32p, _u32p, _u32p, ctypes.c_size_t]),
     "mkacc_eval_batch_u64": (ctypes.c_int, [ctypes.c_void_p, _u32p, _u64p, _u64p, ctypes.c_size_t]),
     "mkacc_is_wide": (ctypes.c_int, [ctypes.c_void_p]),

@@ -59,6 +59,17 @@ def _u32(a: np.ndarray):
     return a.ctypes.data_as(_u32p)
 
 
+def _fingerprint(*arrays) -> int:
+    """Cheap content check of key arrays: shape, dtype and ~4096 strided words each."""
+    h = 0
+    for a in arrays:
+        a = np.asarray(a)
+        flat = a.reshape(-1)
+        step = max(1, flat.size // 4096)
+        h = hash((h, a.shape, a.dtype.str, flat[::step].tobytes()))
+    return h
+
+
 class MKAccumulatorEngine:
     """One device context (mkacc_ctx) with its uploaded keys."""
 
@@ -75,7 +86,7 @@ class MKAccumulatorEngine:
         self.dg = eff.digitsG - 1
         self.nk = 2 if eff.method == MKNTRU else 1
         self.device = device
-        self._key_token = None
+        self._keys_ref = None   # (evk, pkey, fingerprint) of the arrays on the device
         self.ks = None
 
     def close(self):
@@ -111,7 +122,25 @@ class MKAccumulatorEngine:
             e = np.ascontiguousarray(evk, dtype=np.uint32)
             p = np.ascontiguousarray(pkey, dtype=np.uint32)
             check(L.mkacc_upload_keys(self._h, _u32(e), _u32(p)))
-        self._key_token = (id(evk), id(pkey))
+        self._keys_ref = (evk, pkey, _fingerprint(evk, pkey))
+
+    def holds_keys(self, evk, pkey) -> bool:
+        """True if exactly these arrays (same objects, same sampled content) are on the device."""
+        r = self._keys_ref
+        return r is not None and r[0] is evk and r[1] is pkey and r[2] == _fingerprint(evk, pkey)
+
+    def upload_keys_device(self, d_evk, d_pkey):
+        """Keys from device memory (torch tensors or ints on this context's device) in
+        the reference layout; the layout conversion runs on the GPU (no host copy)."""
+        def ptr(t):
+            return ctypes.c_void_p(t if isinstance(t, int) else t.data_ptr())
+        wb = 8 if self.Q >= (1 << 32) else 4
+        if not isinstance(d_evk, int):
+            wb = d_evk.element_size()
+            if d_evk.numel() != int(np.prod(self.evk_shape)) or d_pkey.numel() != int(np.prod(self.pkey_shape)):
+                raise MkaccError(_lib.MKACC_E_ARG, "key arrays have the wrong size")
+        check(_lib.load().mkacc_upload_keys_device(self._h, ptr(d_evk), ptr(d_pkey), wb))
+        self._keys_ref = None
 
     # -- evaluation -------------------------------------------------------------
     @property
@@ -252,10 +281,11 @@ class UniEncAccumulator:
         self.engine = MKAccumulatorEngine(params, device)
 
     def _ensure_keys(self, ek, Pkey):
-        token = (id(ek), id(Pkey))
-        if self.engine._key_token != token:
+        # the engine keeps references to the uploaded arrays, so an identity hit
+        # cannot be a recycled id(); the sampled fingerprint catches in-place edits
+        if not self.engine.holds_keys(ek, Pkey):
             self.engine.upload_keys(np.asarray(ek), np.asarray(Pkey))
-            self.engine._key_token = token
+            self.engine._keys_ref = (ek, Pkey, _fingerprint(ek, Pkey))
 
     def EvalAcc(self, ek, Pkey, skf, acc: np.ndarray, ct) -> None:
         """EvalAcc(params, ek, Pkey, skf, acc, ct): acc [k][N] EVAL updated in place.

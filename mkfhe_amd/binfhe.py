@@ -143,6 +143,11 @@ class BinFHEContext:
             raise NotImplementedError("only NAND is supported (ctGateGen, binfhe-base-scheme.cpp:341-342)")
         if ct1 is ct2:
             raise ConfigError("Input ciphertexts should be independant")
+        if self.method == MKNTRU_B:
+            # the reference hands mod-q MNTRU words to XZW_B as monomial exponents
+            # (binfhecontext.cpp:174, binfhe-base-scheme.cpp:1127, mk-acc-xzw_B.cpp:120,290):
+            # an out-of-range GetMonomial, i.e. undefined behaviour -- rejected here
+            raise ConfigError("MKNTRU_B NAND gates are undefined in the reference; use MKNTRU or MKNTRU_LWE")
         if self.BTKey is None:
             raise ConfigError("Bootstrapping keys have not been generated. Please call MKBTKeyGen before calling "
                               "bootstrapping.")

@@ -556,12 +556,16 @@ __device__ __forceinline__ void step_body(const StepCtx& s, uint32_t k, uint32_t
 
 // c = floor(ct * 2N / q) (mk-acc-xzw.cpp:110,125) or c = ct (mk-acc-xzw_B.cpp:119,124),
 // with c == 2N mapped to 0 (xzw.cpp:301).  Output layout [k*n][B].
+// Device entry points validate their inputs where a kernel reads them anyway:
+// a word outside its range raises the context's `bad` flag (reported by
+// mkacc_sync as MKACC_E_RANGE); the monomial exponent stays masked to [0, 2N).
 __global__ void prep_c_kernel(const uint32_t* __restrict__ ct, uint32_t* __restrict__ cvals, uint32_t B,
-                              uint32_t kn, uint32_t method, uint32_t q) {
+                              uint32_t kn, uint32_t method, uint32_t q, uint32_t* __restrict__ bad) {
     const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= (size_t)B * kn) return;
     const uint32_t s = (uint32_t)(idx / B), b = (uint32_t)(idx % B);
     const uint32_t raw = ct[(size_t)b * kn + s];
+    if (raw >= (method == XZW ? q : 2u * kN + 1u)) *bad = 1u;   // XZW_B: c <= 2N (2N -> 0)
     uint32_t c = method == XZW ? (uint32_t)(((uint64_t)raw * (2u * kN)) / q) : raw;
     if (c >= 2u * kN) c -= 2u * kN;
     cvals[idx] = c;
@@ -569,12 +573,35 @@ __global__ void prep_c_kernel(const uint32_t* __restrict__ ct, uint32_t* __restr
 
 // reference EVAL order -> C4, multiplied by a constant (N^-1 on the way in, N on the way out)
 __global__ void eval_to_c4_kernel(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, size_t npoly,
-                                  uint32_t s, uint32_t sp, uint32_t Q) {
+                                  uint32_t s, uint32_t sp, uint32_t Q, uint32_t* __restrict__ bad) {
     const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= npoly * kN) return;
     const size_t p = idx / kN;
     const uint32_t j = (uint32_t)(idx % kN);
-    out[p * kN + c4_index(j)] = mul_shoup(in[idx], s, sp, Q);
+    const uint32_t x = in[idx];
+    if (bad && x >= Q) *bad = 1u;
+    out[p * kN + c4_index(j)] = mul_shoup(x, s, sp, Q);
+}
+
+// Key upload from device memory: reference layout [k][nk][n+1][dg][2][N] (EVAL,
+// u32 or u64 words) -> device layout [k][n+1][nk][dg][2][N] in C4 order, times
+// N^-1 (s, sp).  pkey [k][dg][N] is the same map with nk = n1 = 1.
+template <typename W>
+__global__ void key_layout_kernel(const W* __restrict__ src, uint32_t* __restrict__ dst, size_t npolys, uint32_t nk,
+                                  uint32_t n1, uint32_t dg2, uint32_t Q, uint32_t s, uint32_t sp,
+                                  uint32_t* __restrict__ bad) {
+    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= npolys * kN) return;
+    size_t p = idx / kN;
+    const uint32_t j = (uint32_t)(idx % kN);
+    const uint32_t dp = (uint32_t)(p % dg2); p /= dg2;
+    const uint32_t i = (uint32_t)(p % n1); p /= n1;
+    const uint32_t jj = (uint32_t)(p % nk);
+    const size_t u = p / nk;
+    const size_t dpoly = ((u * n1 + i) * nk + jj) * dg2 + dp;
+    const uint64_t x = (uint64_t)src[idx];
+    if (x >= Q) *bad = 1u;
+    dst[dpoly * kN + c4_index(j)] = mul_shoup((uint32_t)x, s, sp, Q);
 }
 __global__ void c4_to_eval_kernel(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, size_t npoly,
                                   uint32_t s, uint32_t sp, uint32_t Q) {
@@ -658,6 +685,27 @@ StepFn step_fn(int dg, int method, bool first);
 
 namespace {
 
+// Device key upload for the 64-bit word path: reference layout -> [k][n+1][nk][dg][2][N]
+// (EVAL order), each word in Montgomery form K * 2^64 mod Q (r, rp: 2^64 mod Q and its
+// Shoup companion).
+template <typename W>
+__global__ void wide_key_layout_kernel(const W* __restrict__ src, uint64_t* __restrict__ dst, size_t npolys,
+                                       uint32_t nk, uint32_t n1, uint32_t dg2, uint64_t Q, uint64_t r, uint64_t rp,
+                                       uint32_t* __restrict__ bad) {
+    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= npolys * kN) return;
+    size_t p = idx / kN;
+    const uint32_t j = (uint32_t)(idx % kN);
+    const uint32_t dp = (uint32_t)(p % dg2); p /= dg2;
+    const uint32_t i = (uint32_t)(p % n1); p /= n1;
+    const uint32_t jj = (uint32_t)(p % nk);
+    const size_t u = p / nk;
+    const size_t dpoly = ((u * n1 + i) * nk + jj) * dg2 + dp;
+    const uint64_t x = (uint64_t)src[idx];
+    if (x >= Q) *bad = 1u;
+    dst[dpoly * kN + j] = wide::mul_shoup(x, r, rp, Q);
+}
+
 StepFn step_fn(int dg, int method, bool first) {
     switch (dg) {
         case 2: return pick_step<2>(method, first);
@@ -708,8 +756,9 @@ struct mkacc_ctx {
     size_t gate_B = 0;
     uint8_t* d_digits = nullptr;   // [B][k][dks][N]
     uint32_t* d_bh = nullptr;      // [B] MK-LWE rotation b
-    uint32_t* d_gin = nullptr;     // host API staging of gate inputs
+    uint32_t* d_gin = nullptr;     // host API staging of gate inputs (grow-only)
     uint32_t* d_gout = nullptr;
+    size_t gin_words = 0, gout_words = 0;
     // 64-bit word path (mkacc_wide.hpp), used when Q does not fit the 27-bit kernel
     bool wide = false;
     wide::Mod64 wm{};
@@ -726,6 +775,7 @@ struct mkacc_ctx {
     uint32_t* d_wcvals = nullptr;
     uint32_t* d_wct = nullptr;     // host-pointer API staging
     uint64_t* d_wio = nullptr;
+    uint32_t* d_bad = nullptr;     // input-range flag of the device entry points (mkacc_sync)
     std::mutex mu;
 };
 
@@ -795,7 +845,8 @@ uint32_t* launch_steps(mkacc_ctx* c, size_t B) {
 void launch_prep_c(mkacc_ctx* c, const uint32_t* d_ct, size_t B) {
     const size_t tot = B * (size_t)c->p.k * c->p.n;
     hipLaunchKernelGGL(prep_c_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, c->stream, d_ct,
-                       c->d_cvals, (uint32_t)B, c->p.k * c->p.n, (uint32_t)c->method_class, (uint32_t)c->p.q);
+                       c->d_cvals, (uint32_t)B, c->p.k * c->p.n, (uint32_t)c->method_class, (uint32_t)c->p.q,
+                       c->d_bad);
 }
 
 int launch_batch(mkacc_ctx* c, const uint32_t* d_ct, const uint32_t* d_in, uint32_t* d_out, size_t B) {
@@ -809,7 +860,7 @@ int launch_batch(mkacc_ctx* c, const uint32_t* d_ct, const uint32_t* d_in, uint3
     {
         const size_t tw = npoly * kN;
         hipLaunchKernelGGL(eval_to_c4_kernel, dim3((unsigned)((tw + tpb - 1) / tpb)), dim3(tpb), 0, c->stream, d_in,
-                           c->d_acc0, npoly, c->ninv, c->ninvp, c->mod.Q);
+                           c->d_acc0, npoly, c->ninv, c->ninvp, c->mod.Q, c->d_bad);
     }
     uint32_t* cur = launch_steps(c, B);
     {
@@ -857,7 +908,7 @@ int ensure_test_vector(mkacc_ctx* c) {
     hipLaunchKernelGGL(ntt_fwd_kernel, dim3(1), dim3(kThreads), kStepLdsBytes, c->stream, din, dev, 1u, c->d_img,
                        c->d_twf, c->mod.Q);
     hipLaunchKernelGGL(eval_to_c4_kernel, dim3(kN / 256), dim3(256), 0, c->stream, dev, c->d_tv, (size_t)1, c->ninv,
-                       c->ninvp, c->mod.Q);
+                       c->ninvp, c->mod.Q, (uint32_t*)nullptr);
     HIP_TRY(hipStreamSynchronize(c->stream));
     HIP_TRY(hipFree(din));
     HIP_TRY(hipFree(dev));
@@ -918,10 +969,10 @@ int launch_gates(mkacc_ctx* c, const uint32_t* d_nand, const uint32_t* d_a1, con
     const unsigned g1 = (unsigned)((tot + 255) / 256);
     if (c->method_class == XZW)
         hipLaunchKernelGGL(mntru_head_kernel, dim3(g1), dim3(256), 0, c->stream, d_nand, d_a1, d_a2, c->d_ct,
-                           (uint32_t)B, kn, (uint32_t)c->p.q);
+                           (uint32_t)B, kn, (uint32_t)c->p.q, c->d_bad);
     else
         hipLaunchKernelGGL(mklwe_head_kernel, dim3(g1), dim3(256), 0, c->stream, d_a1, d_b1, d_a2, d_b2, c->d_ct,
-                           c->d_bh, (uint32_t)B, kn, (uint32_t)c->p.q);
+                           c->d_bh, (uint32_t)B, kn, (uint32_t)c->p.q, c->d_bad);
     launch_prep_c(c, c->d_ct, B);
     const size_t tw = B * k * (size_t)kN;
     hipLaunchKernelGGL(acc_init_kernel, dim3((unsigned)((tw + 255) / 256)), dim3(256), 0, c->stream, c->d_acc0,
@@ -982,6 +1033,46 @@ int upload_keys_impl(mkacc_ctx* c, const W* evk, const W* pkey) {
     if (!c->d_pkey) HIP_TRY(hipMalloc(&c->d_pkey, hp.size() * 4));
     HIP_TRY(hipMemcpy(c->d_keys, host.data(), host.size() * 4, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->d_pkey, hp.data(), hp.size() * 4, hipMemcpyHostToDevice));
+    c->have_keys = true;
+    return MKACC_OK;
+}
+
+// keys already in device memory (e.g. the RCCL-broadcast buffer of bench.py):
+// one layout kernel per array on the context stream, no host round trip
+template <typename W>
+int upload_keys_device_impl(mkacc_ctx* c, const W* d_evk, const W* d_pkey) {
+    const uint32_t k = c->p.k, n1 = c->p.n + 1, nk = c->nk, dg = c->dg;
+    const size_t ep = (size_t)k * nk * n1 * dg * 2, pp = (size_t)k * dg;
+    const unsigned tpb = 256;
+    auto grid = [&](size_t np) { return dim3((unsigned)((np * kN + tpb - 1) / tpb)); };
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipMemsetAsync(c->d_bad, 0, 4, c->stream));
+    c->have_keys = false;
+    if (c->wide) {
+        const uint64_t Q = c->p.Q, R = (uint64_t)(((unsigned __int128)1 << 64) % Q);
+        const uint64_t Rp = (uint64_t)(((unsigned __int128)R << 64) / Q);
+        if (!c->d_wkeys) HIP_TRY(hipMalloc(&c->d_wkeys, ep * kN * 8));
+        if (!c->d_wpkey) HIP_TRY(hipMalloc(&c->d_wpkey, pp * kN * 8));
+        hipLaunchKernelGGL(wide_key_layout_kernel<W>, grid(ep), dim3(tpb), 0, c->stream, d_evk, c->d_wkeys, ep, nk,
+                           n1, dg * 2, Q, R, Rp, c->d_bad);
+        hipLaunchKernelGGL(wide_key_layout_kernel<W>, grid(pp), dim3(tpb), 0, c->stream, d_pkey, c->d_wpkey, pp, 1u,
+                           1u, dg, Q, R, Rp, c->d_bad);
+    } else {
+        if (!c->d_keys) HIP_TRY(hipMalloc(&c->d_keys, ep * kN * 4));
+        if (!c->d_pkey) HIP_TRY(hipMalloc(&c->d_pkey, pp * kN * 4));
+        hipLaunchKernelGGL(key_layout_kernel<W>, grid(ep), dim3(tpb), 0, c->stream, d_evk, c->d_keys, ep, nk, n1,
+                           dg * 2, c->mod.Q, c->ninv, c->ninvp, c->d_bad);
+        hipLaunchKernelGGL(key_layout_kernel<W>, grid(pp), dim3(tpb), 0, c->stream, d_pkey, c->d_pkey, pp, 1u, 1u,
+                           dg, c->mod.Q, c->ninv, c->ninvp, c->d_bad);
+    }
+    HIP_TRY(hipGetLastError());
+    uint32_t bad = 0;
+    HIP_TRY(hipMemcpyAsync(&bad, c->d_bad, 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (bad) {
+        HIP_TRY(hipMemset(c->d_bad, 0, 4));
+        return fail(MKACC_E_RANGE, "evk/pkey word not a canonical residue mod Q");
+    }
     c->have_keys = true;
     return MKACC_OK;
 }
@@ -1117,7 +1208,7 @@ int wide_launch_batch(mkacc_ctx* c, const uint32_t* d_ct, const uint64_t* d_in, 
     const uint32_t k = c->p.k, n = c->p.n;
     const size_t tot = B * (size_t)k * n, accb = B * (size_t)k * kN * 8;
     hipLaunchKernelGGL(prep_c_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, c->stream, d_ct, c->d_wcvals,
-                       (uint32_t)B, k * n, (uint32_t)c->method_class, (uint32_t)c->p.q);
+                       (uint32_t)B, k * n, (uint32_t)c->method_class, (uint32_t)c->p.q, c->d_bad);
     HIP_TRY(hipMemcpyAsync(c->d_wacc0, d_in, accb, hipMemcpyDeviceToDevice, c->stream));
     uint64_t* cur = c->d_wacc0;
     uint64_t* nxt = c->d_wacc1;
@@ -1216,6 +1307,21 @@ int check_batch_inputs(const mkacc_ctx* c, const uint32_t* ct, size_t B) {
     return MKACC_OK;
 }
 
+// The reference's MKNTRU_B gate is undefined: GenerateBinFHEContext builds an
+// MNTRU context for it (binfhecontext.cpp:174), EvalBinGate hands the unscaled
+// mod-q MNTRU words to BootstrapGateCore (binfhe-base-scheme.cpp:1127), and
+// XZW_B uses them directly as monomial exponents (mk-acc-xzw_B.cpp:120,126,290),
+// i.e. GetMonomial(c) with c up to q - 1 > 2N -- an out-of-range table read.
+// The gate API rejects it (config_error); EvalAcc itself stays available for
+// MKNTRU_B with exponents in [0, 2N].
+int reject_mkntru_b(const mkacc_ctx* c) {
+    if (c->p.method == MKACC_METHOD_MKNTRU_B)
+        return fail(MKACC_E_ARG, "MKNTRU_B NAND gates are undefined in the reference (MNTRU words mod q used as "
+                                 "XZW_B monomial exponents, binfhe-base-scheme.cpp:1127, mk-acc-xzw_B.cpp:120); "
+                                 "use MKNTRU or MKNTRU_LWE");
+    return MKACC_OK;
+}
+
 }  // namespace
 
 // ---- C ABI ------------------------------------------------------------------------
@@ -1289,6 +1395,8 @@ int mkacc_create(const mkacc_params* pin, int device, mkacc_ctx** out) {
     if (wide) {
         HIP_TRY(hipSetDevice(device));
         HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        HIP_TRY(hipMalloc(&c->d_bad, 4));
+        HIP_TRY(hipMemset(c->d_bad, 0, 4));
         const int rc = wide_setup(c.get());
         if (rc) {
             mkacc_destroy(c.release());
@@ -1319,6 +1427,8 @@ int mkacc_create(const mkacc_params* pin, int device, mkacc_ctx** out) {
 
     HIP_TRY(hipSetDevice(device));
     HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIP_TRY(hipMalloc(&c->d_bad, 4));
+    HIP_TRY(hipMemset(c->d_bad, 0, 4));
     // NTT tables in the reference's order (transformnat-impl.h:705-760)
     std::vector<uint64_t> tf(kN), ti(kN), pw(2 * kN);
     {
@@ -1369,7 +1479,7 @@ void mkacc_destroy(mkacc_ctx* c) {
                     (void*)c->d_io, (void*)c->d_ksk, (void*)c->d_lweA, (void*)c->d_lweB, (void*)c->d_tv,
                     (void*)c->d_digits, (void*)c->d_bh, (void*)c->d_gin, (void*)c->d_gout, (void*)c->d_wtwf,
                     (void*)c->d_wtwi, (void*)c->d_wpsi, (void*)c->d_wkeys, (void*)c->d_wpkey, (void*)c->d_wacc0,
-                    (void*)c->d_wacc1, (void*)c->d_wcvals, (void*)c->d_wct, (void*)c->d_wio})
+                    (void*)c->d_wacc1, (void*)c->d_wcvals, (void*)c->d_wct, (void*)c->d_wio, (void*)c->d_bad})
         if (p) (void)hipFree(p);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -1397,6 +1507,16 @@ int mkacc_upload_keys_u64(mkacc_ctx* c, const uint64_t* evk, const uint64_t* pke
     std::lock_guard<std::mutex> g(c->mu);
     if (c->wide) return wide_upload_keys<uint64_t>(c, evk, pkey);
     return upload_keys_impl<uint64_t>(c, evk, pkey);
+}
+
+int mkacc_upload_keys_device(mkacc_ctx* c, const void* d_evk, const void* d_pkey, uint32_t word_bytes) {
+    if (!c || !d_evk || !d_pkey) return fail(MKACC_E_ARG, "null argument");
+    if (word_bytes != 4 && word_bytes != 8) return fail(MKACC_E_ARG, "word_bytes must be 4 or 8");
+    if (word_bytes == 4 && c->p.Q > 0xFFFFFFFFull) return fail(MKACC_E_ARG, "Q >= 2^32 needs 8-byte key words");
+    std::lock_guard<std::mutex> g(c->mu);
+    if (word_bytes == 4)
+        return upload_keys_device_impl(c, (const uint32_t*)d_evk, (const uint32_t*)d_pkey);
+    return upload_keys_device_impl(c, (const uint64_t*)d_evk, (const uint64_t*)d_pkey);
 }
 
 int mkacc_is_wide(const mkacc_ctx* c) { return c && c->wide ? 1 : 0; }
@@ -1523,6 +1643,7 @@ int mkacc_upload_ksk_mklwe(mkacc_ctx* c, const mkacc_ks_params* ks, const uint32
     std::lock_guard<std::mutex> g(c->mu);
     if (c->wide) return fail(MKACC_E_UNSUPPORTED, "the 64-bit word path covers EvalAcc only; NAND gates need Q < 2^27");
     if (c->method_class != XZW_B) return fail(MKACC_E_ARG, "MK-LWE KeySwitch keys belong to the MKNTRU_LWE method");
+    if (int rc = reject_mkntru_b(c)) return rc;
     int rc = check_ks(c, ks);
     if (rc) return rc;
     const size_t rows = (size_t)c->p.k * kN * ks->baseKS * c->dks;
@@ -1564,12 +1685,20 @@ int gate_host(mkacc_ctx* c, const uint32_t* nand, const uint32_t* a1, const uint
         for (size_t i = 0; i < B; ++i)
             if (b1[i] >= q || b2[i] >= q) return fail(MKACC_E_RANGE, "ciphertext b not a canonical residue mod q");
     HIP_TRY(hipSetDevice(c->device));
+    // staging buffers grow only: a single-gate caller (the reference's
+    // EvalBinGate, boolean-mkntru.cpp:36-38) pays no allocation per gate
     const size_t in_words = kn + 2 * B * kn + 2 * B, out_words = B * kno + B;
-    if (c->d_gin) HIP_TRY(hipFree(c->d_gin));
-    if (c->d_gout) HIP_TRY(hipFree(c->d_gout));
-    c->d_gin = c->d_gout = nullptr;
-    HIP_TRY(hipMalloc(&c->d_gin, in_words * 4));
-    HIP_TRY(hipMalloc(&c->d_gout, out_words * 4));
+    if (in_words > c->gin_words || out_words > c->gout_words) {
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        if (c->d_gin) HIP_TRY(hipFree(c->d_gin));
+        if (c->d_gout) HIP_TRY(hipFree(c->d_gout));
+        c->d_gin = c->d_gout = nullptr;
+        c->gin_words = c->gout_words = 0;
+        HIP_TRY(hipMalloc(&c->d_gin, in_words * 4));
+        HIP_TRY(hipMalloc(&c->d_gout, out_words * 4));
+        c->gin_words = in_words;
+        c->gout_words = out_words;
+    }
     uint32_t* dn = c->d_gin;
     uint32_t* d1 = dn + kn;
     uint32_t* d2 = d1 + B * kn;
@@ -1607,7 +1736,8 @@ int mkacc_eval_nand_mklwe(mkacc_ctx* c, const uint32_t* a1, const uint32_t* b1, 
     if (!c || !a1 || !b1 || !a2 || !b2 || !out_a || !out_b) return fail(MKACC_E_ARG, "null argument");
     std::lock_guard<std::mutex> g(c->mu);
     if (c->wide) return fail(MKACC_E_UNSUPPORTED, "the 64-bit word path covers EvalAcc only; NAND gates need Q < 2^27");
-    if (c->method_class != XZW_B) return fail(MKACC_E_ARG, "method is not MKNTRU_LWE / MKNTRU_B");
+    if (c->method_class != XZW_B) return fail(MKACC_E_ARG, "method is not MKNTRU_LWE");
+    if (int rc = reject_mkntru_b(c)) return rc;
     if (a1 == a2) return fail(MKACC_E_ARG, "Input ciphertexts should be independant");
     if (B == 0) return MKACC_OK;
     return gate_host(c, nullptr, a1, b1, a2, b2, out_a, out_b, B);
@@ -1619,6 +1749,7 @@ int mkacc_eval_nand_device(mkacc_ctx* c, const uint32_t* d_ct_nand, const uint32
     if (!c || !d_a1 || !d_a2 || !d_out_a) return fail(MKACC_E_ARG, "null argument");
     if (c->wide) return fail(MKACC_E_UNSUPPORTED, "the 64-bit word path covers EvalAcc only; NAND gates need Q < 2^27");
     std::lock_guard<std::mutex> g(c->mu);
+    if (int rc = reject_mkntru_b(c)) return rc;
     if (c->method_class == XZW && !d_ct_nand) return fail(MKACC_E_ARG, "null ctNAND");
     if (c->method_class == XZW_B && (!d_b1 || !d_b2 || !d_out_b)) return fail(MKACC_E_ARG, "null b");
     HIP_TRY(hipSetDevice(c->device));
@@ -1642,7 +1773,7 @@ int mkacc_gate_tail(mkacc_ctx* c, const uint32_t* acc, uint32_t* out_a, uint32_t
     HIP_TRY(hipMalloc(&dout, (B * kno + B) * 4));
     HIP_TRY(hipMemcpyAsync(din, acc, npoly * kN * 4, hipMemcpyHostToDevice, c->stream));
     hipLaunchKernelGGL(eval_to_c4_kernel, dim3((unsigned)((npoly * kN + 255) / 256)), dim3(256), 0, c->stream, din,
-                       c->d_acc0, npoly, c->ninv, c->ninvp, c->mod.Q);
+                       c->d_acc0, npoly, c->ninv, c->ninvp, c->mod.Q, (uint32_t*)nullptr);
     launch_tail(c, c->d_acc0, dout, dout + B * kno, B);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(out_a, dout, B * kno * 4, hipMemcpyDeviceToHost, c->stream));
@@ -1655,7 +1786,16 @@ int mkacc_gate_tail(mkacc_ctx* c, const uint32_t* acc, uint32_t* out_a, uint32_t
 
 int mkacc_sync(mkacc_ctx* c) {
     if (!c) return fail(MKACC_E_ARG, "null context");
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_TRY(hipSetDevice(c->device));
+    uint32_t bad = 0;
+    HIP_TRY(hipMemcpyAsync(&bad, c->d_bad, 4, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    if (bad) {
+        HIP_TRY(hipMemset(c->d_bad, 0, 4));
+        return fail(MKACC_E_RANGE, "an input word passed to a device entry point was out of range "
+                                   "(ciphertext not mod q / 2N, accumulator or ciphertext not canonical)");
+    }
     return MKACC_OK;
 }
 

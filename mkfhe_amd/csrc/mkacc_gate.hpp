@@ -25,13 +25,14 @@ __device__ __forceinline__ uint32_t round_qQ(uint32_t v, uint32_t q, uint32_t Q)
 // mntru-pke.cpp:826-838).  s over k*n.
 __global__ void mntru_head_kernel(const uint32_t* __restrict__ ct_nand, const uint32_t* __restrict__ ct1,
                                   const uint32_t* __restrict__ ct2, uint32_t* __restrict__ out, uint32_t B,
-                                  uint32_t kn, uint32_t q) {
+                                  uint32_t kn, uint32_t q, uint32_t* __restrict__ bad) {
     const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= (size_t)B * kn) return;
     const uint32_t s = (uint32_t)(idx % kn);
-    uint32_t t = ct1[idx] + ct2[idx];
+    const uint32_t x1 = ct1[idx], x2 = ct2[idx], a = ct_nand[s];
+    if (x1 >= q || x2 >= q || a >= q) *bad = 1u;
+    uint32_t t = x1 + x2;
     t = t >= q ? t - q : t;
-    const uint32_t a = ct_nand[s];
     out[idx] = a >= t ? a - t : a + q - t;
 }
 
@@ -41,10 +42,11 @@ __global__ void mntru_head_kernel(const uint32_t* __restrict__ ct_nand, const ui
 __global__ void mklwe_head_kernel(const uint32_t* __restrict__ a1, const uint32_t* __restrict__ b1,
                                   const uint32_t* __restrict__ a2, const uint32_t* __restrict__ b2,
                                   uint32_t* __restrict__ c, uint32_t* __restrict__ bh, uint32_t B, uint32_t kn,
-                                  uint32_t q) {
+                                  uint32_t q, uint32_t* __restrict__ bad) {
     const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t M = 2u * kN;
     if (idx < (size_t)B * kn) {
+        if (a1[idx] >= q || a2[idx] >= q) *bad = 1u;
         uint32_t t = a1[idx] + a2[idx];
         t = t >= q ? t - q : t;
         const uint32_t at = t == 0 ? 0 : q - t;
@@ -52,6 +54,7 @@ __global__ void mklwe_head_kernel(const uint32_t* __restrict__ a1, const uint32_
         c[idx] = ams == 0 ? 0 : M - ams;
     }
     if (idx < B) {
+        if (b1[idx] >= q || b2[idx] >= q) *bad = 1u;
         uint32_t t = b1[idx] + b2[idx];
         t = t >= q ? t - q : t;
         const uint32_t b5 = (5u * q / 8u) % q;

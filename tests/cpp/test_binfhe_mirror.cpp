@@ -81,6 +81,17 @@ static void test_cpu() {
     }
     auto c0 = cc.Encrypt(sk, 0), c1 = cc.Encrypt(sk, 1);
     EXPECT(throws<config_error>([&] { cc.EvalBinGate(NAND, c0, c1); }));  // keys not generated
+    {   // MKNTRU_B gates are undefined in the reference (binfhe-base-scheme.cpp:1127, mk-acc-xzw_B.cpp:120)
+        BinFHEContext cb;
+        cb.GenerateBinFHEContext(STD100_MKNTRU, MKNTRU_B);
+        bool named = false;
+        try {
+            cb.EvalBinGate(NAND, c0, c1);
+        } catch (const config_error& e) {
+            named = std::strstr(e.what(), "MKNTRU_B") != nullptr;
+        }
+        EXPECT(named);
+    }
     // secret-key file round trip (mkfhe_keys.h wire format)
     const std::string f = std::string(std::getenv("TMPDIR") ? std::getenv("TMPDIR") : "/tmp") + "/mkfhe_sk_test.mkfk";
     cc.SaveSecretKey(f, sk);
