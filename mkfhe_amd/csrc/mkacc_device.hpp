@@ -28,6 +28,8 @@ struct Mod {
     uint32_t Q;      // modulus, 2^26 < Q < 2^27
     uint32_t mu;     // floor(2^58 / Q)
     uint32_t r32;    // 2^32 mod Q
+    uint32_t qinv;   // -Q^-1 mod 2^32 (Montgomery reduction, R = 2^32)
+    uint32_t m1;     // floor(2^32 / Q): Shoup companion of 1
 };
 
 // ---- buffer-resource memory access -------------------------------------------
@@ -108,6 +110,23 @@ __device__ __forceinline__ uint64_t mul64_pin(uint32_t a, uint32_t b) {
     return r;
 }
 
+// Montgomery reduction (R = 2^32) of a lazy 64-bit sum x < Q * 2^32:
+// m = x * (-Q^-1) mod 2^32 makes x + m Q divisible by 2^32, and
+// (x + m Q) / 2^32 < 2Q is congruent to x * 2^-32 mod Q.  Two instructions
+// (v_mul_lo_u32 + v_mad_u64_u32, result = the high word).  The step kernel's
+// keys are stored times 2^32 mod Q, so the reduction returns the plain sum.
+// Since Q < 2^27, Q * 2^32 > 32 Q^2: sums of up to 32 products of residues
+// below Q (or their equivalent, e.g. 8 products of values < 4Q and < Q) qualify.
+__device__ __forceinline__ uint32_t redc(uint64_t x, uint32_t Q, uint32_t qinv) {
+    const uint32_t m = (uint32_t)x * qinv;
+    return (uint32_t)(mad64_pin<true>(m, Q, x) >> 32);
+}
+// x < Q * 2^32 -> hi * (2^32 mod Q) + lo < Q^2 + 2^32 < 2 Q^2: same residue;
+// keeps a long lazy sum inside redc's range
+__device__ __forceinline__ uint64_t fold64(uint64_t x, uint32_t r32) {
+    return (uint64_t)(uint32_t)(x >> 32) * r32 + (uint32_t)x;
+}
+
 // ---- LDS transposes ---------------------------------------------------------
 // Row padding of one word per 32 (addr = j + j/32) makes every layout's access
 // conflict-free for ds_*_b32 AND additive in (lane, reg), so each transpose uses
@@ -122,10 +141,16 @@ __device__ __forceinline__ uint32_t baseB(uint32_t l) { return 66u * (l >> 1) + 
 __device__ __forceinline__ constexpr uint32_t offB(int r) { return 2u * r + (r >> 4); }
 __device__ __forceinline__ uint32_t baseC(uint32_t l) { return 33u * l; }
 __device__ __forceinline__ constexpr uint32_t offC(int r) { return (uint32_t)r; }
+// layout D (inverse transform, pass 2): x[r] <-> j = ((lane>>5) << 10) | (r << 5) | (lane & 31),
+// regs = bits 9..5; pad(j) = 1056 (lane>>5) + (lane & 31) + 33 r: lanes 0..31 and
+// 32..63 each hit 32 consecutive words, the two halves 32 banks apart
+__device__ __forceinline__ uint32_t baseD(uint32_t l) { return 1056u * (l >> 5) + (l & 31u); }
+__device__ __forceinline__ constexpr uint32_t offD(int r) { return 33u * r; }
 
 __device__ __forceinline__ uint32_t jA(uint32_t l, uint32_t r) { return (r << 6) | l; }
 __device__ __forceinline__ uint32_t jB(uint32_t l, uint32_t r) { return ((l >> 1) << 6) | (r << 1) | (l & 1u); }
 __device__ __forceinline__ uint32_t jC(uint32_t l, uint32_t r) { return (l << 5) | r; }
+__device__ __forceinline__ uint32_t jD(uint32_t l, uint32_t r) { return ((l >> 5) << 10) | (r << 5) | (l & 31u); }
 
 // Keeps the scheduler from hoisting a later stage's twiddle loads (and their
 // VGPRs) above the current stage.
@@ -140,11 +165,11 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 template <int LAYOUT>
 __device__ __forceinline__ uint32_t lbase(uint32_t l) {
-    return LAYOUT == 0 ? baseA(l) : (LAYOUT == 1 ? baseB(l) : baseC(l));
+    return LAYOUT == 0 ? baseA(l) : (LAYOUT == 1 ? baseB(l) : (LAYOUT == 2 ? baseC(l) : baseD(l)));
 }
 template <int LAYOUT>
 __device__ __forceinline__ constexpr uint32_t loff(int r) {
-    return LAYOUT == 0 ? offA(r) : (LAYOUT == 1 ? offB(r) : offC(r));
+    return LAYOUT == 0 ? offA(r) : (LAYOUT == 1 ? offB(r) : (LAYOUT == 2 ? offC(r) : offD(r)));
 }
 
 template <int SRC, int DST>
@@ -182,25 +207,13 @@ __device__ __forceinline__ void ct_bfly_lazy(uint32_t& a, uint32_t& b, uint2 w, 
     a = X - Tn;                                                  // X + T
     b = X + Tn + 2u * Q;                                         // X - T + 2Q
 }
-// last stage: a in [0, 24Q) -> X in [0, 2Q); outputs in [0, 4Q)
-__device__ __forceinline__ void ct_bfly_last(uint32_t& a, uint32_t& b, uint2 w, uint32_t Q) {
-    uint32_t X = min(a, a - 16u * Q);
-    X = min(X, X - 8u * Q);
-    X = min(X, X - 4u * Q);
-    X = min(X, X - 2u * Q);                                      // [0, 2Q)
+// last stage: a in [0, 24Q) -> X in [0, 2Q) as Shoup's product by 1
+// (companion m1 = floor(2^32 / Q)); outputs in [0, 4Q)
+__device__ __forceinline__ void ct_bfly_last(uint32_t& a, uint32_t& b, uint2 w, uint32_t Q, uint32_t m1) {
+    const uint32_t X = a - __umulhi(a, m1) * Q;                  // [0, 2Q)
     const uint32_t Tn = shoup_neg<false>(b, w, Q);
     a = X - Tn;                                                  // [0, 4Q)
     b = X + Tn + 2u * Q;                                         // (0, 4Q)
-}
-// inverse twiddle pairs are { w, floor(w 2^32 / Q) } (not negated)
-template <bool SW = false>
-__device__ __forceinline__ void gs_bfly(uint32_t& a, uint32_t& b, uint2 w, uint32_t Q) {
-    const uint32_t lo = a, hi = b;                               // [0, 2Q)
-    const uint32_t s = lo + hi;
-    a = min(s, s - 2u * Q);                                      // [0, 2Q)
-    const uint32_t d = lo - hi + 2u * Q;                         // (0, 4Q)
-    const uint32_t q = __umulhi(d, w.y);
-    b = (uint32_t)mad64_pin<true>(q, 0u - Q, mul64_pin<SW>(d, w.x));   // d*w - q*Q in [0, 2Q)
 }
 // [0, 4Q) -> [0, Q)
 __device__ __forceinline__ uint32_t canon4(uint32_t x, uint32_t Q) {
@@ -268,26 +281,6 @@ __device__ __forceinline__ void fwd_stage_b(uint32_t (&x)[kRegs], const uint2* t
         sched_fence();
     }
 }
-// inverse pass-B stage on bit B (1..5)
-template <int B>
-__device__ __forceinline__ void inv_stage_b(uint32_t (&x)[kRegs], const uint2* twl, uint32_t lhi, uint32_t Q) {
-    constexpr int NP = 1 << (5 - B), H = 1 << (B - 1), CH = NP > 8 ? 8 : NP;
-    const uint2* t = twl + twl_off(10 - B) + lhi;
-#pragma unroll
-    for (int c0 = 0; c0 < NP; c0 += CH) {
-        uint2 w[CH];
-#pragma unroll
-        for (int j = 0; j < CH; ++j) w[j] = t[32 * (c0 + j)];
-#pragma unroll
-        for (int r = 0; r < kRegs; ++r) {
-            if (r & H) continue;
-            const int m = r >> B;
-            if (m < c0 || m >= c0 + CH) continue;
-            gs_bfly(x[r], x[r + H], w[m - c0], Q);
-        }
-        sched_fence();
-    }
-}
 
 // Forward negacyclic NTT of one polynomial per wave, reference EVAL order.
 //   tw_g : reference forward table (pairs) in global memory, pass A reads it
@@ -297,7 +290,7 @@ __device__ __forceinline__ void inv_stage_b(uint32_t (&x)[kRegs], const uint2* t
 //   tw10 : stage-10 twiddles (pairs (m, lane) at tw10 + 64*m + lane); twl + kTwlC
 //          or a copy of that block in LDS
 __device__ __forceinline__ void ntt_fwd(uint32_t (&x)[kRegs], uint32_t* lds, const uint2* tw_g, const uint2* twl,
-                                        const uint2* tw10, uint32_t l, uint32_t Q) {
+                                        const uint2* tw10, uint32_t l, uint32_t Q, uint32_t m1) {
     // pass A: stages 0..4 (bits 10..6); twiddle index uniform across the wave
     const ConstTable twc{(const_u64*)opaque(tw_g)};
 #pragma unroll
@@ -329,18 +322,119 @@ __device__ __forceinline__ void ntt_fwd(uint32_t (&x)[kRegs], uint32_t* lds, con
 #pragma unroll
         for (int m = 0; m < 8; ++m) w[m] = tc[64 * (8 * hf + m)];
 #pragma unroll
-        for (int m = 0; m < 8; ++m) ct_bfly_last(x[16 * hf + 2 * m], x[16 * hf + 2 * m + 1], w[m], Q);
+        for (int m = 0; m < 8; ++m) ct_bfly_last(x[16 * hf + 2 * m], x[16 * hf + 2 * m + 1], w[m], Q, m1);
         sched_fence();
     }
 }
 
-// ---- inverse NTT WITHOUT the N^-1 factor (Gentleman-Sande) -------------------
-// Reference inverse table (psi^-brv(i)); same split as the forward transform.
-// Input residues in [0, 2Q); output canonical coefficients in [0, Q).
-__device__ __forceinline__ void ntt_inv_noscale(uint32_t (&x)[kRegs], uint32_t* lds, const uint2* twi_g,
-                                                const uint2* twl, uint32_t l, uint32_t Q) {
+// ---- inverse NTT WITHOUT the N^-1 factor: DIT butterflies + post-twist --------
+// The reference's inverse (Gentleman-Sande, transformnat-impl.h:492-552) maps the
+// EVAL vector A (slot j = evaluation at psi^(2 brv(j) + 1)) to
+//   a_i = N^-1 psi^-i sum_k A[brv(k)] w^-ik,   w = psi^2.
+// A is the natural-order evaluation vector stored bit-reversed, so radix-2
+// decimation-in-time butterflies on bits 0, 1, ..., 10 (bit b: pairs (j, j + 2^b),
+// twiddle psi^-(t 2^(11-b)), t = j mod 2^b) produce the cyclic sum in natural
+// order, and one Shoup product by psi^-i per coefficient finishes the transform
+// (N^-1 is folded into keys and accumulator).  Every butterfly is
+// the forward transform's lazy 5-instruction CT butterfly (values grow by < 2Q
+// per stage; the final Shoup product accepts any 32-bit word and returns a
+// canonical residue), and butterflies with twiddle 1 (t = 0, resolved per
+// register in pass 1) drop the product while the bounds allow -- against 8
+// instructions for a lazy GS butterfly.
+//   pass 1 (layout C, regs = bits 4..0): bits 0..4, wave-uniform twiddles (scalar)
+//   pass 2 (layout D, regs = bits 9..5): bits 5..9, per-lane twiddles (lane & 31)
+//   pass 3 (layout A, regs = bits 10..6): bit 10 and the twist, per-lane
+// Tables (mkacc_engine.hip builds them):
+//   tis  [2^b + t], b < 5, t < 2^b  : {-w, w'} of psi^-(t 2^(11-b))   (global, scalar reads)
+//   twl  [twl_off(b) + 32 m + (l & 31)], b = 5..9 : t = (l & 31) | (m << 5)
+//        [kTwlC + 64 m + l]                        : bit 10, t = (m << 6) | l
+//        [kTwlPairs + 64 r + l]                    : {psi^-i, companion}, i = (r << 6) | l
+constexpr int kInvImgPairs = kTwlPairs + kN;
+
+// Pass-1 schedule: value bounds in units of Q per register; a twiddle-1
+// butterfly skips the product when its doubled bound still leaves room for the
+// remaining stages (+2 each); everything entering pass 2 stays below 20 Q, so
+// the six per-lane stages end below 32 Q <= 2^32 (Q < 2^27).
+struct InvPlan {
+    bool skip[5][kRegs];
+    int bound[5][kRegs];   // bound of each register entering stage b
+    int maxb;
+    constexpr explicit InvPlan(int b0) : skip{}, bound{}, maxb(0) {
+        int bd[kRegs] = {};
+        for (int r = 0; r < kRegs; ++r) bd[r] = b0;
+        for (int b = 0; b < 5; ++b) {
+            const int h = 1 << b;
+            for (int r = 0; r < kRegs; ++r) bound[b][r] = bd[r];
+            for (int r = 0; r < kRegs; ++r) {
+                if (r & h) continue;
+                const int s = bd[r] + bd[r + h];
+                if ((r & (h - 1)) == 0 && s + 2 * (4 - b) <= 20) {
+                    skip[b][r] = true;
+                    bd[r] = bd[r + h] = s;
+                } else {
+                    bd[r] = bd[r + h] = bd[r] + 2;
+                }
+            }
+        }
+        for (int r = 0; r < kRegs; ++r) maxb = bd[r] > maxb ? bd[r] : maxb;
+    }
+};
+constexpr InvPlan kInvPlan(2);   // inputs in [0, 2Q)
+static_assert(kInvPlan.maxb <= 20, "inverse NTT bounds");
+
+// pass-2 stage on bit B (5..9), layout D: NP = 2^(B-5) per-lane twiddles
+template <int B>
+__device__ __forceinline__ void inv_stage_d(uint32_t (&x)[kRegs], const uint2* twl, uint32_t l31, uint32_t Q) {
+    constexpr int H = 1 << (B - 5), NP = H, CH = NP > 8 ? 8 : NP;
+    const uint2* t = twl + twl_off(B) + l31;
+#pragma unroll
+    for (int c0 = 0; c0 < NP; c0 += CH) {
+        uint2 w[CH];
+#pragma unroll
+        for (int j = 0; j < CH; ++j) w[j] = t[32 * (c0 + j)];
+#pragma unroll
+        for (int r = 0; r < kRegs; ++r) {
+            if (r & H) continue;
+            const int m = r & (H - 1);
+            if (m < c0 || m >= c0 + CH) continue;
+            ct_bfly_lazy(x[r], x[r + H], w[m - c0], Q);
+        }
+        sched_fence();
+    }
+}
+
+// Input residues in [0, 2Q), layout C; output canonical coefficients, layout A.
+__device__ __forceinline__ void ntt_inv(uint32_t (&x)[kRegs], uint32_t* lds, const uint2* tis, const uint2* twl,
+                                        uint32_t l, uint32_t Q) {
+    // pass 1: bits 0..4 on registers, twiddle index (r mod 2^b) wave-uniform
+    const ConstTable twc{(const_u64*)opaque(tis)};
+#pragma unroll
+    for (int b = 0; b < 5; ++b) {
+        const int h = 1 << b;
+#pragma unroll
+        for (int r = 0; r < kRegs; ++r) {
+            if (r & h) continue;
+            if (kInvPlan.skip[b][r]) {
+                // twiddle 1: X + Y, X - Y + (bound of Y)
+                const uint32_t X = x[r], Y = x[r + h];
+                x[r] = X + Y;
+                x[r + h] = X - Y + (uint32_t)kInvPlan.bound[b][r + h] * Q;
+            } else {
+                ct_bfly_lazy<true>(x[r], x[r + h], twc[h + (r & (h - 1))], Q);
+            }
+        }
+        sched_fence();
+    }
+    transpose<2, 3>(x, lds, l);
     const uint32_t lo = opaque_v(l);
-    // pass C: bit 0
+    const uint32_t l31 = lo & 31u;
+    inv_stage_d<5>(x, twl, l31, Q);
+    inv_stage_d<6>(x, twl, l31, Q);
+    inv_stage_d<7>(x, twl, l31, Q);
+    inv_stage_d<8>(x, twl, l31, Q);
+    inv_stage_d<9>(x, twl, l31, Q);
+    transpose<3, 0>(x, lds, l);
+    // pass 3: bit 10 (pairs (r, r + 16)), two halves of 8 twiddles
     const uint2* tc = twl + kTwlC + lo;
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
@@ -348,33 +442,20 @@ __device__ __forceinline__ void ntt_inv_noscale(uint32_t (&x)[kRegs], uint32_t* 
 #pragma unroll
         for (int m = 0; m < 8; ++m) w[m] = tc[64 * (8 * hf + m)];
 #pragma unroll
-        for (int m = 0; m < 8; ++m) gs_bfly(x[16 * hf + 2 * m], x[16 * hf + 2 * m + 1], w[m], Q);
+        for (int m = 0; m < 8; ++m) ct_bfly_lazy(x[8 * hf + m], x[8 * hf + m + 16], w[m], Q);
         sched_fence();
     }
-    transpose<2, 1>(x, lds, l);
-    // pass B: bits 1..5
-    const uint32_t lhi = lo >> 1;
-    inv_stage_b<1>(x, twl, lhi, Q);
-    inv_stage_b<2>(x, twl, lhi, Q);
-    inv_stage_b<3>(x, twl, lhi, Q);
-    inv_stage_b<4>(x, twl, lhi, Q);
-    inv_stage_b<5>(x, twl, lhi, Q);
-    transpose<1, 0>(x, lds, l);
-    // pass A: bits 6..10 ; uniform twiddles
-    const ConstTable twc{(const_u64*)opaque(twi_g)};
+    // twist by psi^-i, i = (r << 6) | l: canonical output
+    const uint2* tt = twl + kTwlPairs + lo;
 #pragma unroll
-    for (int b = 6; b <= 10; ++b) {
-        const int h = 1 << (b - 6);
+    for (int q4 = 0; q4 < 4; ++q4) {
+        uint2 w[8];
 #pragma unroll
-        for (int r = 0; r < kRegs; ++r) {
-            if (r & h) continue;
-            const uint2 w = twc[(1 << (10 - b)) + (r >> (b - 5))];
-            gs_bfly<true>(x[r], x[r + h], w, Q);
-        }
+        for (int m = 0; m < 8; ++m) w[m] = tt[64 * (8 * q4 + m)];
+#pragma unroll
+        for (int m = 0; m < 8; ++m) x[8 * q4 + m] = mul_shoup(x[8 * q4 + m], w[m].x, w[m].y, Q);
         sched_fence();
     }
-#pragma unroll
-    for (int r = 0; r < kRegs; ++r) x[r] = min(x[r], x[r] - Q);
 }
 
 // ---- device EVAL layout in HBM ("C4") --------------------------------------

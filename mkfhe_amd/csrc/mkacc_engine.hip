@@ -55,17 +55,21 @@ int fail(int code, const std::string& msg) {
 constexpr int kWavesPerBlock = 4;
 constexpr int kThreads = 64 * kWavesPerBlock;
 
-// Table image (built once per context, HBM):
-//   [0, kTwlPairs)                forward per-lane twiddles (mkacc_device.hpp layout)
-//   [kTwlPairs, 2 kTwlPairs)      inverse per-lane twiddles
-//   [2 kTwlPairs, + 2N)           psi^e (e in [0, 2N)) with Shoup companion, at psi_pos(e)
-// The NTTs read the twiddle runs from HBM/L2 (L1-resident, coalesced); the psi
-// table, gathered at data-dependent slots, is copied into LDS at kernel start,
-// followed by one transpose scratch of kLdsWords per wave.
+// Table image (built once per context, HBM), in uint2 pairs:
+//   [0, kTwlPairs)              forward per-lane twiddles (mkacc_device.hpp layout)
+//   [kTwlPairs, +kInvImgPairs)  inverse per-lane twiddles and the psi^-i twist (ntt_inv)
+//   [kPsiOff, + 2N)             psi^e (e in [0, 2N)) with Shoup companion, at psi_pos(e)
+//   [kPsm1Off, + 2N)            psi^e - 1 with Shoup companion, at psi_pos(e)
+// The NTTs read the twiddle runs from HBM/L2 (L1-resident, coalesced); the
+// psi^e - 1 table, gathered at data-dependent slots, is copied into LDS at kernel
+// start, followed by one transpose scratch of kLdsWords per wave.
 constexpr int kPsiPairs = 2 * kN;
-constexpr int kImgPairs = 2 * kTwlPairs + kPsiPairs;
+constexpr int kPsiOff = kTwlPairs + kInvImgPairs;
+constexpr int kPsm1Off = kPsiOff + kPsiPairs;
+constexpr int kImgPairs = kPsm1Off + kPsiPairs;
 constexpr int kImgWords = 2 * kImgPairs;
-// LDS: [forward stage-10 twiddles, 1024 pairs][psi table, 2N pairs][scratch]
+static_assert(kPsm1Off % 2 == 0 && kTwlC % 2 == 0, "LDS tables are copied with dwordx4");
+// LDS: [forward stage-10 twiddles, 1024 pairs][psi^e - 1 table, 2N pairs][scratch]
 constexpr int kLdsTabWords = 2 * (1024 + kPsiPairs);
 constexpr size_t kStepLdsBytes = (size_t)(kLdsTabWords + kWavesPerBlock * kLdsWords) * 4;
 static_assert(kLdsTabWords % 4 == 0, "LDS tables are copied with dwordx4");
@@ -78,40 +82,44 @@ __host__ __device__ __forceinline__ uint32_t psi_pos(uint32_t e) { return e ^ ((
 
 enum { XZW = 0, XZW_B = 1 };
 
+// Device key words (upload_keys_impl / key_layout_kernel): every evk / pkey word
+// is stored times N^-1 * 2^32 mod Q -- N^-1 because the accumulator lives scaled by
+// N^-1 (the inverse NTT then needs no N^-1), 2^32 so that one Montgomery reduction
+// (redc) of a lazy sum of key products returns the plain sum.  For MKNTRU the
+// ev1 block of every step i < n holds ev1 + ev2 (both the d- and f-halves), so
+// ev1 - ev2 X^-c = (ev1 + ev2) + ev2 (X^(N-c) - 1) is one product with a
+// psi^e - 1 table entry (key_eff).
 struct StepArgs {
     const uint32_t* acc_in;    // [B][k][N] C4, scaled by N^-1, residues in [0, 2Q)
     uint32_t* acc_out;         // [B][k][N]
     const uint32_t* cvals;     // [B] monomial exponents c of this step, in [0, 2N)
-    const uint32_t* key1;      // ev1 = (*ek)[u][0][i] : [dg][2][N] C4
+    const uint32_t* key1;      // ev1 (+ ev2 for MKNTRU) of step (u, i) : [dg][2][N] C4
     const uint32_t* key2;      // ev2 = (*ek)[u][1][i] (XZW)
     const uint32_t* keys;      // evs = (*ek)[0][0][n] (first step)
     const uint32_t* pkey;      // [k][dg][N]
-    uint32_t* deff;            // [B][dg][N] per-gate scratch: d_i of this step (XZW, not first)
     const uint32_t* img;       // table image [kImgWords]
     const uint2* tw_fwd;       // [N] reference forward table (pass A, scalar reads)
-    const uint2* tw_inv;       // [N]
+    const uint2* tw_inv;       // [32] inverse pass-1 table (ntt_inv)
     uint32_t B, k, index;
     Mod m;
     SddConsts sd;
 };
 
 // Copy the forward stage-10 twiddles (the largest per-lane run, used by 3/4
-// of the NTTs) and the psi table of the image into this workgroup's LDS.
+// of the NTTs) and the psi^e - 1 table of the image into this workgroup's LDS.
 __device__ __forceinline__ void load_image(uint32_t* smem, const uint32_t* img) {
     const uint4* src = reinterpret_cast<const uint4*>(img);
     uint4* dst = reinterpret_cast<uint4*>(smem);
-    // stage 10 of the forward table: pairs [kTwlC, kTwlC + 1024) = uint4 [kTwlC/2, +512)
     for (int i = threadIdx.x; i < 512; i += blockDim.x) dst[i] = src[kTwlC / 2 + i];
-    // psi: pairs [2 kTwlPairs, + 2N) = uint4 [kTwlPairs, + N)
-    for (int i = threadIdx.x; i < kN; i += blockDim.x) dst[512 + i] = src[kTwlPairs + i];
+    for (int i = threadIdx.x; i < kN; i += blockDim.x) dst[512 + i] = src[kPsm1Off / 2 + i];
     __syncthreads();
 }
 
 struct Tables {
     const uint2* twf;    // HBM image: forward per-lane twiddles
-    const uint2* twi;    // HBM image: inverse per-lane twiddles
+    const uint2* twi;    // HBM image: inverse per-lane twiddles + twist
     const uint2* twfc;   // LDS: forward stage-10 twiddles
-    const uint2* psi;    // LDS
+    const uint2* psi;    // LDS: psi^e - 1
 };
 __device__ __forceinline__ Tables tables(uint32_t* smem, const uint32_t* img) {
     const uint2* g = reinterpret_cast<const uint2*>(img);
@@ -122,7 +130,8 @@ __device__ __forceinline__ Tables tables(uint32_t* smem, const uint32_t* img) {
 // Monomial X^e at EVAL slot j = (lane << 5) | r: the reference stores
 // a(psi^(2 brv(j) + 1)) at position j (transformnat-impl.h:705-760), so
 // X^c -> psi^(c (2 brv(j) + 1)), with 2 brv(j) + 1 = 128 brv5(r) + (2 brv6(lane) + 1).
-// `co` = c * (2 brv6(lane) + 1) per lane; the r part is wave-uniform.
+// `co` = c * (2 brv6(lane) + 1) per lane; the r part is wave-uniform.  at()
+// returns the LDS pair of psi^e - 1, i.e. the EVAL slot of X^c - 1.
 struct Mono {
     uint32_t co;        // per-lane c * (2 brv6(l) + 1)
     uint32_t c;         // wave-uniform exponent
@@ -147,41 +156,64 @@ __device__ __forceinline__ Mono make_mono(uint32_t c, uint32_t l) {
 // Lazy Shoup product x*w in [0, 2Q) (x < 2^32)
 __device__ __forceinline__ uint32_t mul_shoup_lazy(uint32_t x, uint2 w, uint32_t Q) {
     const uint32_t q = __umulhi(x, w.y);
-    return (uint32_t)mad64_pin<true>(q, 0u - Q, mul64_pin<false>(x, w.x));   // x*w - q*Q
+    return (uint32_t)mad64_pin<true>(q, 0u - Q, mul64_pin<false>(x, w.x));   // x*w - q*Q in [0, 2Q)
 }
 
-// effective key word d_i / f_i of mk-acc-xzw(_B).cpp AddToAccXZW{,0}, canonical
-template <int METHOD, bool FIRST>
+// Ranges of the lazy Montgomery sums, in units of Q (values) and Q^2 (sums).
+// redc needs a sum below Q * 2^32 > 32 Q^2.  Digit-NTT outputs are < kG Q
+// (digit_range), effective key words from key_eff < kD Q, and the previous
+// accumulator joins the party sum as acc * (2^32 mod Q) < 2 Q^2 when it fits
+// (kAccInSum), otherwise it is added after the reduction.
+template <int DG, int METHOD, bool FIRST>
+struct Bounds {
+    static constexpr int kG = DG > 4 ? 2 : 4;
+    static constexpr int kD = DG * kG * 3 + 2 <= 32 ? 3 : (DG * kG * 2 <= 32 ? 2 : 1);
+    // the d-words the party sums actually see: XZW_B steps after the first use ev1 itself
+    static constexpr int kDSum = (METHOD == XZW_B && !FIRST) ? 1 : kD;
+    static constexpr bool kAccInSum = !FIRST && DG * kG * kDSum + 2 <= 32;
+    static_assert(DG * kG * kDSum + (kAccInSum ? 2 : 0) <= 32, "party sum bound");
+    // sumV gains DG * kG per party (pkey canonical); fold64 leaves < 2
+    static constexpr int kSvParty = DG * kG;
+    // f-part: the index party's folded sum (< 2, < 4 with the accumulator added
+    // there) plus DG products with canonical f-words (split form) or, in the
+    // first step, with f-words reduced to canonical
+    static_assert(4 + DG * kG <= 32, "f-part bound");
+};
+
+// [0, 3Q) -> [0, KD Q)
+template <int KD>
+__device__ __forceinline__ uint32_t from3q(uint32_t d, uint32_t Q) {
+    if (KD <= 2) d = min(d, d - 2u * Q);
+    if (KD <= 1) d = min(d, d - Q);
+    return d;
+}
+
+// Effective key word d_i / f_i of mk-acc-xzw(_B).cpp AddToAccXZW{,0}, below KD Q.
+// k1 is the stored ev1 word (ev1 + ev2 for MKNTRU, StepArgs), k2 = ev2, ks = evs.
+template <int METHOD, bool FIRST, int KD>
 __device__ __forceinline__ uint32_t key_eff(uint32_t k1, uint32_t k2, uint32_t ks, const uint2* psi,
                                             const Mono& mp, const Mono& mn, int r, uint32_t Q) {
     if (METHOD == XZW) {
-        const uint2 tn = mn.at(psi, r);
         if (FIRST) {
             // evs + ev1*(X^c-1) + ev2*(X^-c-1)          (xzw.cpp:375-378)
-            const uint2 tp = mp.at(psi, r);
-            const uint32_t t1 = sub_mod(mul_shoup(k1, tp.x, tp.y, Q), k1, Q);
-            const uint32_t t2 = sub_mod(mul_shoup(k2, tn.x, tn.y, Q), k2, Q);
-            return add_mod(add_mod(ks, t1, Q), t2, Q);
+            const uint32_t e1 = k1 + Q - k2;                         // ev1, (0, 2Q)
+            uint32_t d = ks + mul_shoup_lazy(e1, mp.at(psi, r), Q) + mul_shoup_lazy(k2, mn.at(psi, r), Q);
+            d = min(d, d - 2u * Q);                                  // [0, 5Q) -> [0, 3Q)
+            return from3q<KD>(d, Q);
         }
-        // ev1 - ev2*(X^-c - 1) - ev2  ==  ev1 - ev2*X^-c   (xzw.cpp:322-325);
-        // mn holds -X^-c here (exponent -c + N: psi^N = -1), so one add
-        uint32_t d = k1 + mul_shoup_lazy(k2, tn, Q);             // [0, 3Q)
-        d = min(d, d - 2u * Q);                                  // [0, 2Q)
-        return min(d, d - Q);
+        // ev1 - ev2*(X^-c - 1) - ev2  ==  ev1 - ev2*X^-c  ==  (ev1 + ev2) + ev2*(X^(N-c) - 1)
+        // (xzw.cpp:322-325); mn is the monomial X^(N-c) = -X^-c here
+        return from3q<KD>(k1 + mul_shoup_lazy(k2, mn.at(psi, r), Q), Q);
     } else {
         if (FIRST) {
             // evs + ev1*(X^c-1)                            (xzw_B.cpp:368-371)
-            const uint2 tp = mp.at(psi, r);
-            return add_mod(ks, sub_mod(mul_shoup(k1, tp.x, tp.y, Q), k1, Q), Q);
+            return from3q<KD>(ks + mul_shoup_lazy(k1, mp.at(psi, r), Q), Q);
         }
         return k1;                                        // (xzw_B.cpp:311-314)
     }
 }
 
-// Bounds of the lazy 64-bit sums (reduce58 needs < 2^58, Q < 2^27): digit NTT
-// outputs are left in [0, 4Q) when DG <= 4 (DG products plus a residue stay
-// below 16 Q^2 < 2^58) and brought to [0, 2Q) at DG = 5 (10 Q^2 + Q < 2^58);
-// keys are canonical.
+// digit NTT outputs: [0, 4Q) for DG <= 4, brought to [0, 2Q) at DG = 5 (Bounds::kG)
 template <int DG>
 __device__ __forceinline__ void digit_range(uint32_t (&x)[kRegs], uint32_t Q) {
     if (DG > 4) {
@@ -199,48 +231,30 @@ struct KeyGroup {
 };
 
 // uj_u += g * d_i ; sv += g * P[u][i]          (xzw.cpp:263-269)
-// START (digit 0): uj_u starts from acc_u (AddToAccXZW's acc + acctemp,
-// xzw.cpp:342-344), streamed in with the keys; 0 in the FIRST step, where
-// AddToAccXZW0 overwrites acc (xzw.cpp:380).
-// How a party pass obtains d_i of an XZW step after the first (xzw.cpp:322-325),
-// which is the same for all k parties: the first party computes it and stores
-// it to the gate's scratch, later parties load it back.
-enum DMode { D_COMPUTE = 0, D_STORE = 1, D_LOAD = 2 };
-// The store/reload of d_i (MKACC_D_SCRATCH=1) is 1% faster at k = 2 but moves
-// 2*dg*N*4 bytes per gate-step through HBM (192 MB per launch at STD128_MKNTRU,
-// B = 4096: 2.7x the algorithmic traffic, PMC profiles/round1_v14_pmc.txt);
-// recomputing it per party keeps HBM traffic near the algorithmic bytes.
-#ifndef MKACC_D_SCRATCH
-#define MKACC_D_SCRATCH 0
-#endif
-constexpr bool kDScratch = MKACC_D_SCRATCH != 0;
-// f-part of the index pass as two key sums and one monomial product per slot
-#ifndef MKACC_SPLIT_F
-#define MKACC_SPLIT_F 1
-#endif
-constexpr bool kSplitF = MKACC_SPLIT_F != 0;
-
-template <int DG, int METHOD, bool FIRST, bool START, int DM>
+// START (digit 0): uj_u starts from acc_u * 2^32 (AddToAccXZW's acc + acctemp,
+// xzw.cpp:342-344; in Montgomery form, redc divides by 2^32) when the bound
+// allows, streamed in with the keys; 0 in the FIRST step, where AddToAccXZW0
+// overwrites acc (xzw.cpp:380).
+template <int DG, int METHOD, bool FIRST, bool START>
 __device__ __forceinline__ void mac_digit(const uint32_t (&g)[kRegs], int i, uint32_t u, uint64_t (&uj)[kRegs],
                                           uint64_t (&sv)[kRegs], __amdgpu_buffer_rsrc_t rk1,
                                           __amdgpu_buffer_rsrc_t rk2, __amdgpu_buffer_rsrc_t rks,
-                                          __amdgpu_buffer_rsrc_t rpk, __amdgpu_buffer_rsrc_t rin,
-                                          __amdgpu_buffer_rsrc_t rd, const uint2* psi, const Mono& mp,
-                                          const Mono& mn, uint32_t vo, uint32_t Q) {
-    const uint32_t polyB = kN * 4u;
-    constexpr bool kDLoad = DM == D_LOAD;
-    const uint32_t koff = (uint32_t)(2 * i) * polyB, doff = (uint32_t)i * polyB;
+                                          __amdgpu_buffer_rsrc_t rpk, __amdgpu_buffer_rsrc_t rin, const uint2* psi,
+                                          const Mono& mp, const Mono& mn, uint32_t vo, const Mod& m) {
+    using Bd = Bounds<DG, METHOD, FIRST>;
+    const uint32_t polyB = kN * 4u, Q = m.Q;
+    constexpr bool kAcc = START && Bd::kAccInSum;
+    const uint32_t koff = (uint32_t)(2 * i) * polyB;
     const uint32_t poff = (u * DG + (uint32_t)i) * polyB;
-    // loading d_i instead of two key words frees the registers for a deeper pipeline
-    constexpr int kPrefetch = DM == D_LOAD && DG <= 3 ? 3 : Prefetch<DG>::value;
+    constexpr int kPrefetch = Prefetch<DG>::value;
     KeyGroup kg[kPrefetch + 1];
     auto issue = [&](KeyGroup& t, int gq) {
         const uint32_t go = gq * 1024u;
-        t.k1 = kDLoad ? bload4(rd, vo, doff + go) : bload4(rk1, vo, koff + go);
+        t.k1 = bload4(rk1, vo, koff + go);
         t.pk = bload4(rpk, vo, poff + go);
-        if (METHOD == XZW && !kDLoad) t.k2 = bload4(rk2, vo, koff + go);
+        if (METHOD == XZW) t.k2 = bload4(rk2, vo, koff + go);
         if (FIRST) t.ks = bload4(rks, vo, koff + go);
-        if (START && !FIRST) t.acc = bload4(rin, vo, u * polyB + go);
+        if (kAcc) t.acc = bload4(rin, vo, u * polyB + go);
     };
 #pragma unroll
     for (int j = 0; j < kPrefetch; ++j) issue(kg[j], j);
@@ -248,22 +262,20 @@ __device__ __forceinline__ void mac_digit(const uint32_t (&g)[kRegs], int i, uin
     for (int gq = 0; gq < 8; ++gq) {
         if (gq + kPrefetch < 8) issue(kg[(gq + kPrefetch) % (kPrefetch + 1)], gq + kPrefetch);
         const KeyGroup& t = kg[gq % (kPrefetch + 1)];
-        u32x4 dd;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const int r = 4 * gq + e;
-            const uint32_t deff =
-                kDLoad ? t.k1[e] : key_eff<METHOD, FIRST>(t.k1[e], t.k2[e], t.ks[e], psi, mp, mn, r, Q);
-            dd[e] = deff;
-            uj[r] = mad64(g[r], deff, START ? (uint64_t)(FIRST ? 0u : t.acc[e]) : uj[r]);
+            const uint32_t deff = key_eff<METHOD, FIRST, Bd::kD>(t.k1[e], t.k2[e], t.ks[e], psi, mp, mn, r, Q);
+            const uint64_t base = kAcc ? mad64(t.acc[e], m.r32, 0) : (START ? 0ull : uj[r]);
+            uj[r] = mad64(g[r], deff, base);
             sv[r] = mad64(g[r], t.pk[e], sv[r]);
         }
-        if (DM == D_STORE) bstore4(dd, rd, vo, doff + gq * 1024u);
         sched_fence();
     }
 }
 
 // w += h * f_i                                  (xzw.cpp:281-288)
+// (first step, and XZW_B: f-words reduced to canonical, Bounds' f-part bound)
 template <int DG, int METHOD, bool FIRST>
 __device__ __forceinline__ void mac_index(const uint32_t (&h)[kRegs], int i, uint64_t (&w)[kRegs],
                                           __amdgpu_buffer_rsrc_t rk1, __amdgpu_buffer_rsrc_t rk2,
@@ -288,7 +300,7 @@ __device__ __forceinline__ void mac_index(const uint32_t (&h)[kRegs], int i, uin
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const int r = 4 * gq + e;
-            const uint32_t feff = key_eff<METHOD, FIRST>(t.k1[e], t.k2[e], t.ks[e], psi, mp, mn, r, Q);
+            const uint32_t feff = key_eff<METHOD, FIRST, 1>(t.k1[e], t.k2[e], t.ks[e], psi, mp, mn, r, Q);
             w[r] = mad64(h[r], feff, w[r]);
         }
         sched_fence();
@@ -296,9 +308,10 @@ __device__ __forceinline__ void mac_index(const uint32_t (&h)[kRegs], int i, uin
 }
 
 // XZW steps after the first: f_i = ev1'_i - ev2'_i X^-c (xzw.cpp:322-325) is
-// linear in the keys, so  sum_i h_i f_i = sum_i h_i ev1'_i - X^-c sum_i h_i ev2'_i:
-// two lazy sums per slot here and ONE monomial product per slot after the
-// last digit (mac_index_finish) instead of one per slot and digit.
+// linear in the keys, so with the stored ev1 + ev2:
+//   sum_i h_i f_i = sum_i h_i (ev1 + ev2)'_i + (X^(N-c) - 1) sum_i h_i ev2'_i
+// two lazy sums per slot here and ONE monomial product per slot after the last
+// digit (step_body) instead of one per slot and digit.
 template <int DG>
 __device__ __forceinline__ void mac_index_split(const uint32_t (&h)[kRegs], int i, uint64_t (&w)[kRegs],
                                                 uint64_t (&w2)[kRegs], __amdgpu_buffer_rsrc_t rk1,
@@ -327,25 +340,7 @@ __device__ __forceinline__ void mac_index_split(const uint32_t (&h)[kRegs], int 
         sched_fence();
     }
 }
-// w - X^-c * w2 per slot (mn holds -X^-c), as a lazy sum below 2^58
-// (w2 < DG * 4Q * Q <= 16 Q^2)
-__device__ __forceinline__ void mac_index_finish(uint64_t (&w)[kRegs], const uint64_t (&w2)[kRegs],
-                                                 const uint2* psi, const Mono& mn, const Mod& m) {
-#pragma unroll
-    for (int r = 0; r < kRegs; ++r) {
-        w[r] += mul_shoup_lazy(reduce58(w2[r], m), mn.at(psi, r), m.Q);   // [0, 2Q)
-        if ((r & 7) == 7) sched_fence();
-    }
-}
 
-// One accumulator step for one gate per wavefront.
-//   FIRST:  AddToAccXZW0 (mk-acc-xzw.cpp:347-381 / xzw_B.cpp:333-381): acc <- HbProd(acc)
-//   else:   AddToAccXZW  (mk-acc-xzw.cpp:292-345 / xzw_B.cpp:281-330):
-//           acc <- acc + HbProd(acc * (X^c - 1))
-// HbProd is mk-acc-xzw.cpp:231-290, register resident: the per-slot sums
-// uj_u = sum_i g_i d_i, sumV = sum_u sum_i g_i P[u][i] and w = sum_i h_i f_i are
-// lazy 64-bit accumulators (v_mad_u64_u32) reduced once; all sums are exact
-// mod Q, so the reordering is bit-exact.
 // Per-wave state shared by the passes of one step.
 struct StepCtx {
     const Tables tb;
@@ -356,22 +351,21 @@ struct StepCtx {
     SddConsts sd;
     Mono mp, mn;
     uint32_t l, vo;
-    __amdgpu_buffer_rsrc_t rin, rout, rk1, rk2, rks, rpk, rd;
+    __amdgpu_buffer_rsrc_t rin, rout, rk1, rk2, rks, rpk;
 };
 
 // One party u of HbProd (mk-acc-xzw.cpp:245-270) fused with AddToAccXZW's
 // rotation and final add (xzw.cpp:336-344):
 //   uj_u = (FIRST ? 0 : acc_u) + sum_i NTT(g_i) * d_i,   g = SDD(iNTT(acc_u * (X^c - 1)))
 //   sv  += sum_i NTT(g_i) * P[u][i]
-// Party `index` is processed last (LAST): its sum stays in registers (`keep`)
-// and receives the f-part of HbProd before the single store.
-template <int DG, int METHOD, bool FIRST, bool LAST, int DM>
+// Party `index` is processed last (LAST): its lazy sum stays in registers
+// (`uj`, folded) and receives the f-part of HbProd before the single store.
+template <int DG, int METHOD, bool FIRST, bool LAST>
 __device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_t (&sv)[kRegs],
-                                           uint32_t (&keep)[kRegs]) {
-    constexpr int kDigitUnroll = 1;
+                                           uint64_t (&uj)[kRegs]) {
+    using Bd = Bounds<DG, METHOD, FIRST>;
     const uint32_t Q = s.m.Q, polyB = kN * 4u;
     uint32_t x[kRegs];
-    uint64_t uj[kRegs];
 #pragma unroll
     for (int gq = 0; gq < 8; ++gq) {
         const u32x4 t = bload4(s.rin, s.vo, u * polyB + gq * 1024u);
@@ -379,18 +373,15 @@ __device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_
     }
     if (!FIRST) {
         // acctemp = acc * (X^c - 1)                     (xzw.cpp:336-338)
-        // x in [0, 2Q) -> x*X^c - x + 2Q in (0, 4Q) -> [0, 2Q)
+        // one Shoup product with the psi^e - 1 table entry: [0, 2Q) for any x
 #pragma unroll
         for (int r0 = 0; r0 < kRegs; r0 += 8) {
 #pragma unroll
-            for (int r = r0; r < r0 + 8; ++r) {
-                const uint32_t y = mul_shoup_lazy(x[r], s.mp.at(s.tb.psi, r), Q) + 2u * Q - x[r];
-                x[r] = min(y, y - 2u * Q);
-            }
+            for (int r = r0; r < r0 + 8; ++r) x[r] = mul_shoup_lazy(x[r], s.mp.at(s.tb.psi, r), Q);
             sched_fence();
         }
     }
-    ntt_inv_noscale(x, s.lds, s.tw_inv, s.tb.twi, s.l, Q);
+    ntt_inv(x, s.lds, s.tw_inv, s.tb.twi, s.l, Q);
     // SignedDigitDecompose (mk-acc.cpp:54-80): digit 1 -> x, digits 2.. packed
     PackedDigits<DG> pd;
 #pragma unroll
@@ -398,49 +389,44 @@ __device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_
         x[r] = pd.put(r, sdd_offset(x[r], s.sd), s.sd);
         if ((r & 7) == 7) sched_fence();
     }
-    ntt_fwd(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, s.l, Q);
+    ntt_fwd(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, s.l, Q, s.m.m1);
     digit_range<DG>(x, Q);
-    mac_digit<DG, METHOD, FIRST, true, DM>(x, 0, u, uj, sv, s.rk1, s.rk2, s.rks, s.rpk, s.rin, s.rd, s.tb.psi, s.mp,
-                                       s.mn, s.vo, Q);
-#pragma unroll kDigitUnroll
+    mac_digit<DG, METHOD, FIRST, true>(x, 0, u, uj, sv, s.rk1, s.rk2, s.rks, s.rpk, s.rin, s.tb.psi, s.mp, s.mn,
+                                       s.vo, s.m);
+#pragma unroll 1
     for (int i = 1; i < DG; ++i) {
 #pragma unroll
         for (int r = 0; r < kRegs; ++r) x[r] = pd.get(r, i + 1, s.sd);
-        ntt_fwd(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, s.l, Q);
+        ntt_fwd(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, s.l, Q, s.m.m1);
         digit_range<DG>(x, Q);
-        mac_digit<DG, METHOD, FIRST, false, DM>(x, i, u, uj, sv, s.rk1, s.rk2, s.rks, s.rpk, s.rin, s.rd, s.tb.psi,
-                                            s.mp, s.mn, s.vo, Q);
+        mac_digit<DG, METHOD, FIRST, false>(x, i, u, uj, sv, s.rk1, s.rk2, s.rks, s.rpk, s.rin, s.tb.psi, s.mp,
+                                            s.mn, s.vo, s.m);
     }
-    // acc_u <- uj_u (canonical); sumV reduced per party
+    if (LAST) {
+        // the index party's sum continues into the f-part (step_body)
+#pragma unroll
+        for (int r = 0; r < kRegs; ++r) uj[r] = fold64(uj[r], s.m.r32);
+        return;
+    }
+    // acc_u <- redc(uj_u) (+ acc_u when it is not in the sum), in [0, 2Q)
 #pragma unroll
     for (int gq = 0; gq < 8; ++gq) {
         u32x4 t;
+        if constexpr (!Bd::kAccInSum && !FIRST) t = bload4(s.rin, s.vo, u * polyB + gq * 1024u);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const int r = 4 * gq + e;
-            t[e] = reduce58_lazy(uj[r], s.m);
-            // sumV: a full reduction only before its iNTT; in between, folding the
-            // high word (hi * 2^32 mod Q, < 2^53) keeps the next party's DG <= 3
-            // products under reduce58's 2^58
-            if (LAST || DG > 3)
-                sv[r] = reduce58(sv[r], s.m);
-            else
-                sv[r] = mad64((uint32_t)(sv[r] >> 32), s.m.r32, (uint32_t)sv[r]);
-            if (LAST) keep[r] = t[e];
+            uint32_t v = redc(uj[r], Q, s.m.qinv);
+            if constexpr (!Bd::kAccInSum && !FIRST) {
+                v += t[e];
+                v = min(v, v - 2u * Q);
+            }
+            t[e] = v;
         }
-        if (!LAST) bstore4(t, s.rout, s.vo, u * polyB + gq * 1024u);
+        bstore4(t, s.rout, s.vo, u * polyB + gq * 1024u);
     }
 }
 
-// One accumulator step for one gate per wavefront.
-//   FIRST:  AddToAccXZW0 (mk-acc-xzw.cpp:347-381 / xzw_B.cpp:333-381): acc <- HbProd(acc)
-//   else:   AddToAccXZW  (mk-acc-xzw.cpp:292-345 / xzw_B.cpp:281-330):
-//           acc <- acc + HbProd(acc * (X^c - 1))
-// HbProd is mk-acc-xzw.cpp:231-290, register resident: the per-slot sums
-// uj_u = sum_i g_i d_i, sumV = sum_u sum_i g_i P[u][i] and w = sum_i h_i f_i are
-// lazy 64-bit accumulators (v_mad_u64_u32) reduced once; all sums are exact
-// mod Q, so the reordering (parties in the order index+1, ..., index) is
-// bit-exact.
 template <int DG, int METHOD, bool FIRST>
 __device__ __forceinline__ void step_body(const StepCtx& s, uint32_t k, uint32_t index);
 
@@ -465,7 +451,7 @@ __global__ __launch_bounds__(kThreads, 2) void mk_step_kernel(StepArgs a) {
                     a.m,
                     a.sd,
                     make_mono(c, l),
-                    // X^-c in the first step; -X^-c = X^(N-c) in the later XZW steps (key_eff)
+                    // X^-c in the first step; X^(N-c) = -X^-c in the later XZW steps (key_eff)
                     make_mono(FIRST || METHOD != XZW ? cneg : (cneg + kN) & (2u * kN - 1u), l),
                     l,
                     l * 16u,
@@ -474,80 +460,97 @@ __global__ __launch_bounds__(kThreads, 2) void mk_step_kernel(StepArgs a) {
                     make_rsrc(a.key1, DG * 2 * polyB),
                     make_rsrc(a.key2, DG * 2 * polyB),
                     make_rsrc(a.keys, DG * 2 * polyB),
-                    make_rsrc(a.pkey, k * DG * polyB),
-                    make_rsrc(a.deff + (size_t)gate * DG * kN, DG * polyB)};
+                    make_rsrc(a.pkey, k * DG * polyB)};
     step_body<DG, METHOD, FIRST>(s, k, a.index);
 }
 
+// One accumulator step for one gate per wavefront.
+//   FIRST:  AddToAccXZW0 (mk-acc-xzw.cpp:347-381 / xzw_B.cpp:333-381): acc <- HbProd(acc)
+//   else:   AddToAccXZW  (mk-acc-xzw.cpp:292-345 / xzw_B.cpp:281-330):
+//           acc <- acc + HbProd(acc * (X^c - 1))
+// HbProd is mk-acc-xzw.cpp:231-290, register resident: the per-slot sums
+// uj_u = sum_i g_i d_i, sumV = sum_u sum_i g_i P[u][i] and w = sum_i h_i f_i are
+// lazy 64-bit accumulators (v_mad_u64_u32) reduced once (Montgomery); all sums
+// are exact mod Q, so the reordering (parties in the order index+1, ..., index)
+// is bit-exact.
 template <int DG, int METHOD, bool FIRST>
 __device__ __forceinline__ void step_body(const StepCtx& s, uint32_t k, uint32_t index) {
-    // no digit unrolling: at DG = 2 unrolling the f-part loop spilled ~250 VGPRs
-    // (-Rpass-analysis=kernel-resource-usage, mkfhe_amd/lib/resource_usage.txt)
-    constexpr int kDigitUnroll = 1;
+    using Bd = Bounds<DG, METHOD, FIRST>;
     const uint32_t Q = s.m.Q;
     const uint32_t l = s.l;
     const uint32_t polyB = kN * 4u;
     uint64_t sv[kRegs];
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) sv[r] = 0;
-    uint32_t keep[kRegs];
-    if constexpr (METHOD == XZW && !FIRST && kDScratch) {
-        // d_i is the same for all parties: the first pass computes and stores
-        // it, the later ones load it (k == 1: the single pass computes it)
-        if (k == 1) {
-            party_pass<DG, METHOD, FIRST, true, D_COMPUTE>(s, index, sv, keep);
-        } else {
-            party_pass<DG, METHOD, FIRST, false, D_STORE>(s, index + 1 < k ? index + 1 : index + 1 - k, sv, keep);
-            for (uint32_t t = 2; t < k; ++t)
-                party_pass<DG, METHOD, FIRST, false, D_LOAD>(s, index + t < k ? index + t : index + t - k, sv, keep);
-            party_pass<DG, METHOD, FIRST, true, D_LOAD>(s, index, sv, keep);
+    uint64_t w[kRegs];
+    // sumV grows by kSvParty (units of Q^2) per party; fold it before it could
+    // pass 32 (fold64 leaves < 2)
+    int svb = 0;
+    for (uint32_t t = 1; t < k; ++t) {
+        party_pass<DG, METHOD, FIRST, false>(s, index + t < k ? index + t : index + t - k, sv, w);
+        svb += Bd::kSvParty;
+        if (svb + Bd::kSvParty > 32) {
+#pragma unroll
+            for (int r = 0; r < kRegs; ++r) sv[r] = fold64(sv[r], s.m.r32);
+            svb = 2;
         }
-    } else {
-        for (uint32_t t = 1; t < k; ++t) party_pass<DG, METHOD, FIRST, false, D_COMPUTE>(s, index + t < k ? index + t : index + t - k, sv,
-                                                                 keep);
-        party_pass<DG, METHOD, FIRST, true, D_COMPUTE>(s, index, sv, keep);
+    }
+    party_pass<DG, METHOD, FIRST, true>(s, index, sv, w);
+    if constexpr (!Bd::kAccInSum && !FIRST) {
+        // acc[index] joins the f-part sum (Bounds: < 4 Q^2 with the folded party sum)
+#pragma unroll
+        for (int gq = 0; gq < 8; ++gq) {
+            const u32x4 t = bload4(s.rin, s.vo, index * polyB + gq * 1024u);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) w[4 * gq + e] = mad64(t[e], s.m.r32, w[4 * gq + e]);
+        }
     }
 
     // second half of HbProd: iNTT(sumV) -> SDD -> NTT -> acc[index] += <., f>
     uint32_t x[kRegs];
 #pragma unroll
-    for (int r = 0; r < kRegs; ++r) x[r] = (uint32_t)sv[r];
-    ntt_inv_noscale(x, s.lds, s.tw_inv, s.tb.twi, l, Q);
+    for (int r = 0; r < kRegs; ++r) x[r] = redc(sv[r], Q, s.m.qinv);
+    ntt_inv(x, s.lds, s.tw_inv, s.tb.twi, l, Q);
     PackedDigits<DG> pd;
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) {
         x[r] = pd.put(r, sdd_offset(x[r], s.sd), s.sd);
         if ((r & 7) == 7) sched_fence();
     }
-    uint64_t w[kRegs];
-#pragma unroll
-    for (int r = 0; r < kRegs; ++r) w[r] = keep[r];
-    constexpr bool kSplit = METHOD == XZW && !FIRST && kSplitF;
+    constexpr bool kSplit = METHOD == XZW && !FIRST;
     uint64_t w2[kSplit ? kRegs : 1];
     if constexpr (kSplit) {
 #pragma unroll
         for (int r = 0; r < kRegs; ++r) w2[r] = 0;
     }
-#pragma unroll kDigitUnroll
+#pragma unroll 1
     for (int i = 0; i < DG; ++i) {
         if (i > 0) {
 #pragma unroll
             for (int r = 0; r < kRegs; ++r) x[r] = pd.get(r, i + 1, s.sd);
         }
-        ntt_fwd(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, l, Q);
+        ntt_fwd(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, l, Q, s.m.m1);
         digit_range<DG>(x, Q);
         if constexpr (kSplit)
             mac_index_split<DG>(x, i, w, w2, s.rk1, s.rk2, s.vo);
         else
             mac_index<DG, METHOD, FIRST>(x, i, w, s.rk1, s.rk2, s.rks, s.tb.psi, s.mp, s.mn, s.vo, Q);
     }
-    if constexpr (kSplit) mac_index_finish(w, w2, s.tb.psi, s.mn, s.m);
     const uint32_t ioff = index * polyB;
 #pragma unroll
     for (int gq = 0; gq < 8; ++gq) {
         u32x4 t;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) t[e] = reduce58_lazy(w[4 * gq + e], s.m);
+        for (int e = 0; e < 4; ++e) {
+            const int r = 4 * gq + e;
+            uint32_t v = redc(w[r], Q, s.m.qinv);                                   // [0, 2Q)
+            if constexpr (kSplit) {
+                // + (X^(N-c) - 1) * sum_i h_i ev2'_i
+                v += mul_shoup_lazy(redc(w2[r], Q, s.m.qinv), s.mn.at(s.tb.psi, r), Q);   // [0, 4Q)
+                v = min(v, v - 2u * Q);
+            }
+            t[e] = v;
+        }
         bstore4(t, s.rout, s.vo, ioff + gq * 1024u);
     }
 }
@@ -585,7 +588,8 @@ __global__ void eval_to_c4_kernel(const uint32_t* __restrict__ in, uint32_t* __r
 
 // Key upload from device memory: reference layout [k][nk][n+1][dg][2][N] (EVAL,
 // u32 or u64 words) -> device layout [k][n+1][nk][dg][2][N] in C4 order, times
-// N^-1 (s, sp).  pkey [k][dg][N] is the same map with nk = n1 = 1.
+// N^-1 2^32 (s, sp; StepArgs).  MKNTRU (nk = 2): the ev1 words of the steps i < n
+// become ev1 + ev2.  pkey [k][dg][N] is the same map with nk = n1 = 1.
 template <typename W>
 __global__ void key_layout_kernel(const W* __restrict__ src, uint32_t* __restrict__ dst, size_t npolys, uint32_t nk,
                                   uint32_t n1, uint32_t dg2, uint32_t Q, uint32_t s, uint32_t sp,
@@ -601,7 +605,13 @@ __global__ void key_layout_kernel(const W* __restrict__ src, uint32_t* __restric
     const size_t dpoly = ((u * n1 + i) * nk + jj) * dg2 + dp;
     const uint64_t x = (uint64_t)src[idx];
     if (x >= Q) *bad = 1u;
-    dst[dpoly * kN + c4_index(j)] = mul_shoup((uint32_t)x, s, sp, Q);
+    uint32_t v = (uint32_t)x;
+    if (nk == 2 && jj == 0 && i + 1 < n1) {
+        // ev1 + ev2 (the ev2 word is range-checked by its own thread)
+        const uint64_t y = (uint64_t)src[idx + (size_t)n1 * dg2 * kN];
+        v = (uint32_t)((x + (y < Q ? y : 0)) % Q);
+    }
+    dst[dpoly * kN + c4_index(j)] = mul_shoup(v, s, sp, Q);
 }
 __global__ void c4_to_eval_kernel(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, size_t npoly,
                                   uint32_t s, uint32_t sp, uint32_t Q) {
@@ -616,7 +626,7 @@ __global__ void c4_to_eval_kernel(const uint32_t* __restrict__ in, uint32_t* __r
 
 __global__ __launch_bounds__(kThreads) void ntt_fwd_kernel(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
                                                             uint32_t count, const uint32_t* img, const uint2* twf,
-                                                            uint32_t Q) {
+                                                            uint32_t Q, uint32_t m1) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     load_image(smem, img);
     const Tables tb = tables(smem, img);
@@ -627,7 +637,7 @@ __global__ __launch_bounds__(kThreads) void ntt_fwd_kernel(const uint32_t* __res
     uint32_t x[kRegs];
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) x[r] = src[jA(l, r)];
-    ntt_fwd(x, smem + kLdsTabWords + wv * kLdsWords, twf, tb.twf, tb.twfc, l, Q);
+    ntt_fwd(x, smem + kLdsTabWords + wv * kLdsWords, twf, tb.twf, tb.twfc, l, Q, m1);
     uint32_t* dst = out + (size_t)p * kN;
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) dst[jC(l, r)] = canon4(x[r], Q);
@@ -646,7 +656,7 @@ __global__ __launch_bounds__(kThreads) void ntt_inv_kernel(const uint32_t* __res
     uint32_t x[kRegs];
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) x[r] = src[jC(l, r)];
-    ntt_inv_noscale(x, smem + kLdsTabWords + wv * kLdsWords, twi, tb.twi, l, Q);
+    ntt_inv(x, smem + kLdsTabWords + wv * kLdsWords, twi, tb.twi, l, Q);
     uint32_t* dst = out + (size_t)p * kN;
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) dst[jA(l, r)] = mul_shoup(x[r], ninv, ninvp, Q);
@@ -728,6 +738,7 @@ struct mkacc_ctx {
     Mod mod{};
     SddConsts sd{};
     uint32_t ninv = 0, ninvp = 0, nval = 0, nvalp = 0;
+    uint32_t kscale = 0, kscalep = 0;   // key words: N^-1 2^32 mod Q and its companion
     hipStream_t stream = nullptr;
     uint2* d_twf = nullptr;
     uint2* d_twi = nullptr;
@@ -740,7 +751,6 @@ struct mkacc_ctx {
     uint32_t* d_acc0 = nullptr;
     uint32_t* d_acc1 = nullptr;
     uint32_t* d_cvals = nullptr;
-    uint32_t* d_deff = nullptr;   // [B][dg][N] step scratch (d_i shared by the k parties)
     // host-pointer API staging
     size_t io_B = 0;
     uint32_t* d_ct = nullptr;
@@ -793,14 +803,12 @@ int ensure_ws(mkacc_ctx* c, size_t B) {
     if (c->d_acc0) HIP_TRY(hipFree(c->d_acc0));
     if (c->d_acc1) HIP_TRY(hipFree(c->d_acc1));
     if (c->d_cvals) HIP_TRY(hipFree(c->d_cvals));
-    if (c->d_deff) HIP_TRY(hipFree(c->d_deff));
-    c->d_acc0 = c->d_acc1 = c->d_cvals = c->d_deff = nullptr;
+    c->d_acc0 = c->d_acc1 = c->d_cvals = nullptr;
     c->ws_B = 0;
     const size_t accw = B * c->p.k * (size_t)kN;
     HIP_TRY(hipMalloc(&c->d_acc0, accw * 4));
     HIP_TRY(hipMalloc(&c->d_acc1, accw * 4));
     HIP_TRY(hipMalloc(&c->d_cvals, B * c->p.k * (size_t)c->p.n * 4));
-    HIP_TRY(hipMalloc(&c->d_deff, B * c->dg * (size_t)kN * 4));
     c->ws_B = B;
     return MKACC_OK;
 }
@@ -825,7 +833,6 @@ uint32_t* launch_steps(mkacc_ctx* c, size_t B) {
             a.key2 = c->nk == 2 ? key_step(c, u, i, 1) : a.key1;
             a.keys = key_step(c, 0, n, 0);
             a.pkey = c->d_pkey;
-            a.deff = c->d_deff;
             a.tw_fwd = c->d_twf;
             a.tw_inv = c->d_twi;
             a.img = c->d_img;
@@ -906,7 +913,7 @@ int ensure_test_vector(mkacc_ctx* c) {
     HIP_TRY(hipMalloc(&c->d_tv, kN * 4));
     HIP_TRY(hipMemcpyAsync(din, rx.data(), kN * 4, hipMemcpyHostToDevice, c->stream));
     hipLaunchKernelGGL(ntt_fwd_kernel, dim3(1), dim3(kThreads), kStepLdsBytes, c->stream, din, dev, 1u, c->d_img,
-                       c->d_twf, c->mod.Q);
+                       c->d_twf, c->mod.Q, c->mod.m1);
     hipLaunchKernelGGL(eval_to_c4_kernel, dim3(kN / 256), dim3(256), 0, c->stream, dev, c->d_tv, (size_t)1, c->ninv,
                        c->ninvp, c->mod.Q, (uint32_t*)nullptr);
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -919,7 +926,7 @@ TailConsts tail_consts(const mkacc_ctx* c) {
     return TailConsts{c->mod.Q, (uint32_t)c->ks.qKS, c->ks.baseKS, c->dks};
 }
 
-const uint2* psi_image(const mkacc_ctx* c) { return reinterpret_cast<const uint2*>(c->d_img) + 2 * kTwlPairs; }
+const uint2* psi_image(const mkacc_ctx* c) { return reinterpret_cast<const uint2*>(c->d_img) + kPsiOff; }
 
 // tail on the C4 accumulators `acc`: extraction + ModSwitch + digits, then the
 // method's key switch into out_a (and out_b for MK-LWE)
@@ -983,13 +990,6 @@ int launch_gates(mkacc_ctx* c, const uint32_t* d_nand, const uint32_t* d_a1, con
     return MKACC_OK;
 }
 
-std::vector<uint2> shoup_table(const std::vector<uint64_t>& vals, uint64_t Q) {
-    std::vector<uint2> t(vals.size());
-    for (size_t i = 0; i < vals.size(); ++i)
-        t[i] = make_uint2((uint32_t)vals[i], (uint32_t)(((unsigned __int128)vals[i] << 32) / Q));
-    return t;
-}
-
 template <typename W>
 int upload_keys_impl(mkacc_ctx* c, const W* evk, const W* pkey) {
     if (!evk || !pkey) return fail(MKACC_E_ARG, "null key pointer");
@@ -997,9 +997,11 @@ int upload_keys_impl(mkacc_ctx* c, const W* evk, const W* pkey) {
     const uint32_t k = c->p.k, n = c->p.n, nk = c->nk, dg = c->dg;
     const size_t npolys = (size_t)k * nk * (n + 1) * dg * 2;
     std::vector<uint32_t> host((size_t)k * (n + 1) * key_block_words(c));
-    // reference [k][nk][n+1][dg][2][N]  ->  device [k][n+1][nk][dg][2][N] (C4, * N^-1)
+    // reference [k][nk][n+1][dg][2][N]  ->  device [k][n+1][nk][dg][2][N] (C4, * N^-1 2^32;
+    // MKNTRU: ev1 + ev2 in the ev1 blocks of the steps i < n, StepArgs)
     bool bad = false;
-    const uint64_t ninv = c->ninv;
+    const uint64_t ks = c->kscale;
+    const size_t ev2_stride = (size_t)(n + 1) * dg * 2 * kN;
     auto worker = [&](size_t p0, size_t p1) {
         for (size_t p = p0; p < p1; ++p) {
             size_t t = p;
@@ -1009,10 +1011,16 @@ int upload_keys_impl(mkacc_ctx* c, const W* evk, const W* pkey) {
             const size_t u = t;
             const W* src = evk + p * kN;
             uint32_t* dst = host.data() + (((u * (n + 1) + i) * nk + j) * dg * 2 + dp) * kN;
+            const bool comb = nk == 2 && j == 0 && i < n;
             for (uint32_t s = 0; s < (uint32_t)kN; ++s) {
-                const uint64_t x = (uint64_t)src[s];
+                uint64_t x = (uint64_t)src[s];
                 if (x >= Q) bad = true;
-                dst[c4_index(s)] = (uint32_t)((x * ninv) % Q);
+                if (comb) {
+                    const uint64_t y = (uint64_t)src[ev2_stride + s];
+                    if (y >= Q) bad = true;
+                    x = (x + y) % Q;
+                }
+                dst[c4_index(s)] = (uint32_t)((x % Q) * ks % Q);
             }
         }
     };
@@ -1026,7 +1034,7 @@ int upload_keys_impl(mkacc_ctx* c, const W* evk, const W* pkey) {
         for (uint32_t s = 0; s < (uint32_t)kN; ++s) {
             const uint64_t x = (uint64_t)pkey[p * kN + s];
             if (x >= Q) return fail(MKACC_E_RANGE, "pkey word not a canonical residue mod Q");
-            hp[p * kN + c4_index(s)] = (uint32_t)((x * ninv) % Q);
+            hp[p * kN + c4_index(s)] = (uint32_t)((x * ks) % Q);
         }
     HIP_TRY(hipSetDevice(c->device));
     if (!c->d_keys) HIP_TRY(hipMalloc(&c->d_keys, host.size() * 4));
@@ -1061,9 +1069,9 @@ int upload_keys_device_impl(mkacc_ctx* c, const W* d_evk, const W* d_pkey) {
         if (!c->d_keys) HIP_TRY(hipMalloc(&c->d_keys, ep * kN * 4));
         if (!c->d_pkey) HIP_TRY(hipMalloc(&c->d_pkey, pp * kN * 4));
         hipLaunchKernelGGL(key_layout_kernel<W>, grid(ep), dim3(tpb), 0, c->stream, d_evk, c->d_keys, ep, nk, n1,
-                           dg * 2, c->mod.Q, c->ninv, c->ninvp, c->d_bad);
+                           dg * 2, c->mod.Q, c->kscale, c->kscalep, c->d_bad);
         hipLaunchKernelGGL(key_layout_kernel<W>, grid(pp), dim3(tpb), 0, c->stream, d_pkey, c->d_pkey, pp, 1u, 1u,
-                           dg, c->mod.Q, c->ninv, c->ninvp, c->d_bad);
+                           dg, c->mod.Q, c->kscale, c->kscalep, c->d_bad);
     }
     HIP_TRY(hipGetLastError());
     uint32_t bad = 0;
@@ -1091,7 +1099,7 @@ int prim_launch(mkacc_ctx* c, const uint32_t* in, uint32_t* out, size_t count, s
     const dim3 grid((unsigned)((count + kWavesPerBlock - 1) / kWavesPerBlock)), block(kThreads);
     if (which == 0)
         hipLaunchKernelGGL(ntt_fwd_kernel, grid, block, lds, c->stream, din, dout, (uint32_t)count, c->d_img, c->d_twf,
-                           c->mod.Q);
+                           c->mod.Q, c->mod.m1);
     else if (which == 1)
         hipLaunchKernelGGL(ntt_inv_kernel, grid, block, lds, c->stream, din, dout, (uint32_t)count, c->d_img, c->d_twi,
                            c->mod.Q, c->ninv, c->ninvp);
@@ -1409,6 +1417,12 @@ int mkacc_create(const mkacc_params* pin, int device, mkacc_ctx** out) {
     c->mod.mu = (uint32_t)((1ull << 58) / p.Q);
     c->mod.r32 = (uint32_t)((1ull << 32) % p.Q);
     {
+        uint32_t qi = (uint32_t)p.Q;          // Q^-1 mod 2^32 by Newton (Q odd)
+        for (int it = 0; it < 5; ++it) qi *= 2u - (uint32_t)p.Q * qi;
+        c->mod.qinv = 0u - qi;
+        c->mod.m1 = (uint32_t)((1ull << 32) / p.Q);
+    }
+    {
         // offset-word digit decomposition constants (mkacc_device.hpp)
         const uint32_t b = (uint32_t)__builtin_ctz(p.baseG);
         uint64_t C = 0;
@@ -1422,6 +1436,8 @@ int mkacc_create(const mkacc_params* pin, int device, mkacc_ctx** out) {
     const uint64_t ninv = modinv(p.N, p.Q);
     c->ninv = (uint32_t)ninv;
     c->ninvp = (uint32_t)(((unsigned __int128)ninv << 32) / p.Q);
+    c->kscale = (uint32_t)(ninv * c->mod.r32 % p.Q);
+    c->kscalep = (uint32_t)(((unsigned __int128)c->kscale << 32) / p.Q);
     c->nval = p.N;
     c->nvalp = (uint32_t)(((unsigned __int128)p.N << 32) / p.Q);
 
@@ -1429,39 +1445,58 @@ int mkacc_create(const mkacc_params* pin, int device, mkacc_ctx** out) {
     HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIP_TRY(hipMalloc(&c->d_bad, 4));
     HIP_TRY(hipMemset(c->d_bad, 0, 4));
-    // NTT tables in the reference's order (transformnat-impl.h:705-760)
-    std::vector<uint64_t> tf(kN), ti(kN), pw(2 * kN);
+    // forward NTT table in the reference's order (transformnat-impl.h:705-760),
+    // powers psi^e and psi^-e (e < 2N) for the inverse transform and the monomials
+    const uint64_t Q = p.Q, psi = p.root, psii = modinv(psi, Q);
+    std::vector<uint64_t> tf(kN), pw(2 * kN), pwi(2 * kN);
     {
-        const uint64_t Q = p.Q, psi = p.root, psii = modinv(psi, Q);
-        uint64_t x = 1, xi = 1;
+        uint64_t x = 1;
         for (uint32_t i = 0; i < (uint32_t)kN; ++i) {
-            const uint32_t r = bit_reverse(i, kLogN);
-            tf[r] = x;
-            ti[r] = xi;
+            tf[bit_reverse(i, kLogN)] = x;
             x = mulmod(x, psi, Q);
-            xi = mulmod(xi, psii, Q);
         }
-        uint64_t e = 1;
-        for (uint32_t i = 0; i < 2u * kN; ++i) { pw[i] = e; e = mulmod(e, psi, Q); }
+        uint64_t e = 1, ei = 1;
+        for (uint32_t i = 0; i < 2u * kN; ++i) {
+            pw[i] = e;
+            pwi[i] = ei;
+            e = mulmod(e, psi, Q);
+            ei = mulmod(ei, psii, Q);
+        }
     }
-    auto htf = shoup_table(tf, p.Q), hti = shoup_table(ti, p.Q), hpw = shoup_table(pw, p.Q);
-    for (uint2& t : htf) t.x = 0u - t.x;   // forward pairs carry -w (ct_bfly_lazy's negated product)
+    auto pair = [Q](uint64_t w) { return make_uint2((uint32_t)w, (uint32_t)(((unsigned __int128)w << 32) / Q)); };
+    auto npair = [&](uint64_t w) { uint2 t = pair(w); t.x = 0u - t.x; return t; };   // ct_bfly_lazy's -w
+    std::vector<uint2> htf(kN), hti(32, make_uint2(0, 0));
+    for (int i = 0; i < kN; ++i) htf[i] = npair(tf[i]);
+    // inverse pass 1 (ntt_inv): bit b < 5, t < 2^b -> psi^-(t 2^(11-b))
+    for (int b = 0; b < 5; ++b)
+        for (int t = 0; t < (1 << b); ++t) hti[(1 << b) + t] = npair(pwi[(size_t)t << (11 - b)]);
     HIP_TRY(hipMalloc(&c->d_twf, htf.size() * sizeof(uint2)));
     HIP_TRY(hipMalloc(&c->d_twi, hti.size() * sizeof(uint2)));
-    // LDS image: per-lane twiddle runs of both directions + swizzled psi table
+    // table image (kImgPairs, layout at StepArgs / ntt_inv)
     std::vector<uint2> img(kImgPairs);
-    for (int dir = 0; dir < 2; ++dir) {
-        const std::vector<uint2>& T = dir == 0 ? htf : hti;
-        uint2* L = img.data() + dir * kTwlPairs;
+    {
+        uint2* F = img.data();
         for (int st = 5; st <= 9; ++st) {
             const int NP = 1 << (st - 5);
             for (int lhi = 0; lhi < 32; ++lhi)
-                for (int m = 0; m < NP; ++m) L[twl_off(st) + 32 * m + lhi] = T[(1 << st) + lhi * NP + m];
+                for (int m = 0; m < NP; ++m) F[twl_off(st) + 32 * m + lhi] = htf[(1 << st) + lhi * NP + m];
         }
         for (int ln = 0; ln < 64; ++ln)
-            for (int m = 0; m < 16; ++m) L[kTwlC + 64 * m + ln] = T[1024 + 16 * ln + m];
+            for (int m = 0; m < 16; ++m) F[kTwlC + 64 * m + ln] = htf[1024 + 16 * ln + m];
+        uint2* I = img.data() + kTwlPairs;
+        for (int b = 5; b <= 9; ++b)
+            for (int m = 0; m < (1 << (b - 5)); ++m)
+                for (int l31 = 0; l31 < 32; ++l31)
+                    I[twl_off(b) + 32 * m + l31] = npair(pwi[(size_t)(l31 | (m << 5)) << (11 - b)]);
+        for (int m = 0; m < 16; ++m)
+            for (int ln = 0; ln < 64; ++ln) I[kTwlC + 64 * m + ln] = npair(pwi[(size_t)((m << 6) | ln) << 1]);
+        for (int r = 0; r < 32; ++r)
+            for (int ln = 0; ln < 64; ++ln) I[kTwlPairs + 64 * r + ln] = pair(pwi[(r << 6) | ln]);
+        for (uint32_t e = 0; e < 2u * kN; ++e) {
+            img[kPsiOff + psi_pos(e)] = pair(pw[e]);
+            img[kPsm1Off + psi_pos(e)] = pair((pw[e] + Q - 1) % Q);
+        }
     }
-    for (uint32_t e = 0; e < 2u * kN; ++e) img[2 * kTwlPairs + psi_pos(e)] = hpw[e];
     HIP_TRY(hipMalloc(&c->d_img, img.size() * sizeof(uint2)));
     HIP_TRY(hipMemcpy(c->d_twf, htf.data(), htf.size() * sizeof(uint2), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->d_twi, hti.data(), hti.size() * sizeof(uint2), hipMemcpyHostToDevice));
@@ -1475,7 +1510,7 @@ void mkacc_destroy(mkacc_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (void* p : {(void*)c->d_twf, (void*)c->d_twi, (void*)c->d_img, (void*)c->d_keys, (void*)c->d_pkey,
-                    (void*)c->d_acc0, (void*)c->d_acc1, (void*)c->d_cvals, (void*)c->d_deff, (void*)c->d_ct,
+                    (void*)c->d_acc0, (void*)c->d_acc1, (void*)c->d_cvals, (void*)c->d_ct,
                     (void*)c->d_io, (void*)c->d_ksk, (void*)c->d_lweA, (void*)c->d_lweB, (void*)c->d_tv,
                     (void*)c->d_digits, (void*)c->d_bh, (void*)c->d_gin, (void*)c->d_gout, (void*)c->d_wtwf,
                     (void*)c->d_wtwi, (void*)c->d_wpsi, (void*)c->d_wkeys, (void*)c->d_wpkey, (void*)c->d_wacc0,

@@ -114,7 +114,7 @@ __global__ __launch_bounds__(256) void extract_kernel(const uint32_t* __restrict
     if (p >= npoly) return;
     uint32_t x[kRegs];
     load_c4(x, acc + (size_t)p * kN, l);
-    ntt_inv_noscale(x, smem + wv * kLdsWords, tw_inv, twl_inv, l, tc.Q);
+    ntt_inv(x, smem + wv * kLdsWords, tw_inv, twl_inv, l, tc.Q);
     uint8_t* dp = digits + (size_t)p * tc.dks * kN;
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) {
