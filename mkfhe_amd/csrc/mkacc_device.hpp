@@ -282,6 +282,72 @@ __device__ __forceinline__ void fwd_stage_b(uint32_t (&x)[kRegs], const uint2* t
     }
 }
 
+// Per-lane twiddle streams, software-pipelined: the loads of chunk I+1 are
+// issued before the butterflies of chunk I (double-buffered 4-pair chunks: the
+// same 16 live twiddle VGPRs as one 8-pair chunk), and the first chunk is issued
+// before the LDS transpose that precedes the stream, so L1/L2 latency overlaps
+// arithmetic instead of stalling the wave.  A stream is a list of chunks
+// {stage, first pair m0, pair count}; LD / AP are the direction's load and
+// butterfly functors.
+#ifndef MKACC_TWPIPE
+#define MKACC_TWPIPE 1
+#endif
+struct TwChunk { int s, m0, cnt; };
+template <class SEQ, int I, class LD, class AP>
+__device__ __forceinline__ void tw_pipe(uint2 (&wa)[4], uint2 (&wb)[4], const LD& ld, const AP& ap) {
+    constexpr TwChunk c = SEQ::at(I);
+    if constexpr (I + 1 < SEQ::N) {
+        constexpr TwChunk n = SEQ::at(I + 1);
+        ld.template go<n.s, n.m0, n.cnt>((I + 1) % 2 ? wb : wa);
+    }
+    ap.template go<c.s, c.m0, c.cnt>(I % 2 ? wb : wa);
+    sched_fence();
+    if constexpr (I + 1 < SEQ::N) tw_pipe<SEQ, I + 1>(wa, wb, ld, ap);
+}
+// forward passes B (stages 5..9, layout B) and C (stage 10, layout C)
+struct FwdSeq {
+    static constexpr int N = 13;
+    static constexpr TwChunk at(int i) {
+        constexpr TwChunk c[N] = {{5, 0, 1},  {6, 0, 2},  {7, 0, 4},  {8, 0, 4},  {8, 4, 4},
+                                  {9, 0, 4},  {9, 4, 4},  {9, 8, 4},  {9, 12, 4}, {10, 0, 4},
+                                  {10, 4, 4}, {10, 8, 4}, {10, 12, 4}};
+        return c[i];
+    }
+};
+struct FwdLoad {
+    const uint2* twl;    // stages 5..9: + twl_off(s) + 32 m + (lane >> 1)
+    const uint2* tw10;   // stage 10: + 64 m + lane
+    __device__ __forceinline__ FwdLoad(const uint2* t, const uint2* t10, uint32_t lo)
+        : twl(t + (lo >> 1)), tw10(t10 + lo) {}
+    template <int S, int M0, int CNT>
+    __device__ __forceinline__ void go(uint2 (&w)[4]) const {
+#pragma unroll
+        for (int j = 0; j < CNT; ++j) w[j] = S < 10 ? twl[twl_off(S < 10 ? S : 5) + 32 * (M0 + j)] : tw10[64 * (M0 + j)];
+    }
+};
+struct FwdApply {
+    uint32_t (&x)[kRegs];
+    uint32_t* lds;
+    uint32_t l, Q, m1;
+    template <int S, int M0, int CNT>
+    __device__ __forceinline__ void go(const uint2 (&w)[4]) const {
+        if constexpr (S < 10) {
+            constexpr int H = 1 << (9 - S), SH = 10 - S;
+#pragma unroll
+            for (int r = 0; r < kRegs; ++r) {
+                if (r & H) continue;
+                const int m = r >> SH;
+                if (m < M0 || m >= M0 + CNT) continue;
+                ct_bfly_lazy(x[r], x[r + H], w[m - M0], Q);
+            }
+        } else {
+            if constexpr (M0 == 0) transpose<1, 2>(x, lds, l);
+#pragma unroll
+            for (int j = 0; j < CNT; ++j) ct_bfly_last(x[2 * (M0 + j)], x[2 * (M0 + j) + 1], w[j], Q, m1);
+        }
+    }
+};
+
 // Forward negacyclic NTT of one polynomial per wave, reference EVAL order.
 //   tw_g : reference forward table (pairs) in global memory, pass A reads it
 //          with scalar loads (wave-uniform indices 1..31)
@@ -304,9 +370,21 @@ __device__ __forceinline__ void ntt_fwd(uint32_t (&x)[kRegs], uint32_t* lds, con
         }
         sched_fence();
     }
+    const uint32_t lo = opaque_v(l);
+#if MKACC_TWPIPE
+    // passes B (stages 5..9, bits 5..1) and C (stage 10, bit 0), one twiddle stream
+    {
+        const FwdLoad ld(twl, tw10, lo);
+        const FwdApply ap{x, lds, l, Q, m1};
+        uint2 wa[4], wb[4];
+        ld.template go<5, 0, 1>(wa);
+        transpose<0, 1>(x, lds, l);
+        tw_pipe<FwdSeq, 0>(wa, wb, ld, ap);
+    }
+    return;
+#endif
     transpose<0, 1>(x, lds, l);
     // pass B: stages 5..9 (bits 5..1)
-    const uint32_t lo = opaque_v(l);
     const uint32_t lhi = lo >> 1;
     fwd_stage_b<5>(x, twl, lhi, Q);
     fwd_stage_b<6>(x, twl, lhi, Q);
@@ -403,6 +481,55 @@ __device__ __forceinline__ void inv_stage_d(uint32_t (&x)[kRegs], const uint2* t
     }
 }
 
+// inverse pass 2 (stages 5..9, layout D), bit 10 (layout A) and the twist
+struct InvSeq {
+    static constexpr int N = 21;
+    static constexpr TwChunk at(int i) {
+        constexpr TwChunk c[N] = {{5, 0, 1},   {6, 0, 2},   {7, 0, 4},   {8, 0, 4},   {8, 4, 4},   {9, 0, 4},
+                                  {9, 4, 4},   {9, 8, 4},   {9, 12, 4},  {10, 0, 4},  {10, 4, 4},  {10, 8, 4},
+                                  {10, 12, 4}, {11, 0, 4},  {11, 4, 4},  {11, 8, 4},  {11, 12, 4}, {11, 16, 4},
+                                  {11, 20, 4}, {11, 24, 4}, {11, 28, 4}};
+        return c[i];
+    }
+};
+struct InvLoad {
+    const uint2* t31;   // stages 5..9: + twl_off(s) + 32 m + (lane & 31)
+    const uint2* t64;   // bit 10: + kTwlC + 64 m + lane; twist: + kTwlPairs + 64 r + lane
+    __device__ __forceinline__ InvLoad(const uint2* twl, uint32_t lo) : t31(twl + (lo & 31u)), t64(twl + lo) {}
+    template <int S, int M0, int CNT>
+    __device__ __forceinline__ void go(uint2 (&w)[4]) const {
+#pragma unroll
+        for (int j = 0; j < CNT; ++j)
+            w[j] = S < 10 ? t31[twl_off(S < 10 ? S : 5) + 32 * (M0 + j)]
+                          : t64[(S == 10 ? kTwlC : kTwlPairs) + 64 * (M0 + j)];
+    }
+};
+struct InvApply {
+    uint32_t (&x)[kRegs];
+    uint32_t* lds;
+    uint32_t l, Q;
+    template <int S, int M0, int CNT>
+    __device__ __forceinline__ void go(const uint2 (&w)[4]) const {
+        if constexpr (S < 10) {
+            constexpr int H = 1 << (S - 5);
+#pragma unroll
+            for (int r = 0; r < kRegs; ++r) {
+                if (r & H) continue;
+                const int m = r & (H - 1);
+                if (m < M0 || m >= M0 + CNT) continue;
+                ct_bfly_lazy(x[r], x[r + H], w[m - M0], Q);
+            }
+        } else if constexpr (S == 10) {
+            if constexpr (M0 == 0) transpose<3, 0>(x, lds, l);
+#pragma unroll
+            for (int j = 0; j < CNT; ++j) ct_bfly_lazy(x[M0 + j], x[M0 + j + 16], w[j], Q);
+        } else {
+#pragma unroll
+            for (int j = 0; j < CNT; ++j) x[M0 + j] = mul_shoup(x[M0 + j], w[j].x, w[j].y, Q);
+        }
+    }
+};
+
 // Input residues in [0, 2Q), layout C; output canonical coefficients, layout A.
 __device__ __forceinline__ void ntt_inv(uint32_t (&x)[kRegs], uint32_t* lds, const uint2* tis, const uint2* twl,
                                         uint32_t l, uint32_t Q) {
@@ -425,8 +552,19 @@ __device__ __forceinline__ void ntt_inv(uint32_t (&x)[kRegs], uint32_t* lds, con
         }
         sched_fence();
     }
-    transpose<2, 3>(x, lds, l);
     const uint32_t lo = opaque_v(l);
+#if MKACC_TWPIPE
+    {
+        const InvLoad ld(twl, lo);
+        const InvApply ap{x, lds, l, Q};
+        uint2 wa[4], wb[4];
+        ld.template go<5, 0, 1>(wa);
+        transpose<2, 3>(x, lds, l);
+        tw_pipe<InvSeq, 0>(wa, wb, ld, ap);
+    }
+    return;
+#endif
+    transpose<2, 3>(x, lds, l);
     const uint32_t l31 = lo & 31u;
     inv_stage_d<5>(x, twl, l31, Q);
     inv_stage_d<6>(x, twl, l31, Q);

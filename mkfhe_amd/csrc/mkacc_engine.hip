@@ -224,10 +224,32 @@ __device__ __forceinline__ void digit_range(uint32_t (&x)[kRegs], uint32_t Q) {
 
 // Key words of one 4-register group of a MAC: software-pipelined kPrefetch
 // groups ahead so the L2 latency of the step's key block overlaps the arithmetic.
+#ifndef MKACC_PREFETCH3
+#define MKACC_PREFETCH3 1
+#endif
+#ifndef MKACC_KEY_AUX
+#define MKACC_KEY_AUX 0
+#endif
 template <int DG>
-struct Prefetch { static constexpr int value = DG <= 3 ? 1 : 0; };
+struct Prefetch { static constexpr int value = DG <= 3 ? MKACC_PREFETCH3 : 0; };
+// key-block loads (shared by every gate of the launch, streamed from L2)
+__device__ __forceinline__ u32x4 kload4(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    return __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, MKACC_KEY_AUX);
+}
 struct KeyGroup {
     u32x4 k1, k2, ks, pk, acc;
+    uint2 mono[4];   // X^(N-c) - 1 at the group's slots (XZW after the first step)
+};
+#ifndef MKACC_MONO_PREFETCH
+#define MKACC_MONO_PREFETCH 1
+#endif
+// per-wave resources of the MAC helpers
+struct StepRes {
+    __amdgpu_buffer_rsrc_t rin, rk1, rk2, rks, rpk;
+    const uint2* psi;
+    Mono mp, mn;
+    Mod m;
+    uint32_t vo;
 };
 
 // uj_u += g * d_i ; sv += g * P[u][i]          (xzw.cpp:263-269)
@@ -235,44 +257,55 @@ struct KeyGroup {
 // xzw.cpp:342-344; in Montgomery form, redc divides by 2^32) when the bound
 // allows, streamed in with the keys; 0 in the FIRST step, where AddToAccXZW0
 // overwrites acc (xzw.cpp:380).
+// The caller issues the first kPrefetch key groups (issue()) BEFORE the digit's
+// forward NTT, so the MAC starts on loaded keys; run() streams the rest.
+#ifndef MKACC_EARLY_KEYS
+#define MKACC_EARLY_KEYS 0
+#endif
 template <int DG, int METHOD, bool FIRST, bool START>
-__device__ __forceinline__ void mac_digit(const uint32_t (&g)[kRegs], int i, uint32_t u, uint64_t (&uj)[kRegs],
-                                          uint64_t (&sv)[kRegs], __amdgpu_buffer_rsrc_t rk1,
-                                          __amdgpu_buffer_rsrc_t rk2, __amdgpu_buffer_rsrc_t rks,
-                                          __amdgpu_buffer_rsrc_t rpk, __amdgpu_buffer_rsrc_t rin, const uint2* psi,
-                                          const Mono& mp, const Mono& mn, uint32_t vo, const Mod& m) {
+struct DigitMac {
     using Bd = Bounds<DG, METHOD, FIRST>;
-    const uint32_t polyB = kN * 4u, Q = m.Q;
-    constexpr bool kAcc = START && Bd::kAccInSum;
-    const uint32_t koff = (uint32_t)(2 * i) * polyB;
-    const uint32_t poff = (u * DG + (uint32_t)i) * polyB;
-    constexpr int kPrefetch = Prefetch<DG>::value;
-    KeyGroup kg[kPrefetch + 1];
-    auto issue = [&](KeyGroup& t, int gq) {
+    static constexpr bool kAcc = START && Bd::kAccInSum;
+    static constexpr bool kMonoPf = MKACC_MONO_PREFETCH && METHOD == XZW && !FIRST;
+    static constexpr int kPrefetch = Prefetch<DG>::value;
+    static constexpr int kBuf = kPrefetch + 1;
+    const StepRes& sr;
+    uint32_t koff, poff, aoff;
+    __device__ __forceinline__ DigitMac(const StepRes& r, int i, uint32_t u)
+        : sr(r), koff((uint32_t)(2 * i) * (kN * 4u)), poff((u * DG + (uint32_t)i) * (kN * 4u)), aoff(u * (kN * 4u)) {}
+    __device__ __forceinline__ void issue(KeyGroup& t, int gq) const {
         const uint32_t go = gq * 1024u;
-        t.k1 = bload4(rk1, vo, koff + go);
-        t.pk = bload4(rpk, vo, poff + go);
-        if (METHOD == XZW) t.k2 = bload4(rk2, vo, koff + go);
-        if (FIRST) t.ks = bload4(rks, vo, koff + go);
-        if (kAcc) t.acc = bload4(rin, vo, u * polyB + go);
-    };
+        t.k1 = kload4(sr.rk1, sr.vo, koff + go);
+        t.pk = kload4(sr.rpk, sr.vo, poff + go);
+        if (METHOD == XZW) t.k2 = kload4(sr.rk2, sr.vo, koff + go);
+        if (FIRST) t.ks = kload4(sr.rks, sr.vo, koff + go);
+        if (kAcc) t.acc = bload4(sr.rin, sr.vo, aoff + go);
+        if (kMonoPf) {
 #pragma unroll
-    for (int j = 0; j < kPrefetch; ++j) issue(kg[j], j);
-#pragma unroll
-    for (int gq = 0; gq < 8; ++gq) {
-        if (gq + kPrefetch < 8) issue(kg[(gq + kPrefetch) % (kPrefetch + 1)], gq + kPrefetch);
-        const KeyGroup& t = kg[gq % (kPrefetch + 1)];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const int r = 4 * gq + e;
-            const uint32_t deff = key_eff<METHOD, FIRST, Bd::kD>(t.k1[e], t.k2[e], t.ks[e], psi, mp, mn, r, Q);
-            const uint64_t base = kAcc ? mad64(t.acc[e], m.r32, 0) : (START ? 0ull : uj[r]);
-            uj[r] = mad64(g[r], deff, base);
-            sv[r] = mad64(g[r], t.pk[e], sv[r]);
+            for (int e = 0; e < 4; ++e) t.mono[e] = sr.mn.at(sr.psi, 4 * gq + e);
         }
-        sched_fence();
     }
-}
+    __device__ __forceinline__ void run(const uint32_t (&g)[kRegs], uint64_t (&uj)[kRegs], uint64_t (&sv)[kRegs],
+                                        KeyGroup (&kg)[kBuf]) const {
+        const uint32_t Q = sr.m.Q;
+#pragma unroll
+        for (int gq = 0; gq < 8; ++gq) {
+            if (gq + kPrefetch < 8) issue(kg[(gq + kPrefetch) % kBuf], gq + kPrefetch);
+            const KeyGroup& t = kg[gq % kBuf];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int r = 4 * gq + e;
+                const uint32_t deff =
+                    kMonoPf ? from3q<Bd::kD>(t.k1[e] + mul_shoup_lazy(t.k2[e], t.mono[e], Q), Q)   // = key_eff
+                            : key_eff<METHOD, FIRST, Bd::kD>(t.k1[e], t.k2[e], t.ks[e], sr.psi, sr.mp, sr.mn, r, Q);
+                const uint64_t base = kAcc ? mad64(t.acc[e], sr.m.r32, 0) : (START ? 0ull : uj[r]);
+                uj[r] = mad64(g[r], deff, base);
+                sv[r] = mad64(g[r], t.pk[e], sv[r]);
+            }
+            sched_fence();
+        }
+    }
+};
 
 // w += h * f_i                                  (xzw.cpp:281-288)
 // (first step, and XZW_B: f-words reduced to canonical, Bounds' f-part bound)
@@ -287,9 +320,9 @@ __device__ __forceinline__ void mac_index(const uint32_t (&h)[kRegs], int i, uin
     KeyGroup kg[kPrefetch + 1];
     auto issue = [&](KeyGroup& t, int gq) {
         const uint32_t go = gq * 1024u;
-        t.k1 = bload4(rk1, vo, koff + go);
-        if (METHOD == XZW) t.k2 = bload4(rk2, vo, koff + go);
-        if (FIRST) t.ks = bload4(rks, vo, koff + go);
+        t.k1 = kload4(rk1, vo, koff + go);
+        if (METHOD == XZW) t.k2 = kload4(rk2, vo, koff + go);
+        if (FIRST) t.ks = kload4(rks, vo, koff + go);
     };
 #pragma unroll
     for (int j = 0; j < kPrefetch; ++j) issue(kg[j], j);
@@ -313,33 +346,33 @@ __device__ __forceinline__ void mac_index(const uint32_t (&h)[kRegs], int i, uin
 // two lazy sums per slot here and ONE monomial product per slot after the last
 // digit (step_body) instead of one per slot and digit.
 template <int DG>
-__device__ __forceinline__ void mac_index_split(const uint32_t (&h)[kRegs], int i, uint64_t (&w)[kRegs],
-                                                uint64_t (&w2)[kRegs], __amdgpu_buffer_rsrc_t rk1,
-                                                __amdgpu_buffer_rsrc_t rk2, uint32_t vo) {
-    const uint32_t polyB = kN * 4u;
-    const uint32_t koff = (uint32_t)(2 * i + 1) * polyB;
-    constexpr int kPrefetch = Prefetch<DG>::value;
-    KeyGroup kg[kPrefetch + 1];
-    auto issue = [&](KeyGroup& t, int gq) {
+struct SplitMac {
+    static constexpr int kPrefetch = Prefetch<DG>::value;
+    static constexpr int kBuf = kPrefetch + 1;
+    const StepRes& sr;
+    uint32_t koff;
+    __device__ __forceinline__ SplitMac(const StepRes& r, int i) : sr(r), koff((uint32_t)(2 * i + 1) * (kN * 4u)) {}
+    __device__ __forceinline__ void issue(KeyGroup& t, int gq) const {
         const uint32_t go = gq * 1024u;
-        t.k1 = bload4(rk1, vo, koff + go);
-        t.k2 = bload4(rk2, vo, koff + go);
-    };
-#pragma unroll
-    for (int j = 0; j < kPrefetch; ++j) issue(kg[j], j);
-#pragma unroll
-    for (int gq = 0; gq < 8; ++gq) {
-        if (gq + kPrefetch < 8) issue(kg[(gq + kPrefetch) % (kPrefetch + 1)], gq + kPrefetch);
-        const KeyGroup& t = kg[gq % (kPrefetch + 1)];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const int r = 4 * gq + e;
-            w[r] = mad64(h[r], t.k1[e], w[r]);
-            w2[r] = mad64(h[r], t.k2[e], w2[r]);
-        }
-        sched_fence();
+        t.k1 = kload4(sr.rk1, sr.vo, koff + go);
+        t.k2 = kload4(sr.rk2, sr.vo, koff + go);
     }
-}
+    __device__ __forceinline__ void run(const uint32_t (&h)[kRegs], uint64_t (&w)[kRegs], uint64_t (&w2)[kRegs],
+                                        KeyGroup (&kg)[kBuf]) const {
+#pragma unroll
+        for (int gq = 0; gq < 8; ++gq) {
+            if (gq + kPrefetch < 8) issue(kg[(gq + kPrefetch) % kBuf], gq + kPrefetch);
+            const KeyGroup& t = kg[gq % kBuf];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int r = 4 * gq + e;
+                w[r] = mad64(h[r], t.k1[e], w[r]);
+                w2[r] = mad64(h[r], t.k2[e], w2[r]);
+            }
+            sched_fence();
+        }
+    }
+};
 
 // Per-wave state shared by the passes of one step.
 struct StepCtx {
@@ -352,6 +385,7 @@ struct StepCtx {
     Mono mp, mn;
     uint32_t l, vo;
     __amdgpu_buffer_rsrc_t rin, rout, rk1, rk2, rks, rpk;
+    __device__ __forceinline__ StepRes res() const { return StepRes{rin, rk1, rk2, rks, rpk, tb.psi, mp, mn, m, vo}; }
 };
 
 // One party u of HbProd (mk-acc-xzw.cpp:245-270) fused with AddToAccXZW's
@@ -373,13 +407,14 @@ __device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_
     }
     if (!FIRST) {
         // acctemp = acc * (X^c - 1)                     (xzw.cpp:336-338)
-        // one Shoup product with the psi^e - 1 table entry: [0, 2Q) for any x
+        // one Shoup product with the psi^e - 1 table entry: [0, 2Q) for any x;
+        // the 32 table reads are issued while the accumulator loads are in flight
+        uint2 mw[kRegs];
 #pragma unroll
-        for (int r0 = 0; r0 < kRegs; r0 += 8) {
+        for (int r = 0; r < kRegs; ++r) mw[r] = s.mp.at(s.tb.psi, r);
+        sched_fence();
 #pragma unroll
-            for (int r = r0; r < r0 + 8; ++r) x[r] = mul_shoup_lazy(x[r], s.mp.at(s.tb.psi, r), Q);
-            sched_fence();
-        }
+        for (int r = 0; r < kRegs; ++r) x[r] = mul_shoup_lazy(x[r], mw[r], Q);
     }
     ntt_inv(x, s.lds, s.tw_inv, s.tb.twi, s.l, Q);
     // SignedDigitDecompose (mk-acc.cpp:54-80): digit 1 -> x, digits 2.. packed
@@ -389,18 +424,39 @@ __device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_
         x[r] = pd.put(r, sdd_offset(x[r], s.sd), s.sd);
         if ((r & 7) == 7) sched_fence();
     }
-    ntt_fwd(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, s.l, Q, s.m.m1);
-    digit_range<DG>(x, Q);
-    mac_digit<DG, METHOD, FIRST, true>(x, 0, u, uj, sv, s.rk1, s.rk2, s.rks, s.rpk, s.rin, s.tb.psi, s.mp, s.mn,
-                                       s.vo, s.m);
+    const StepRes sr = s.res();
+    {
+        const DigitMac<DG, METHOD, FIRST, true> mac(sr, 0, u);
+        KeyGroup kg[mac.kBuf];
+        if (MKACC_EARLY_KEYS) {
+#pragma unroll
+            for (int j = 0; j < mac.kPrefetch; ++j) mac.issue(kg[j], j);
+        }
+        ntt_fwd(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, s.l, Q, s.m.m1);
+        digit_range<DG>(x, Q);
+        if (!MKACC_EARLY_KEYS) {
+#pragma unroll
+            for (int j = 0; j < mac.kPrefetch; ++j) mac.issue(kg[j], j);
+        }
+        mac.run(x, uj, sv, kg);
+    }
 #pragma unroll 1
     for (int i = 1; i < DG; ++i) {
 #pragma unroll
         for (int r = 0; r < kRegs; ++r) x[r] = pd.get(r, i + 1, s.sd);
+        const DigitMac<DG, METHOD, FIRST, false> mac(sr, i, u);
+        KeyGroup kg[mac.kBuf];
+        if (MKACC_EARLY_KEYS) {
+#pragma unroll
+            for (int j = 0; j < mac.kPrefetch; ++j) mac.issue(kg[j], j);
+        }
         ntt_fwd(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, s.l, Q, s.m.m1);
         digit_range<DG>(x, Q);
-        mac_digit<DG, METHOD, FIRST, false>(x, i, u, uj, sv, s.rk1, s.rk2, s.rks, s.rpk, s.rin, s.tb.psi, s.mp,
-                                            s.mn, s.vo, s.m);
+        if (!MKACC_EARLY_KEYS) {
+#pragma unroll
+            for (int j = 0; j < mac.kPrefetch; ++j) mac.issue(kg[j], j);
+        }
+        mac.run(x, uj, sv, kg);
     }
     if (LAST) {
         // the index party's sum continues into the f-part (step_body)
@@ -507,6 +563,7 @@ __device__ __forceinline__ void step_body(const StepCtx& s, uint32_t k, uint32_t
     }
 
     // second half of HbProd: iNTT(sumV) -> SDD -> NTT -> acc[index] += <., f>
+    const StepRes sr = s.res();
     uint32_t x[kRegs];
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) x[r] = redc(sv[r], Q, s.m.qinv);
@@ -529,14 +586,32 @@ __device__ __forceinline__ void step_body(const StepCtx& s, uint32_t k, uint32_t
 #pragma unroll
             for (int r = 0; r < kRegs; ++r) x[r] = pd.get(r, i + 1, s.sd);
         }
-        ntt_fwd(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, l, Q, s.m.m1);
-        digit_range<DG>(x, Q);
-        if constexpr (kSplit)
-            mac_index_split<DG>(x, i, w, w2, s.rk1, s.rk2, s.vo);
-        else
+        if constexpr (kSplit) {
+            const SplitMac<DG> mac(sr, i);
+            KeyGroup kg[mac.kBuf];
+            if (MKACC_EARLY_KEYS) {
+#pragma unroll
+                for (int j = 0; j < mac.kPrefetch; ++j) mac.issue(kg[j], j);
+            }
+            ntt_fwd(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, l, Q, s.m.m1);
+            digit_range<DG>(x, Q);
+            if (!MKACC_EARLY_KEYS) {
+#pragma unroll
+                for (int j = 0; j < mac.kPrefetch; ++j) mac.issue(kg[j], j);
+            }
+            mac.run(x, w, w2, kg);
+        } else {
+            ntt_fwd(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, l, Q, s.m.m1);
+            digit_range<DG>(x, Q);
             mac_index<DG, METHOD, FIRST>(x, i, w, s.rk1, s.rk2, s.rks, s.tb.psi, s.mp, s.mn, s.vo, Q);
+        }
     }
     const uint32_t ioff = index * polyB;
+    uint2 mw[kSplit ? kRegs : 1];
+    if constexpr (kSplit) {
+#pragma unroll
+        for (int r = 0; r < kRegs; ++r) mw[r] = s.mn.at(s.tb.psi, r);
+    }
 #pragma unroll
     for (int gq = 0; gq < 8; ++gq) {
         u32x4 t;
@@ -546,7 +621,7 @@ __device__ __forceinline__ void step_body(const StepCtx& s, uint32_t k, uint32_t
             uint32_t v = redc(w[r], Q, s.m.qinv);                                   // [0, 2Q)
             if constexpr (kSplit) {
                 // + (X^(N-c) - 1) * sum_i h_i ev2'_i
-                v += mul_shoup_lazy(redc(w2[r], Q, s.m.qinv), s.mn.at(s.tb.psi, r), Q);   // [0, 4Q)
+                v += mul_shoup_lazy(redc(w2[r], Q, s.m.qinv), mw[r], Q);             // [0, 4Q)
                 v = min(v, v - 2u * Q);
             }
             t[e] = v;
@@ -716,12 +791,21 @@ __global__ void wide_key_layout_kernel(const W* __restrict__ src, uint64_t* __re
     dst[dpoly * kN + j] = wide::mul_shoup(x, r, rp, Q);
 }
 
+// MKACC_ONLY_DG=d (developer builds for ISA studies): instantiate one digit count
 StepFn step_fn(int dg, int method, bool first) {
     switch (dg) {
+#if !defined(MKACC_ONLY_DG) || MKACC_ONLY_DG == 2
         case 2: return pick_step<2>(method, first);
+#endif
+#if !defined(MKACC_ONLY_DG) || MKACC_ONLY_DG == 3
         case 3: return pick_step<3>(method, first);
+#endif
+#if !defined(MKACC_ONLY_DG) || MKACC_ONLY_DG == 4
         case 4: return pick_step<4>(method, first);
+#endif
+#if !defined(MKACC_ONLY_DG) || MKACC_ONLY_DG == 5
         case 5: return pick_step<5>(method, first);
+#endif
         default: return nullptr;
     }
 }
