@@ -19,7 +19,7 @@ uploads them straight from the received device buffer
 the data path ("weak" scaling: B gates per GPU).
 
 Proof of the timed run: after timing, every rank copies back the outputs of
-the first G gates of ITS timed batch and recomputes them with the CPU oracle
+G gates spread over ITS timed batch and recomputes them with the CPU oracle
 (oracle/, the checker) from the same inputs and keys; rank 0 reports
 `parity_checked` / `parity_mismatches` summed over ranks and the run fails on a
 mismatch.  At N = 1 those G gates, one per host core, are also the CPU
@@ -203,7 +203,7 @@ class OracleChecker:
 def run_rank(args, env: dict, make_engine, make_checker, torch_device: str, backend: str) -> dict | None:
     """Bench logic of one rank: key broadcast + device upload, this rank's shard
     of synthetic gates, warmup, barrier-bracketed timing of K steps, max over
-    ranks, the oracle check of the first G gates of the timed batch, and (rank 0)
+    ranks, the oracle check of G gates spread over the timed batch, and (rank 0)
     the JSON result.  make_engine / make_checker / torch_device / backend are
     the only things tests/test_bench_ranks.py replaces (CPU stand-ins, gloo)."""
     import torch
@@ -318,10 +318,16 @@ def run_rank(args, env: dict, make_engine, make_checker, torch_device: str, back
         per_launch_s = ev0.elapsed_time(ev1) / 1e3 / (p.k * p.n)
         del e_ct, e_in, e_out
 
-    # ---- proof: the first G gates of this rank's timed batch against the oracle ----
+    # ---- proof: G gates of this rank's timed batch against the oracle, spread over
+    # the whole batch (first and last gate included, so every workgroup slot
+    # and dispatch round is sampled -- a first-G sample once hid a defect that
+    # only hit gates from the second workgroup slot of each CU) ----
     cpu = cpu_info()
     G = args.check_gates or (cpu["usable"] if world == 1 else 2)
     G = max(1, min(G, B))
+    idx = np.unique(np.round(np.linspace(0, B - 1, G)).astype(np.int64))
+    G = len(idx)
+    idx_d = torch.as_tensor(idx, device=torch_device)
     threads = args.cpu_threads or (cpu["usable"] if world == 1 else max(1, min(G, cpu["usable"] // world)))
     chk = make_checker(p, lwe)
     keys_h = keys.cpu().numpy().view(np.uint64 if word == 8 else np.uint32)
@@ -330,18 +336,18 @@ def run_rank(args, env: dict, make_engine, make_checker, torch_device: str, back
     del keys
     t_c = time.perf_counter()
     if stage == "gate":
-        sub = {key: (v[:G] if key != "nand" else v) for key, v in h.items()}
+        sub = {key: (v[idx] if key != "nand" else v) for key, v in h.items()}
         ksk64 = (tuple(x.astype(np.uint64) for x in ksk) if lwe else ksk)
         exp_a, exp_b = chk.gates((evk_h, pkey_h), ksk64, sub, threads, (qKS, baseKS, n_out))
         dt_c = time.perf_counter() - t_c
-        got_a = d_oa[:G].cpu().numpy().view(np.uint32).astype(np.uint64)
+        got_a = d_oa[idx_d].cpu().numpy().view(np.uint32).astype(np.uint64)
         bad = np.any((got_a != exp_a.reshape(got_a.shape)).reshape(G, -1), axis=1)
         if lwe:
-            bad |= d_ob[:G].cpu().numpy().view(np.uint32).astype(np.uint64) != exp_b
+            bad |= d_ob[idx_d].cpu().numpy().view(np.uint32).astype(np.uint64) != exp_b
     else:
-        exp = chk.evalacc(evk_h, pkey_h, ct_h[:G].astype(np.uint64), acc_h[:G].astype(np.uint64), threads)
+        exp = chk.evalacc(evk_h, pkey_h, ct_h[idx].astype(np.uint64), acc_h[idx].astype(np.uint64), threads)
         dt_c = time.perf_counter() - t_c
-        got = d_out[:G].cpu().numpy().view(np.uint64 if word == 8 else np.uint32).astype(np.uint64)
+        got = d_out[idx_d].cpu().numpy().view(np.uint64 if word == 8 else np.uint32).astype(np.uint64)
         bad = np.any((got != exp).reshape(G, -1), axis=1)
     counts = torch.tensor([G, int(bad.sum())], dtype=torch.int64, device=torch_device)
     if world > 1:
@@ -376,7 +382,8 @@ def run_rank(args, env: dict, make_engine, make_checker, torch_device: str, back
                        "parallelism": f"gate-sharded x{world}"},
             "parity_checked": checked,
             "parity_mismatches": mismatches,
-            "parity": (f"first {G} gates of every rank's timed batch recomputed by the CPU oracle (oracle/, "
+            "parity": (f"{G} gates of every rank's timed batch, evenly spread from the first to the last, "
+                       "recomputed by the CPU oracle (oracle/, "
                        "bit-exact integer compare of every output word); the oracle's primitives are pinned by the "
                        "reference's KATs, the EvalAcc composition is 'parity unpinned' beyond them (DESIGN.md s3)"),
             "roofline": {"bound": "hbm", "achieved": by / pl / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
@@ -396,7 +403,7 @@ def run_rank(args, env: dict, make_engine, make_checker, torch_device: str, back
             ref = REF_CPU_S_PER_EVALACC.get(args.paramset) if not (wide or args.n_override) else None
             result["cpu_baseline"] = {
                 "value": G / dt_c, "unit": "bootstraps/s", "cores": threads, "kind": chk.kind,
-                "sample": (f"the first {G} {what} of the timed batch ({p.k}x{p.n} accumulator steps each), one per "
+                "sample": (f"{G} {what} spread over the timed batch ({p.k}x{p.n} accumulator steps each), one per "
                            f"thread on {threads} threads, {dt_c:.2f} s wall; the same gates are the parity check"),
                 "host": cpu,
                 "reference_1core_s_per_evalacc": ref,

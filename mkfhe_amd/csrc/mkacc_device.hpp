@@ -8,12 +8,15 @@
 //   layout A  x[r] <-> j = (r << 6) | lane                 regs = bits 10..6
 //   layout B  x[r] <-> j = ((lane>>1) << 6) | (r<<1) | (lane&1)   regs = bits 5..1
 //   layout C  x[r] <-> j = (lane << 5) | r                 regs = bits 4..0
+//   layout D  x[r] <-> j = ((lane>>5) << 10) | (r<<5) | (lane&31)   regs = bits 9..5
 //
 // Forward (coefficient, layout A) -> stages on bits 10..6 (A) -> 5..1 (B) -> 0 (C)
 // produces the reference's EVALUATION order (bit-reversed CT output,
-// transformnat-impl.h:300-354) in layout C.  The inverse runs the GS stages in
-// the opposite order (transformnat-impl.h:492-552) and returns layout A; its
-// N^-1 factor is folded into the keys by the host.
+// transformnat-impl.h:300-354) in layout C.  The inverse (ntt_inv) runs
+// decimation-in-time butterflies on bits 0..4 (C), 5..9 (D), 10 (A) and a
+// psi^-i post-twist, the same map as the reference's GS inverse
+// (transformnat-impl.h:492-552); its N^-1 factor is folded into the keys and
+// the accumulator by the host.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -48,8 +51,19 @@ __device__ __forceinline__ u32x4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t voff,
 __device__ __forceinline__ u32x2 bload2(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
     return __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
 }
+// A 16-byte store reads its data VGPRs after it issues: they must not be
+// rewritten for 2 wait states (gfx950: VMEM store of more than 8 bytes ->
+// VALU write of its data registers).  hipcc (ROCm 7.2) inserts no wait states
+// for buffer stores with an SGPR soffset and reuses the data registers on the
+// next instruction; under load (two workgroups per CU) the store then wrote
+// the NEXT group's values for part of the wave (lanes 12-15 of each row), the
+// wrong-result "race" of round 1.  The s_nop sits between scheduling barriers
+// so nothing is moved into the gap.  tools/isa_audit.py checks every build.
 __device__ __forceinline__ void bstore4(u32x4 v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
     __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, soff, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 1");
+    __builtin_amdgcn_sched_barrier(0);
 }
 
 // ---- modular arithmetic ---------------------------------------------------
@@ -259,28 +273,6 @@ __host__ __device__ constexpr int twl_off(int s) { return 32 * ((1 << (s - 5)) -
 constexpr int kTwlC = 992;                 // = twl_off(10)
 constexpr int kTwlPairs = kTwlC + 1024;    // 2016 pairs per direction
 
-// forward pass-B stage s (5..9) on bit 10-s
-template <int S>
-__device__ __forceinline__ void fwd_stage_b(uint32_t (&x)[kRegs], const uint2* twl, uint32_t lhi, uint32_t Q) {
-    // twiddle runs longer than 8 pairs are processed in chunks of 8 to cap the
-    // live twiddle registers at 16
-    constexpr int NP = 1 << (S - 5), H = 1 << (9 - S), CH = NP > 8 ? 8 : NP, SH = 10 - S;
-    const uint2* t = twl + twl_off(S) + lhi;
-#pragma unroll
-    for (int c0 = 0; c0 < NP; c0 += CH) {
-        uint2 w[CH];
-#pragma unroll
-        for (int j = 0; j < CH; ++j) w[j] = t[32 * (c0 + j)];
-#pragma unroll
-        for (int r = 0; r < kRegs; ++r) {
-            if (r & H) continue;
-            const int m = r >> SH;
-            if (m < c0 || m >= c0 + CH) continue;
-            ct_bfly_lazy(x[r], x[r + H], w[m - c0], Q);
-        }
-        sched_fence();
-    }
-}
 
 // Per-lane twiddle streams, software-pipelined: the loads of chunk I+1 are
 // issued before the butterflies of chunk I (double-buffered 4-pair chunks: the
@@ -289,12 +281,9 @@ __device__ __forceinline__ void fwd_stage_b(uint32_t (&x)[kRegs], const uint2* t
 // arithmetic instead of stalling the wave.  A stream is a list of chunks
 // {stage, first pair m0, pair count}; LD / AP are the direction's load and
 // butterfly functors.
-#ifndef MKACC_TWPIPE
-#define MKACC_TWPIPE 1
-#endif
 struct TwChunk { int s, m0, cnt; };
-template <class SEQ, int I, class LD, class AP>
-__device__ __forceinline__ void tw_pipe(uint2 (&wa)[4], uint2 (&wb)[4], const LD& ld, const AP& ap) {
+template <class SEQ, int I, int W, class LD, class AP>
+__device__ __forceinline__ void tw_pipe(uint2 (&wa)[W], uint2 (&wb)[W], const LD& ld, const AP& ap) {
     constexpr TwChunk c = SEQ::at(I);
     if constexpr (I + 1 < SEQ::N) {
         constexpr TwChunk n = SEQ::at(I + 1);
@@ -304,6 +293,38 @@ __device__ __forceinline__ void tw_pipe(uint2 (&wa)[4], uint2 (&wb)[4], const LD
     sched_fence();
     if constexpr (I + 1 < SEQ::N) tw_pipe<SEQ, I + 1>(wa, wb, ld, ap);
 }
+// forward pass A (stages 0..4, layout A): wave-uniform twiddles, scalar loads
+// double-buffered in 8-pair chunks (the 16 pairs of stage 4 never all live)
+struct FwdASeq {
+    static constexpr int N = 6;
+    static constexpr TwChunk at(int i) {
+        constexpr TwChunk c[N] = {{0, 0, 1}, {1, 0, 2}, {2, 0, 4}, {3, 0, 8}, {4, 0, 8}, {4, 8, 8}};
+        return c[i];
+    }
+};
+struct FwdALoad {
+    const ConstTable& twc;
+    template <int S, int M0, int CNT>
+    __device__ __forceinline__ void go(uint2 (&w)[8]) const {
+#pragma unroll
+        for (int j = 0; j < CNT; ++j) w[j] = twc[(1 << S) + M0 + j];
+    }
+};
+struct FwdAApply {
+    uint32_t (&x)[kRegs];
+    uint32_t Q;
+    template <int S, int M0, int CNT>
+    __device__ __forceinline__ void go(const uint2 (&w)[8]) const {
+        constexpr int H = 16 >> S;
+#pragma unroll
+        for (int r = 0; r < kRegs; ++r) {
+            if (r & H) continue;
+            const int m = r >> (5 - S);
+            if (m < M0 || m >= M0 + CNT) continue;
+            ct_bfly_lazy<true>(x[r], x[r + H], w[m - M0], Q);
+        }
+    }
+};
 // forward passes B (stages 5..9, layout B) and C (stage 10, layout C)
 struct FwdSeq {
     static constexpr int N = 13;
@@ -359,19 +380,14 @@ __device__ __forceinline__ void ntt_fwd(uint32_t (&x)[kRegs], uint32_t* lds, con
                                         const uint2* tw10, uint32_t l, uint32_t Q, uint32_t m1) {
     // pass A: stages 0..4 (bits 10..6); twiddle index uniform across the wave
     const ConstTable twc{(const_u64*)opaque(tw_g)};
-#pragma unroll
-    for (int s = 0; s < 5; ++s) {
-        const int h = 16 >> s;
-#pragma unroll
-        for (int r = 0; r < kRegs; ++r) {
-            if (r & h) continue;
-            const uint2 w = twc[(1 << s) + (r >> (5 - s))];
-            ct_bfly_lazy<true>(x[r], x[r + h], w, Q);
-        }
-        sched_fence();
+    {
+        const FwdALoad ld{twc};
+        const FwdAApply ap{x, Q};
+        uint2 sa[8], sb[8];
+        ld.template go<0, 0, 1>(sa);
+        tw_pipe<FwdASeq, 0>(sa, sb, ld, ap);
     }
     const uint32_t lo = opaque_v(l);
-#if MKACC_TWPIPE
     // passes B (stages 5..9, bits 5..1) and C (stage 10, bit 0), one twiddle stream
     {
         const FwdLoad ld(twl, tw10, lo);
@@ -380,28 +396,6 @@ __device__ __forceinline__ void ntt_fwd(uint32_t (&x)[kRegs], uint32_t* lds, con
         ld.template go<5, 0, 1>(wa);
         transpose<0, 1>(x, lds, l);
         tw_pipe<FwdSeq, 0>(wa, wb, ld, ap);
-    }
-    return;
-#endif
-    transpose<0, 1>(x, lds, l);
-    // pass B: stages 5..9 (bits 5..1)
-    const uint32_t lhi = lo >> 1;
-    fwd_stage_b<5>(x, twl, lhi, Q);
-    fwd_stage_b<6>(x, twl, lhi, Q);
-    fwd_stage_b<7>(x, twl, lhi, Q);
-    fwd_stage_b<8>(x, twl, lhi, Q);
-    fwd_stage_b<9>(x, twl, lhi, Q);
-    transpose<1, 2>(x, lds, l);
-    // pass C: stage 10 (bit 0), in two halves of 8 twiddles
-    const uint2* tc = tw10 + lo;
-#pragma unroll
-    for (int hf = 0; hf < 2; ++hf) {
-        uint2 w[8];
-#pragma unroll
-        for (int m = 0; m < 8; ++m) w[m] = tc[64 * (8 * hf + m)];
-#pragma unroll
-        for (int m = 0; m < 8; ++m) ct_bfly_last(x[16 * hf + 2 * m], x[16 * hf + 2 * m + 1], w[m], Q, m1);
-        sched_fence();
     }
 }
 
@@ -460,27 +454,46 @@ struct InvPlan {
 constexpr InvPlan kInvPlan(2);   // inputs in [0, 2Q)
 static_assert(kInvPlan.maxb <= 20, "inverse NTT bounds");
 
-// pass-2 stage on bit B (5..9), layout D: NP = 2^(B-5) per-lane twiddles
-template <int B>
-__device__ __forceinline__ void inv_stage_d(uint32_t (&x)[kRegs], const uint2* twl, uint32_t l31, uint32_t Q) {
-    constexpr int H = 1 << (B - 5), NP = H, CH = NP > 8 ? 8 : NP;
-    const uint2* t = twl + twl_off(B) + l31;
+
+// inverse pass 1 (bits 0..4, layout C): scalar twiddle chunks; t = 0 entries
+// entries (twiddle 1) are loaded even where the butterflies skip the product
+struct Inv1Seq {
+    static constexpr int N = 6;
+    static constexpr TwChunk at(int i) {
+        constexpr TwChunk c[N] = {{0, 0, 0}, {1, 0, 2}, {2, 0, 4}, {3, 0, 8}, {4, 0, 8}, {4, 8, 8}};
+        return c[i];
+    }
+};
+struct Inv1Load {
+    const ConstTable& twc;
+    template <int S, int M0, int CNT>
+    __device__ __forceinline__ void go(uint2 (&w)[8]) const {
 #pragma unroll
-    for (int c0 = 0; c0 < NP; c0 += CH) {
-        uint2 w[CH];
-#pragma unroll
-        for (int j = 0; j < CH; ++j) w[j] = t[32 * (c0 + j)];
+        for (int j = 0; j < CNT; ++j) w[j] = twc[(1 << S) + M0 + j];
+    }
+};
+struct Inv1Apply {
+    uint32_t (&x)[kRegs];
+    uint32_t Q;
+    template <int S, int M0, int CNT>
+    __device__ __forceinline__ void go(const uint2 (&w)[8]) const {
+        constexpr int H = 1 << S;
 #pragma unroll
         for (int r = 0; r < kRegs; ++r) {
             if (r & H) continue;
-            const int m = r & (H - 1);
-            if (m < c0 || m >= c0 + CH) continue;
-            ct_bfly_lazy(x[r], x[r + H], w[m - c0], Q);
+            const int t = r & (H - 1);
+            if (S > 0 && (t < M0 || t >= M0 + CNT)) continue;
+            if (S == 0 && M0 != 0) continue;
+            if (kInvPlan.skip[S][r]) {
+                const uint32_t X = x[r], Y = x[r + H];
+                x[r] = X + Y;
+                x[r + H] = X - Y + (uint32_t)kInvPlan.bound[S][r + H] * Q;
+            } else {
+                ct_bfly_lazy<true>(x[r], x[r + H], w[t - M0], Q);
+            }
         }
-        sched_fence();
     }
-}
-
+};
 // inverse pass 2 (stages 5..9, layout D), bit 10 (layout A) and the twist
 struct InvSeq {
     static constexpr int N = 21;
@@ -535,25 +548,13 @@ __device__ __forceinline__ void ntt_inv(uint32_t (&x)[kRegs], uint32_t* lds, con
                                         uint32_t l, uint32_t Q) {
     // pass 1: bits 0..4 on registers, twiddle index (r mod 2^b) wave-uniform
     const ConstTable twc{(const_u64*)opaque(tis)};
-#pragma unroll
-    for (int b = 0; b < 5; ++b) {
-        const int h = 1 << b;
-#pragma unroll
-        for (int r = 0; r < kRegs; ++r) {
-            if (r & h) continue;
-            if (kInvPlan.skip[b][r]) {
-                // twiddle 1: X + Y, X - Y + (bound of Y)
-                const uint32_t X = x[r], Y = x[r + h];
-                x[r] = X + Y;
-                x[r + h] = X - Y + (uint32_t)kInvPlan.bound[b][r + h] * Q;
-            } else {
-                ct_bfly_lazy<true>(x[r], x[r + h], twc[h + (r & (h - 1))], Q);
-            }
-        }
-        sched_fence();
+    {
+        const Inv1Load ld{twc};
+        const Inv1Apply ap{x, Q};
+        uint2 sa[8], sb[8];
+        tw_pipe<Inv1Seq, 0>(sa, sb, ld, ap);
     }
     const uint32_t lo = opaque_v(l);
-#if MKACC_TWPIPE
     {
         const InvLoad ld(twl, lo);
         const InvApply ap{x, lds, l, Q};
@@ -561,38 +562,6 @@ __device__ __forceinline__ void ntt_inv(uint32_t (&x)[kRegs], uint32_t* lds, con
         ld.template go<5, 0, 1>(wa);
         transpose<2, 3>(x, lds, l);
         tw_pipe<InvSeq, 0>(wa, wb, ld, ap);
-    }
-    return;
-#endif
-    transpose<2, 3>(x, lds, l);
-    const uint32_t l31 = lo & 31u;
-    inv_stage_d<5>(x, twl, l31, Q);
-    inv_stage_d<6>(x, twl, l31, Q);
-    inv_stage_d<7>(x, twl, l31, Q);
-    inv_stage_d<8>(x, twl, l31, Q);
-    inv_stage_d<9>(x, twl, l31, Q);
-    transpose<3, 0>(x, lds, l);
-    // pass 3: bit 10 (pairs (r, r + 16)), two halves of 8 twiddles
-    const uint2* tc = twl + kTwlC + lo;
-#pragma unroll
-    for (int hf = 0; hf < 2; ++hf) {
-        uint2 w[8];
-#pragma unroll
-        for (int m = 0; m < 8; ++m) w[m] = tc[64 * (8 * hf + m)];
-#pragma unroll
-        for (int m = 0; m < 8; ++m) ct_bfly_lazy(x[8 * hf + m], x[8 * hf + m + 16], w[m], Q);
-        sched_fence();
-    }
-    // twist by psi^-i, i = (r << 6) | l: canonical output
-    const uint2* tt = twl + kTwlPairs + lo;
-#pragma unroll
-    for (int q4 = 0; q4 < 4; ++q4) {
-        uint2 w[8];
-#pragma unroll
-        for (int m = 0; m < 8; ++m) w[m] = tt[64 * (8 * q4 + m)];
-#pragma unroll
-        for (int m = 0; m < 8; ++m) x[8 * q4 + m] = mul_shoup(x[8 * q4 + m], w[m].x, w[m].y, Q);
-        sched_fence();
     }
 }
 

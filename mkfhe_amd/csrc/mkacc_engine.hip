@@ -224,25 +224,22 @@ __device__ __forceinline__ void digit_range(uint32_t (&x)[kRegs], uint32_t Q) {
 
 // Key words of one 4-register group of a MAC: software-pipelined kPrefetch
 // groups ahead so the L2 latency of the step's key block overlaps the arithmetic.
-#ifndef MKACC_PREFETCH3
-#define MKACC_PREFETCH3 1
-#endif
-#ifndef MKACC_KEY_AUX
-#define MKACC_KEY_AUX 0
-#endif
 template <int DG>
-struct Prefetch { static constexpr int value = DG <= 3 ? MKACC_PREFETCH3 : 0; };
+struct Prefetch { static constexpr int value = DG <= 3 ? 1 : 0; };
+// accumulator loads: each gate's own rows, written by the previous step launch
+__device__ __forceinline__ u32x4 aload4(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    return __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
+}
 // key-block loads (shared by every gate of the launch, streamed from L2)
 __device__ __forceinline__ u32x4 kload4(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-    return __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, MKACC_KEY_AUX);
+    // default cache policy: the 8 waves of a CU share the key lines through L1
+    // (non-temporal loads measured 11% slower, profiles/r2/ab_series1.txt)
+    return __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
 }
 struct KeyGroup {
     u32x4 k1, k2, ks, pk, acc;
     uint2 mono[4];   // X^(N-c) - 1 at the group's slots (XZW after the first step)
 };
-#ifndef MKACC_MONO_PREFETCH
-#define MKACC_MONO_PREFETCH 1
-#endif
 // per-wave resources of the MAC helpers
 struct StepRes {
     __amdgpu_buffer_rsrc_t rin, rk1, rk2, rks, rpk;
@@ -257,16 +254,14 @@ struct StepRes {
 // xzw.cpp:342-344; in Montgomery form, redc divides by 2^32) when the bound
 // allows, streamed in with the keys; 0 in the FIRST step, where AddToAccXZW0
 // overwrites acc (xzw.cpp:380).
-// The caller issues the first kPrefetch key groups (issue()) BEFORE the digit's
-// forward NTT, so the MAC starts on loaded keys; run() streams the rest.
-#ifndef MKACC_EARLY_KEYS
-#define MKACC_EARLY_KEYS 0
-#endif
+// The caller issues the first kPrefetch key groups (issue()), run() streams
+// the rest kPrefetch groups ahead.  (Issuing the first group before the digit
+// NTT spilled 23 VGPRs and measured 4% slower, profiles/r2/ab_series1.txt.)
 template <int DG, int METHOD, bool FIRST, bool START>
 struct DigitMac {
     using Bd = Bounds<DG, METHOD, FIRST>;
     static constexpr bool kAcc = START && Bd::kAccInSum;
-    static constexpr bool kMonoPf = MKACC_MONO_PREFETCH && METHOD == XZW && !FIRST;
+    static constexpr bool kMonoPf = METHOD == XZW && !FIRST;
     static constexpr int kPrefetch = Prefetch<DG>::value;
     static constexpr int kBuf = kPrefetch + 1;
     const StepRes& sr;
@@ -279,7 +274,7 @@ struct DigitMac {
         t.pk = kload4(sr.rpk, sr.vo, poff + go);
         if (METHOD == XZW) t.k2 = kload4(sr.rk2, sr.vo, koff + go);
         if (FIRST) t.ks = kload4(sr.rks, sr.vo, koff + go);
-        if (kAcc) t.acc = bload4(sr.rin, sr.vo, aoff + go);
+        if (kAcc) t.acc = aload4(sr.rin, sr.vo, aoff + go);
         if (kMonoPf) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) t.mono[e] = sr.mn.at(sr.psi, 4 * gq + e);
@@ -402,7 +397,7 @@ __device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_
     uint32_t x[kRegs];
 #pragma unroll
     for (int gq = 0; gq < 8; ++gq) {
-        const u32x4 t = bload4(s.rin, s.vo, u * polyB + gq * 1024u);
+        const u32x4 t = aload4(s.rin, s.vo, u * polyB + gq * 1024u);
         x[4 * gq] = t.x; x[4 * gq + 1] = t.y; x[4 * gq + 2] = t.z; x[4 * gq + 3] = t.w;
     }
     if (!FIRST) {
@@ -428,16 +423,10 @@ __device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_
     {
         const DigitMac<DG, METHOD, FIRST, true> mac(sr, 0, u);
         KeyGroup kg[mac.kBuf];
-        if (MKACC_EARLY_KEYS) {
-#pragma unroll
-            for (int j = 0; j < mac.kPrefetch; ++j) mac.issue(kg[j], j);
-        }
         ntt_fwd(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, s.l, Q, s.m.m1);
         digit_range<DG>(x, Q);
-        if (!MKACC_EARLY_KEYS) {
 #pragma unroll
-            for (int j = 0; j < mac.kPrefetch; ++j) mac.issue(kg[j], j);
-        }
+        for (int j = 0; j < mac.kPrefetch; ++j) mac.issue(kg[j], j);
         mac.run(x, uj, sv, kg);
     }
 #pragma unroll 1
@@ -446,16 +435,10 @@ __device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_
         for (int r = 0; r < kRegs; ++r) x[r] = pd.get(r, i + 1, s.sd);
         const DigitMac<DG, METHOD, FIRST, false> mac(sr, i, u);
         KeyGroup kg[mac.kBuf];
-        if (MKACC_EARLY_KEYS) {
-#pragma unroll
-            for (int j = 0; j < mac.kPrefetch; ++j) mac.issue(kg[j], j);
-        }
         ntt_fwd(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, s.l, Q, s.m.m1);
         digit_range<DG>(x, Q);
-        if (!MKACC_EARLY_KEYS) {
 #pragma unroll
-            for (int j = 0; j < mac.kPrefetch; ++j) mac.issue(kg[j], j);
-        }
+        for (int j = 0; j < mac.kPrefetch; ++j) mac.issue(kg[j], j);
         mac.run(x, uj, sv, kg);
     }
     if (LAST) {
@@ -468,7 +451,7 @@ __device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_
 #pragma unroll
     for (int gq = 0; gq < 8; ++gq) {
         u32x4 t;
-        if constexpr (!Bd::kAccInSum && !FIRST) t = bload4(s.rin, s.vo, u * polyB + gq * 1024u);
+        if constexpr (!Bd::kAccInSum && !FIRST) t = aload4(s.rin, s.vo, u * polyB + gq * 1024u);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const int r = 4 * gq + e;
@@ -556,7 +539,7 @@ __device__ __forceinline__ void step_body(const StepCtx& s, uint32_t k, uint32_t
         // acc[index] joins the f-part sum (Bounds: < 4 Q^2 with the folded party sum)
 #pragma unroll
         for (int gq = 0; gq < 8; ++gq) {
-            const u32x4 t = bload4(s.rin, s.vo, index * polyB + gq * 1024u);
+            const u32x4 t = aload4(s.rin, s.vo, index * polyB + gq * 1024u);
 #pragma unroll
             for (int e = 0; e < 4; ++e) w[4 * gq + e] = mad64(t[e], s.m.r32, w[4 * gq + e]);
         }
@@ -589,16 +572,10 @@ __device__ __forceinline__ void step_body(const StepCtx& s, uint32_t k, uint32_t
         if constexpr (kSplit) {
             const SplitMac<DG> mac(sr, i);
             KeyGroup kg[mac.kBuf];
-            if (MKACC_EARLY_KEYS) {
-#pragma unroll
-                for (int j = 0; j < mac.kPrefetch; ++j) mac.issue(kg[j], j);
-            }
             ntt_fwd(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, l, Q, s.m.m1);
             digit_range<DG>(x, Q);
-            if (!MKACC_EARLY_KEYS) {
 #pragma unroll
-                for (int j = 0; j < mac.kPrefetch; ++j) mac.issue(kg[j], j);
-            }
+            for (int j = 0; j < mac.kPrefetch; ++j) mac.issue(kg[j], j);
             mac.run(x, w, w2, kg);
         } else {
             ntt_fwd(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, l, Q, s.m.m1);
@@ -905,7 +882,10 @@ uint32_t* launch_steps(mkacc_ctx* c, size_t B) {
     uint32_t* cur = c->d_acc0;
     uint32_t* nxt = c->d_acc1;
     const dim3 grid((unsigned)((B + kWavesPerBlock - 1) / kWavesPerBlock)), block(kThreads);
-    const size_t lds = kStepLdsBytes;
+    // MKACC_DBG_LDS=<bytes> (diagnosis, tools/dbg/determ2.py): extra dynamic LDS per
+    // workgroup; 10240 leaves one workgroup per CU, the co-residency reference
+    const char* dl = std::getenv("MKACC_DBG_LDS");
+    const size_t lds = kStepLdsBytes + (dl ? std::strtoul(dl, nullptr, 0) : 0);
     for (uint32_t u = 0; u < k; ++u) {
         for (uint32_t i = 0; i < n; ++i) {
             const bool first = (u == 0 && i == 0);

@@ -2,7 +2,7 @@
 
 `python bench.py --stub-engine` runs bench.py's real rank logic -- launcher,
 key broadcast, per-rank shards, warmup, barrier-bracketed timing, max-over-ranks
-reduction, the per-rank check of the first G gates and the sum over ranks --
+reduction, the per-rank check of G gates spread over the batch and the sum over ranks --
 over gloo on the CPU, with only the GPU engine and the oracle replaced by these
 toy functions.  The toy "accumulator" depends on the broadcast keys and on every
 input word, so a rank that received the wrong keys or a mis-sharded batch
