@@ -100,6 +100,7 @@ struct StepArgs {
     const uint32_t* img;       // table image [kImgWords]
     const uint2* tw_fwd;       // [N] reference forward table (pass A, scalar reads)
     const uint2* tw_inv;       // [32] inverse pass-1 table (ntt_inv)
+    uint32_t* dscr;            // [B][dg][N] C4 scratch of the step's d_i (mk_step_kernel DSCR) or null
     uint32_t B, k, index;
     Mod m;
     SddConsts sd;
@@ -242,7 +243,7 @@ struct KeyGroup {
 };
 // per-wave resources of the MAC helpers
 struct StepRes {
-    __amdgpu_buffer_rsrc_t rin, rk1, rk2, rks, rpk;
+    __amdgpu_buffer_rsrc_t rin, rk1, rk2, rks, rpk, rds;
     const uint2* psi;
     Mono mp, mn;
     Mod m;
@@ -257,22 +258,37 @@ struct StepRes {
 // The caller issues the first kPrefetch key groups (issue()), run() streams
 // the rest kPrefetch groups ahead.  (Issuing the first group before the digit
 // NTT spilled 23 VGPRs and measured 4% slower, profiles/r2/ab_series1.txt.)
-template <int DG, int METHOD, bool FIRST, bool START>
+// DS (XZW after the first step, mk_step_kernel DSCR): d_i is the same for every
+// party of the step, so the first party pass computes it and stores it to the
+// gate's HBM scratch (DS = 1) and the later passes load it (DS = 2) instead of
+// the ev1'/ev2 words and the psi^e - 1 gathers; DS = 0 computes it per party.
+template <int DG, int METHOD, bool FIRST, bool START, int DS = 0>
 struct DigitMac {
     using Bd = Bounds<DG, METHOD, FIRST>;
+    static_assert(DS == 0 || (METHOD == XZW && !FIRST), "d_i scratch: XZW steps after the first");
     static constexpr bool kAcc = START && Bd::kAccInSum;
-    static constexpr bool kMonoPf = METHOD == XZW && !FIRST;
-    static constexpr int kPrefetch = Prefetch<DG>::value;
+    static constexpr bool kMonoPf = METHOD == XZW && !FIRST && DS != 2;
+    // a d_i reload comes from HBM and frees the k2 / psi registers: prefetched
+    // 3 groups ahead at DG <= 3, 2 at DG >= 4 (3 spill 10 VGPRs there); 1 group measured
+    // 1-4% slower (profiles/r2/ab_dscr.txt)
+#ifndef MKACC_DSCR_PF
+#define MKACC_DSCR_PF 0
+#endif
+    static constexpr int kPrefetch = DS == 2 ? (MKACC_DSCR_PF ? MKACC_DSCR_PF : (DG <= 3 ? 3 : 2)) : Prefetch<DG>::value;
     static constexpr int kBuf = kPrefetch + 1;
     const StepRes& sr;
-    uint32_t koff, poff, aoff;
+    uint32_t koff, poff, aoff, doff;
     __device__ __forceinline__ DigitMac(const StepRes& r, int i, uint32_t u)
-        : sr(r), koff((uint32_t)(2 * i) * (kN * 4u)), poff((u * DG + (uint32_t)i) * (kN * 4u)), aoff(u * (kN * 4u)) {}
+        : sr(r), koff((uint32_t)(2 * i) * (kN * 4u)), poff((u * DG + (uint32_t)i) * (kN * 4u)), aoff(u * (kN * 4u)),
+          doff((uint32_t)i * (kN * 4u)) {}
     __device__ __forceinline__ void issue(KeyGroup& t, int gq) const {
         const uint32_t go = gq * 1024u;
-        t.k1 = kload4(sr.rk1, sr.vo, koff + go);
+        if (DS == 2)
+            t.k1 = aload4(sr.rds, sr.vo, doff + go);   // d_i of the first party pass
+        else
+            t.k1 = kload4(sr.rk1, sr.vo, koff + go);
         t.pk = kload4(sr.rpk, sr.vo, poff + go);
-        if (METHOD == XZW) t.k2 = kload4(sr.rk2, sr.vo, koff + go);
+        if (METHOD == XZW && DS != 2) t.k2 = kload4(sr.rk2, sr.vo, koff + go);
         if (FIRST) t.ks = kload4(sr.rks, sr.vo, koff + go);
         if (kAcc) t.acc = aload4(sr.rin, sr.vo, aoff + go);
         if (kMonoPf) {
@@ -287,16 +303,20 @@ struct DigitMac {
         for (int gq = 0; gq < 8; ++gq) {
             if (gq + kPrefetch < 8) issue(kg[(gq + kPrefetch) % kBuf], gq + kPrefetch);
             const KeyGroup& t = kg[gq % kBuf];
+            u32x4 dv;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const int r = 4 * gq + e;
                 const uint32_t deff =
-                    kMonoPf ? from3q<Bd::kD>(t.k1[e] + mul_shoup_lazy(t.k2[e], t.mono[e], Q), Q)   // = key_eff
-                            : key_eff<METHOD, FIRST, Bd::kD>(t.k1[e], t.k2[e], t.ks[e], sr.psi, sr.mp, sr.mn, r, Q);
+                    DS == 2 ? t.k1[e]
+                    : kMonoPf ? from3q<Bd::kD>(t.k1[e] + mul_shoup_lazy(t.k2[e], t.mono[e], Q), Q)   // = key_eff
+                              : key_eff<METHOD, FIRST, Bd::kD>(t.k1[e], t.k2[e], t.ks[e], sr.psi, sr.mp, sr.mn, r, Q);
+                dv[e] = deff;
                 const uint64_t base = kAcc ? mad64(t.acc[e], sr.m.r32, 0) : (START ? 0ull : uj[r]);
                 uj[r] = mad64(g[r], deff, base);
                 sv[r] = mad64(g[r], t.pk[e], sv[r]);
             }
+            if (DS == 1) bstore4(dv, sr.rds, sr.vo, doff + gq * 1024u);
             sched_fence();
         }
     }
@@ -379,8 +399,8 @@ struct StepCtx {
     SddConsts sd;
     Mono mp, mn;
     uint32_t l, vo;
-    __amdgpu_buffer_rsrc_t rin, rout, rk1, rk2, rks, rpk;
-    __device__ __forceinline__ StepRes res() const { return StepRes{rin, rk1, rk2, rks, rpk, tb.psi, mp, mn, m, vo}; }
+    __amdgpu_buffer_rsrc_t rin, rout, rk1, rk2, rks, rpk, rds;
+    __device__ __forceinline__ StepRes res() const { return StepRes{rin, rk1, rk2, rks, rpk, rds, tb.psi, mp, mn, m, vo}; }
 };
 
 // One party u of HbProd (mk-acc-xzw.cpp:245-270) fused with AddToAccXZW's
@@ -389,7 +409,7 @@ struct StepCtx {
 //   sv  += sum_i NTT(g_i) * P[u][i]
 // Party `index` is processed last (LAST): its lazy sum stays in registers
 // (`uj`, folded) and receives the f-part of HbProd before the single store.
-template <int DG, int METHOD, bool FIRST, bool LAST>
+template <int DG, int METHOD, bool FIRST, bool LAST, int DS = 0>
 __device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_t (&sv)[kRegs],
                                            uint64_t (&uj)[kRegs]) {
     using Bd = Bounds<DG, METHOD, FIRST>;
@@ -421,7 +441,7 @@ __device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_
     }
     const StepRes sr = s.res();
     {
-        const DigitMac<DG, METHOD, FIRST, true> mac(sr, 0, u);
+        const DigitMac<DG, METHOD, FIRST, true, DS> mac(sr, 0, u);
         KeyGroup kg[mac.kBuf];
         ntt_fwd(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, s.l, Q, s.m.m1);
         digit_range<DG>(x, Q);
@@ -433,7 +453,7 @@ __device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_
     for (int i = 1; i < DG; ++i) {
 #pragma unroll
         for (int r = 0; r < kRegs; ++r) x[r] = pd.get(r, i + 1, s.sd);
-        const DigitMac<DG, METHOD, FIRST, false> mac(sr, i, u);
+        const DigitMac<DG, METHOD, FIRST, false, DS> mac(sr, i, u);
         KeyGroup kg[mac.kBuf];
         ntt_fwd(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, s.l, Q, s.m.m1);
         digit_range<DG>(x, Q);
@@ -466,10 +486,12 @@ __device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_
     }
 }
 
-template <int DG, int METHOD, bool FIRST>
+template <int DG, int METHOD, bool FIRST, bool DSCR>
 __device__ __forceinline__ void step_body(const StepCtx& s, uint32_t k, uint32_t index);
 
-template <int DG, int METHOD, bool FIRST>
+// DSCR: d_i computed once per step and gate (first party pass) and reloaded from
+// a.dscr by the other k - 1 passes (DigitMac DS); the host picks it by k.
+template <int DG, int METHOD, bool FIRST, bool DSCR = false>
 __global__ __launch_bounds__(kThreads, 2) void mk_step_kernel(StepArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     load_image(smem, a.img);
@@ -499,8 +521,9 @@ __global__ __launch_bounds__(kThreads, 2) void mk_step_kernel(StepArgs a) {
                     make_rsrc(a.key1, DG * 2 * polyB),
                     make_rsrc(a.key2, DG * 2 * polyB),
                     make_rsrc(a.keys, DG * 2 * polyB),
-                    make_rsrc(a.pkey, k * DG * polyB)};
-    step_body<DG, METHOD, FIRST>(s, k, a.index);
+                    make_rsrc(a.pkey, k * DG * polyB),
+                    make_rsrc(DSCR ? a.dscr + (size_t)gate * DG * kN : a.acc_in, DSCR ? DG * polyB : 0u)};
+    step_body<DG, METHOD, FIRST, DSCR>(s, k, a.index);
 }
 
 // One accumulator step for one gate per wavefront.
@@ -512,7 +535,7 @@ __global__ __launch_bounds__(kThreads, 2) void mk_step_kernel(StepArgs a) {
 // lazy 64-bit accumulators (v_mad_u64_u32) reduced once (Montgomery); all sums
 // are exact mod Q, so the reordering (parties in the order index+1, ..., index)
 // is bit-exact.
-template <int DG, int METHOD, bool FIRST>
+template <int DG, int METHOD, bool FIRST, bool DSCR>
 __device__ __forceinline__ void step_body(const StepCtx& s, uint32_t k, uint32_t index) {
     using Bd = Bounds<DG, METHOD, FIRST>;
     const uint32_t Q = s.m.Q;
@@ -525,16 +548,27 @@ __device__ __forceinline__ void step_body(const StepCtx& s, uint32_t k, uint32_t
     // sumV grows by kSvParty (units of Q^2) per party; fold it before it could
     // pass 32 (fold64 leaves < 2)
     int svb = 0;
-    for (uint32_t t = 1; t < k; ++t) {
-        party_pass<DG, METHOD, FIRST, false>(s, index + t < k ? index + t : index + t - k, sv, w);
+    auto grow_sv = [&]() {
         svb += Bd::kSvParty;
         if (svb + Bd::kSvParty > 32) {
 #pragma unroll
             for (int r = 0; r < kRegs; ++r) sv[r] = fold64(sv[r], s.m.r32);
             svb = 2;
         }
+    };
+    uint32_t t0 = 1;
+    if constexpr (DSCR) {   // k >= 2 (host: use_dscr)
+        party_pass<DG, METHOD, FIRST, false, 1>(s, index + 1 < k ? index + 1 : 0, sv, w);
+        grow_sv();
+        t0 = 2;
+        // the scratch stores complete before the later passes read them back
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    party_pass<DG, METHOD, FIRST, true>(s, index, sv, w);
+    for (uint32_t t = t0; t < k; ++t) {
+        party_pass<DG, METHOD, FIRST, false, DSCR ? 2 : 0>(s, index + t < k ? index + t : index + t - k, sv, w);
+        grow_sv();
+    }
+    party_pass<DG, METHOD, FIRST, true, DSCR ? 2 : 0>(s, index, sv, w);
     if constexpr (!Bd::kAccInSum && !FIRST) {
         // acc[index] joins the f-part sum (Bounds: < 4 Q^2 with the folded party sum)
 #pragma unroll
@@ -733,12 +767,15 @@ __global__ void sdd_kernel(const uint32_t* __restrict__ in, uint32_t* __restrict
 using StepFn = void (*)(StepArgs);
 
 template <int DG>
-StepFn pick_step(int method, bool first) {
-    if (method == XZW) return first ? mk_step_kernel<DG, XZW, true> : mk_step_kernel<DG, XZW, false>;
+StepFn pick_step(int method, bool first, bool dscr) {
+    if (method == XZW) {
+        if (first) return mk_step_kernel<DG, XZW, true>;
+        return dscr ? mk_step_kernel<DG, XZW, false, true> : mk_step_kernel<DG, XZW, false>;
+    }
     return first ? mk_step_kernel<DG, XZW_B, true> : mk_step_kernel<DG, XZW_B, false>;
 }
 
-StepFn step_fn(int dg, int method, bool first);
+StepFn step_fn(int dg, int method, bool first, bool dscr);
 
 }  // namespace
 
@@ -769,19 +806,19 @@ __global__ void wide_key_layout_kernel(const W* __restrict__ src, uint64_t* __re
 }
 
 // MKACC_ONLY_DG=d (developer builds for ISA studies): instantiate one digit count
-StepFn step_fn(int dg, int method, bool first) {
+StepFn step_fn(int dg, int method, bool first, bool dscr) {
     switch (dg) {
 #if !defined(MKACC_ONLY_DG) || MKACC_ONLY_DG == 2
-        case 2: return pick_step<2>(method, first);
+        case 2: return pick_step<2>(method, first, dscr);
 #endif
 #if !defined(MKACC_ONLY_DG) || MKACC_ONLY_DG == 3
-        case 3: return pick_step<3>(method, first);
+        case 3: return pick_step<3>(method, first, dscr);
 #endif
 #if !defined(MKACC_ONLY_DG) || MKACC_ONLY_DG == 4
-        case 4: return pick_step<4>(method, first);
+        case 4: return pick_step<4>(method, first, dscr);
 #endif
 #if !defined(MKACC_ONLY_DG) || MKACC_ONLY_DG == 5
-        case 5: return pick_step<5>(method, first);
+        case 5: return pick_step<5>(method, first, dscr);
 #endif
         default: return nullptr;
     }
@@ -812,6 +849,7 @@ struct mkacc_ctx {
     uint32_t* d_acc0 = nullptr;
     uint32_t* d_acc1 = nullptr;
     uint32_t* d_cvals = nullptr;
+    uint32_t* d_dscr = nullptr;   // [B][dg][N] d_i scratch (use_dscr), sized with the workspace
     // host-pointer API staging
     size_t io_B = 0;
     uint32_t* d_ct = nullptr;
@@ -859,17 +897,32 @@ const uint32_t* key_step(const mkacc_ctx* c, uint32_t u, uint32_t i, uint32_t j)
     return c->d_keys + ((size_t)u * (c->p.n + 1) + i) * key_block_words(c) + (size_t)j * c->dg * 2 * kN;
 }
 
+// d_i scratch (mk_step_kernel DSCR): the XZW steps after the first compute the
+// step's d_i once per gate instead of once per party pass.  It trades
+// (k - 1) dg N Shoup products and psi gathers per gate-step for an HBM round
+// trip of dg N words; default on from k >= kDscrMinK,
+// MKACC_DSCR=0/1 overrides.
+constexpr uint32_t kDscrMinK = 4;
+bool use_dscr(const mkacc_ctx* c) {
+    if (c->method_class != XZW || c->p.k < 2) return false;
+    const char* e = std::getenv("MKACC_DSCR");
+    if (e && *e) return e[0] != '0';
+    return c->p.k >= kDscrMinK;
+}
+
 int ensure_ws(mkacc_ctx* c, size_t B) {
     if (B <= c->ws_B) return MKACC_OK;
     if (c->d_acc0) HIP_TRY(hipFree(c->d_acc0));
     if (c->d_acc1) HIP_TRY(hipFree(c->d_acc1));
     if (c->d_cvals) HIP_TRY(hipFree(c->d_cvals));
-    c->d_acc0 = c->d_acc1 = c->d_cvals = nullptr;
+    if (c->d_dscr) HIP_TRY(hipFree(c->d_dscr));
+    c->d_acc0 = c->d_acc1 = c->d_cvals = c->d_dscr = nullptr;
     c->ws_B = 0;
     const size_t accw = B * c->p.k * (size_t)kN;
     HIP_TRY(hipMalloc(&c->d_acc0, accw * 4));
     HIP_TRY(hipMalloc(&c->d_acc1, accw * 4));
     HIP_TRY(hipMalloc(&c->d_cvals, B * c->p.k * (size_t)c->p.n * 4));
+    if (use_dscr(c)) HIP_TRY(hipMalloc(&c->d_dscr, B * c->dg * (size_t)kN * 4));
     c->ws_B = B;
     return MKACC_OK;
 }
@@ -905,7 +958,8 @@ uint32_t* launch_steps(mkacc_ctx* c, size_t B) {
             a.index = u;
             a.m = c->mod;
             a.sd = c->sd;
-            StepFn fn = step_fn((int)c->dg, c->method_class, first);
+            a.dscr = c->d_dscr;
+            StepFn fn = step_fn((int)c->dg, c->method_class, first, !first && c->d_dscr != nullptr);
             hipLaunchKernelGGL(fn, grid, block, lds, c->stream, a);
             std::swap(cur, nxt);
         }
@@ -1574,7 +1628,7 @@ void mkacc_destroy(mkacc_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (void* p : {(void*)c->d_twf, (void*)c->d_twi, (void*)c->d_img, (void*)c->d_keys, (void*)c->d_pkey,
-                    (void*)c->d_acc0, (void*)c->d_acc1, (void*)c->d_cvals, (void*)c->d_ct,
+                    (void*)c->d_acc0, (void*)c->d_acc1, (void*)c->d_cvals, (void*)c->d_dscr, (void*)c->d_ct,
                     (void*)c->d_io, (void*)c->d_ksk, (void*)c->d_lweA, (void*)c->d_lweB, (void*)c->d_tv,
                     (void*)c->d_digits, (void*)c->d_bh, (void*)c->d_gin, (void*)c->d_gout, (void*)c->d_wtwf,
                     (void*)c->d_wtwi, (void*)c->d_wpsi, (void*)c->d_wkeys, (void*)c->d_wpkey, (void*)c->d_wacc0,

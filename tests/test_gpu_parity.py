@@ -104,6 +104,25 @@ def test_evalacc_small_parity(mk, oracle, case):
     assert np.array_equal(eng.eval_batch(ct.astype(np.uint32), acc.astype(np.uint32)), got)
 
 
+DSCR_CASES = [c for c in CASES if c[0] == "XZW" and c[1] >= 2]
+
+
+@pytest.mark.parametrize("dscr", ["0", "1"])
+@pytest.mark.parametrize("case", DSCR_CASES, ids=[f"k{c[1]}-logB{c[4].bit_length() - 1}" for c in DSCR_CASES])
+def test_evalacc_dscr_modes(mk, oracle, case, dscr, monkeypatch):
+    """Both d_i modes of the XZW step kernel (recomputed per party pass, or
+    computed by the first pass and reloaded from the HBM scratch; the engine
+    picks by k, MKACC_DSCR forces one) give the oracle's accumulators."""
+    meth, k, n, q, baseG, B = case
+    monkeypatch.setenv("MKACC_DSCR", dscr)   # read when the context sizes its workspace
+    orc, evk, pkey, ct, acc = make_case(oracle, oracle.XZW, k, n, q, baseG, B + 2, seed=k * 31 + n)
+    exp = orc.evalacc_batch(evk, pkey, ct, acc, 8)
+    eng = mk.MKAccumulatorEngine(mk.make_params(mk.MKNTRU, k, n, 2048, Q_MK, q, baseG))
+    eng.upload_keys(evk.astype(np.uint32), pkey.astype(np.uint32))
+    got = eng.eval_batch(ct.astype(np.uint32), acc.astype(np.uint32))
+    assert np.array_equal(got, exp.astype(np.uint32))
+
+
 def test_interface_mirror_evalacc(mk, oracle):
     """UniEncAccumulatorXZW.EvalAcc updates acc in place like the reference."""
     orc, evk, pkey, ct, acc = make_case(oracle, oracle.XZW, 2, 3, 45181, 1 << 9, 1, seed=9)
