@@ -49,6 +49,9 @@ METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 
 # measured on this pool (tools/ubench_intops.hip, profiles/round1_ubench_intops.txt)
 PEAK_SHOUP_MULMOD_TPS = 7.744e12     # 27-bit Shoup mod-mul / s, whole chip
+# 64-bit word path (tools/ubench_wide.hip, profiles/r2/ubench_wide.txt, 50-bit Q):
+PEAK_FP64_MULMOD_TPS = 5.7455e12     # exact FP64 product (mkacc_widefp.hpp) / s
+PEAK_INT64_MULMOD_TPS = 1.7433e12    # limb-built 64-bit Shoup product (mkacc_wide.hpp) / s
 PEAK_HBM_GBS = 8000.0                # MI355X_MICROARCH.md (spec)
 Q50 = 1125899906826241               # config 5 stress modulus
 REF_CPU_S_PER_EVALACC = {            # reference EvalAcc, 1 core of the survey container
@@ -362,6 +365,10 @@ def run_rank(args, env: dict, make_engine, make_checker, torch_device: str, back
         stage_txt = ("NAND gates: head + BootstrapGateCore (EvalAcc) + extraction/ModSwitch/"
                      f"{'KeySwitch' if lwe else 'KeySwitch2'}") if stage == "gate" else "EvalAcc (blind rotation) only"
         pl = per_launch_s or float("nan")
+        wide_fp = wide and getattr(eng, "wide_fp", False)
+        peak_mm, peak_src = ((PEAK_FP64_MULMOD_TPS, "exact FP64 product, profiles/r2/ubench_wide.txt") if wide_fp else
+                             (PEAK_INT64_MULMOD_TPS, "64-bit Shoup product, profiles/r2/ubench_wide.txt") if wide else
+                             (PEAK_SHOUP_MULMOD_TPS, "27-bit Shoup product, profiles/round1_ubench_intops.txt"))
         result = {
             "metric": METRIC,
             "value": world * B * args.steps / T,
@@ -373,7 +380,8 @@ def run_rank(args, env: dict, make_engine, make_checker, torch_device: str, back
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "u64 (50-bit residues mod Q)" if word == 8 else "u32 (27-bit residues mod Q)",
+            "dtype": ("f64 (exact integer residues mod a 50-bit Q; u64 words at the boundary)" if wide_fp else
+                      "u64 (residues mod Q)") if word == 8 else "u32 (27-bit residues mod Q)",
             "data": "synthetic: uniform keys, key-switching keys and ciphertexts (seeded)",
             "config": {"workload": f"{args.paramset} {p.k}-party {'MK-LWE' if lwe else 'MK-NTRU'} {stage_txt} "
                                    f"(k={p.k}, n={p.n}, N={p.N}, dg={dg}"
@@ -389,13 +397,15 @@ def run_rank(args, env: dict, make_engine, make_checker, torch_device: str, back
             "roofline": {"bound": "hbm", "achieved": by / pl / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": by / pl / 1e9 / PEAK_HBM_GBS,
                          "traffic": measured_traffic(args.paramset) if not (args.n_override or wide) else None,
-                         "kernel": "wide::step_kernel" if wide else "mk_step_kernel",
+                         "kernel": ("widefp::step_kernel" if wide_fp else "wide::step_kernel") if wide else "mk_step_kernel",
                          "per_launch_us": pl * 1e6,
                          "bytes_per_launch": by},
-            # the VALU peak is the measured 32-bit Shoup rate: not a bound for 64-bit words
-            "roofline_valu": None if wide else {
-                "bound": "valu-int", "achieved": mm / pl / 1e12, "peak": PEAK_SHOUP_MULMOD_TPS / 1e12,
-                "unit": "T mod-mul/s", "frac": mm / pl / PEAK_SHOUP_MULMOD_TPS, "mulmods_per_launch": mm},
+            # VALU view: algorithmic mod-muls per launch against the measured rate of the
+            # product the kernel is built on (32-bit Shoup; FP64 or 64-bit Shoup on the wide path)
+            "roofline_valu": {
+                "bound": "valu-fp64" if wide_fp else "valu-int", "achieved": mm / pl / 1e12,
+                "peak": peak_mm / 1e12, "unit": "T mod-mul/s", "frac": mm / pl / peak_mm,
+                "mulmods_per_launch": mm, "peak_source": peak_src},
         }
         if world == 1 and args.cpu_baseline:
             what = ("NAND gates (head + EvalAcc + extraction/ModSwitch/key switch)" if stage == "gate"

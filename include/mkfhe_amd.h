@@ -108,9 +108,9 @@ int mkacc_eval_batch(mkacc_ctx* ctx, const uint32_t* ct, const uint32_t* acc_in,
 /* Same with 64-bit accumulator words (NATIVE_SIZE=64, NativeInteger of 64 bits):
  * required when Q >= 2^32; valid for every context. */
 int mkacc_eval_batch_u64(mkacc_ctx* ctx, const uint32_t* ct, const uint64_t* acc_in, uint64_t* acc_out, size_t B);
-/* 1 if the context runs the 64-bit word path (mkfhe_amd/csrc/mkacc_wide.hpp): then
- * mkacc_eval_batch_device takes uint64_t accumulators and the gate calls are
- * unsupported. */
+/* Nonzero if the context runs the 64-bit word path (mkfhe_amd/csrc/mkacc_wide.hpp):
+ * then mkacc_eval_batch_device takes uint64_t accumulators and the gate calls are
+ * unsupported.  1: integer kernels; 2: the FP64 kernels (mkacc_widefp.hpp, Q < 2^50). */
 int mkacc_is_wide(const mkacc_ctx* ctx);
 
 /* Same with DEVICE pointers on the context's device; enqueued on the context

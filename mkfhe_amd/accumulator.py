@@ -148,6 +148,11 @@ class MKAccumulatorEngine:
         """True if the context runs the 64-bit word path (Q >= 2^27)."""
         return bool(_lib.load().mkacc_is_wide(self._h))
 
+    @property
+    def wide_fp(self) -> bool:
+        """True if the 64-bit word path runs its FP64 kernels (Q < 2^50, mkacc_widefp.hpp)."""
+        return _lib.load().mkacc_is_wide(self._h) == 2
+
     def eval_batch(self, ct: np.ndarray, acc: np.ndarray) -> np.ndarray:
         """EvalAcc on B gates: ct [B][k][n], acc [B][k][N] EVAL -> new acc.
         uint64 accumulators (or Q >= 2^32) go through mkacc_eval_batch_u64."""

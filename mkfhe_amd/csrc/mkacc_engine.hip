@@ -781,16 +781,17 @@ StepFn step_fn(int dg, int method, bool first, bool dscr);
 
 #include "mkacc_gate.hpp"
 #include "mkacc_wide.hpp"
+#include "mkacc_widefp.hpp"
 
 namespace {
 
 // Device key upload for the 64-bit word path: reference layout -> [k][n+1][nk][dg][2][N]
 // (EVAL order), each word in Montgomery form K * 2^64 mod Q (r, rp: 2^64 mod Q and its
-// Shoup companion).
+// Shoup companion), or for the FP64 variant (fp) the bits of the balanced double.
 template <typename W>
 __global__ void wide_key_layout_kernel(const W* __restrict__ src, uint64_t* __restrict__ dst, size_t npolys,
                                        uint32_t nk, uint32_t n1, uint32_t dg2, uint64_t Q, uint64_t r, uint64_t rp,
-                                       uint32_t* __restrict__ bad) {
+                                       bool fp, uint32_t* __restrict__ bad) {
     const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= npolys * kN) return;
     size_t p = idx / kN;
@@ -802,7 +803,12 @@ __global__ void wide_key_layout_kernel(const W* __restrict__ src, uint64_t* __re
     const size_t dpoly = ((u * n1 + i) * nk + jj) * dg2 + dp;
     const uint64_t x = (uint64_t)src[idx];
     if (x >= Q) *bad = 1u;
-    dst[dpoly * kN + j] = wide::mul_shoup(x, r, rp, Q);
+    if (fp) {
+        const double d = (double)(x < Q ? x : 0) - (x > (Q >> 1) && x < Q ? (double)Q : 0.0);
+        dst[dpoly * kN + j] = (uint64_t)__double_as_longlong(d);
+    } else {
+        dst[dpoly * kN + j] = wide::mul_shoup(x, r, rp, Q);
+    }
 }
 
 // MKACC_ONLY_DG=d (developer builds for ISA studies): instantiate one digit count
@@ -876,8 +882,15 @@ struct mkacc_ctx {
     ulonglong2* d_wtwf = nullptr;  // forward table {w, w'} (reference order)
     ulonglong2* d_wtwi = nullptr;
     ulonglong2* d_wpsi = nullptr;  // psi^e, e < 2N
-    uint64_t* d_wkeys = nullptr;   // [k][n+1][nk][dg][2][N] EVAL
+    uint64_t* d_wkeys = nullptr;   // [k][n+1][nk][dg][2][N] EVAL (FP64 variant: balanced doubles)
     uint64_t* d_wpkey = nullptr;   // [k][dg][N]
+    // FP64 variant of the wide path (mkacc_widefp.hpp), Q < 2^50
+    bool wfp = false;
+    widefp::FMod wfm{};
+    double wfninv = 0, wfC = 0;
+    double* d_ftwf = nullptr;      // forward / inverse twiddles and psi^e, balanced
+    double* d_ftwi = nullptr;
+    double* d_fpsi = nullptr;
     size_t wws_B = 0, wio_B = 0;
     uint64_t* d_wacc0 = nullptr;
     uint64_t* d_wacc1 = nullptr;
@@ -1180,9 +1193,9 @@ int upload_keys_device_impl(mkacc_ctx* c, const W* d_evk, const W* d_pkey) {
         if (!c->d_wkeys) HIP_TRY(hipMalloc(&c->d_wkeys, ep * kN * 8));
         if (!c->d_wpkey) HIP_TRY(hipMalloc(&c->d_wpkey, pp * kN * 8));
         hipLaunchKernelGGL(wide_key_layout_kernel<W>, grid(ep), dim3(tpb), 0, c->stream, d_evk, c->d_wkeys, ep, nk,
-                           n1, dg * 2, Q, R, Rp, c->d_bad);
+                           n1, dg * 2, Q, R, Rp, c->wfp, c->d_bad);
         hipLaunchKernelGGL(wide_key_layout_kernel<W>, grid(pp), dim3(tpb), 0, c->stream, d_pkey, c->d_wpkey, pp, 1u,
-                           1u, dg, Q, R, Rp, c->d_bad);
+                           1u, dg, Q, R, Rp, c->wfp, c->d_bad);
     } else {
         if (!c->d_keys) HIP_TRY(hipMalloc(&c->d_keys, ep * kN * 4));
         if (!c->d_pkey) HIP_TRY(hipMalloc(&c->d_pkey, pp * kN * 4));
@@ -1271,6 +1284,29 @@ int wide_setup(mkacc_ctx* c) {
     HIP_TRY(hipMemcpy(c->d_wtwf, tf.data(), kN * sizeof(ulonglong2), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->d_wtwi, ti.data(), kN * sizeof(ulonglong2), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->d_wpsi, pw.data(), 2 * kN * sizeof(ulonglong2), hipMemcpyHostToDevice));
+    // FP64 variant (mkacc_widefp.hpp): exact while every value stays below 8 Q <= 2^53
+    // and the SDD offset word below 2^53; MKACC_WIDE_FP=0 keeps the integer kernels
+    const char* fe = std::getenv("MKACC_WIDE_FP");
+    c->wfp = Q < (1ull << 50) && b * c->p.digitsG <= 52 && !(fe && fe[0] == '0');
+    if (c->wfp) {
+        const double Qd = (double)Q;
+        c->wfm = widefp::FMod{Qd, 1.0 / Qd, (double)(Q >> 1)};
+        auto bal = [Q](uint64_t x) { return x > (Q >> 1) ? (double)x - (double)Q : (double)x; };
+        c->wfninv = bal(c->wninv);
+        c->wfC = (double)C;
+        std::vector<double> ftf(kN), fti(kN), fpw(2 * kN);
+        for (uint32_t i = 0; i < (uint32_t)kN; ++i) {
+            ftf[i] = bal(tf[i].x);
+            fti[i] = bal(ti[i].x);
+        }
+        for (uint32_t i = 0; i < 2u * kN; ++i) fpw[i] = bal(pw[i].x);
+        HIP_TRY(hipMalloc(&c->d_ftwf, kN * sizeof(double)));
+        HIP_TRY(hipMalloc(&c->d_ftwi, kN * sizeof(double)));
+        HIP_TRY(hipMalloc(&c->d_fpsi, 2 * kN * sizeof(double)));
+        HIP_TRY(hipMemcpy(c->d_ftwf, ftf.data(), kN * sizeof(double), hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(c->d_ftwi, fti.data(), kN * sizeof(double), hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(c->d_fpsi, fpw.data(), 2 * kN * sizeof(double), hipMemcpyHostToDevice));
+    }
     return MKACC_OK;
 }
 
@@ -1281,7 +1317,16 @@ int wide_upload_keys(mkacc_ctx* c, const W* evk, const W* pkey) {
     if (!evk || !pkey) return fail(MKACC_E_ARG, "null key pointer");
     const uint64_t Q = c->p.Q;
     const uint64_t R = (uint64_t)(((unsigned __int128)1 << 64) % Q);
-    auto mont = [Q, R](uint64_t x) { return (uint64_t)((unsigned __int128)x * R % Q); };
+    const bool fp = c->wfp;   // FP64 variant: the bits of the balanced double
+    auto mont = [Q, R, fp](uint64_t x) {
+        if (fp) {
+            const double d = x > (Q >> 1) ? (double)x - (double)Q : (double)x;
+            uint64_t bits;
+            std::memcpy(&bits, &d, 8);
+            return bits;
+        }
+        return (uint64_t)((unsigned __int128)x * R % Q);
+    };
     const uint32_t k = c->p.k, n = c->p.n, nk = c->nk, dg = c->dg;
     const size_t blk = (size_t)dg * 2 * kN;
     std::vector<uint64_t> host((size_t)k * (n + 1) * nk * blk);
@@ -1335,13 +1380,51 @@ int wide_launch_batch(mkacc_ctx* c, const uint32_t* d_ct, const uint64_t* d_in, 
     const size_t tot = B * (size_t)k * n, accb = B * (size_t)k * kN * 8;
     hipLaunchKernelGGL(prep_c_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, c->stream, d_ct, c->d_wcvals,
                        (uint32_t)B, k * n, (uint32_t)c->method_class, (uint32_t)c->p.q, c->d_bad);
-    HIP_TRY(hipMemcpyAsync(c->d_wacc0, d_in, accb, hipMemcpyDeviceToDevice, c->stream));
-    uint64_t* cur = c->d_wacc0;
-    uint64_t* nxt = c->d_wacc1;
     const size_t blk = (size_t)c->dg * 2 * kN;
     auto key = [&](uint32_t u, uint32_t i, uint32_t j) {
         return c->d_wkeys + (((size_t)u * (n + 1) + i) * c->nk + j) * blk;
     };
+    if (c->wfp) {   // FP64 variant: balanced doubles between the prologue and the epilogue
+        const size_t words = B * (size_t)k * kN;
+        const dim3 g((unsigned)((words + 255) / 256));
+        double* cur = reinterpret_cast<double*>(c->d_wacc0);
+        double* nxt = reinterpret_cast<double*>(c->d_wacc1);
+        hipLaunchKernelGGL(widefp::to_balanced_kernel, g, dim3(256), 0, c->stream, d_in, cur, words, c->wfm);
+        auto dk = [](const uint64_t* p) { return reinterpret_cast<const double*>(p); };
+        for (uint32_t u = 0; u < k; ++u)
+            for (uint32_t i = 0; i < n; ++i) {
+                const bool first = (u == 0 && i == 0);
+                widefp::StepArgs a;
+                a.acc_in = cur;
+                a.acc_out = nxt;
+                a.cvals = c->d_wcvals + ((size_t)u * n + i) * B;
+                a.key1 = dk(key(u, i, 0));
+                a.key2 = dk(c->nk == 2 ? key(u, i, 1) : key(u, i, 0));
+                a.keys = dk(key(0, n, 0));
+                a.pkey = dk(c->d_wpkey);
+                a.twf = c->d_ftwf;
+                a.twi = c->d_ftwi;
+                a.psi = c->d_fpsi;
+                a.k = k;
+                a.index = u;
+                a.dg = c->dg;
+                a.ninv = c->wfninv;
+                a.C = c->wfC;
+                a.m = c->wfm;
+                a.sd = c->wsd;
+                void (*fn)(widefp::StepArgs);
+                if (c->method_class == XZW) fn = first ? widefp::step_kernel<XZW, true> : widefp::step_kernel<XZW, false>;
+                else fn = first ? widefp::step_kernel<XZW_B, true> : widefp::step_kernel<XZW_B, false>;
+                hipLaunchKernelGGL(fn, dim3((unsigned)B), dim3(widefp::kThreads), 0, c->stream, a);
+                std::swap(cur, nxt);
+            }
+        hipLaunchKernelGGL(widefp::to_canonical_kernel, g, dim3(256), 0, c->stream, cur, d_out, words, c->wfm);
+        HIP_TRY(hipGetLastError());
+        return MKACC_OK;
+    }
+    HIP_TRY(hipMemcpyAsync(c->d_wacc0, d_in, accb, hipMemcpyDeviceToDevice, c->stream));
+    uint64_t* cur = c->d_wacc0;
+    uint64_t* nxt = c->d_wacc1;
     for (uint32_t u = 0; u < k; ++u)
         for (uint32_t i = 0; i < n; ++i) {
             const bool first = (u == 0 && i == 0);
@@ -1408,7 +1491,13 @@ int wide_prim(mkacc_ctx* c, const uint64_t* in, uint64_t* out, size_t count, int
     HIP_TRY(hipMalloc(&din, count * kN * 8));
     HIP_TRY(hipMalloc(&dout, count * kN * 8 * out_mul));
     HIP_TRY(hipMemcpyAsync(din, in, count * kN * 8, hipMemcpyHostToDevice, c->stream));
-    if (which == 0)
+    if (which == 0 && c->wfp)
+        hipLaunchKernelGGL(widefp::ntt_fwd_kernel, dim3((unsigned)count), dim3(widefp::kThreads), 0, c->stream, din,
+                           dout, c->d_ftwf, c->wfm);
+    else if (which == 1 && c->wfp)
+        hipLaunchKernelGGL(widefp::ntt_inv_kernel, dim3((unsigned)count), dim3(widefp::kThreads), 0, c->stream, din,
+                           dout, c->d_ftwi, c->wfm, c->wfninv);
+    else if (which == 0)
         hipLaunchKernelGGL(wide::ntt_fwd_kernel, dim3((unsigned)count), dim3(wide::kThreads), 0, c->stream, din, dout,
                            c->d_wtwf, Q);
     else if (which == 1)
@@ -1631,7 +1720,8 @@ void mkacc_destroy(mkacc_ctx* c) {
                     (void*)c->d_acc0, (void*)c->d_acc1, (void*)c->d_cvals, (void*)c->d_dscr, (void*)c->d_ct,
                     (void*)c->d_io, (void*)c->d_ksk, (void*)c->d_lweA, (void*)c->d_lweB, (void*)c->d_tv,
                     (void*)c->d_digits, (void*)c->d_bh, (void*)c->d_gin, (void*)c->d_gout, (void*)c->d_wtwf,
-                    (void*)c->d_wtwi, (void*)c->d_wpsi, (void*)c->d_wkeys, (void*)c->d_wpkey, (void*)c->d_wacc0,
+                    (void*)c->d_wtwi, (void*)c->d_wpsi, (void*)c->d_ftwf, (void*)c->d_ftwi, (void*)c->d_fpsi,
+                    (void*)c->d_wkeys, (void*)c->d_wpkey, (void*)c->d_wacc0,
                     (void*)c->d_wacc1, (void*)c->d_wcvals, (void*)c->d_wct, (void*)c->d_wio, (void*)c->d_bad})
         if (p) (void)hipFree(p);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1672,7 +1762,7 @@ int mkacc_upload_keys_device(mkacc_ctx* c, const void* d_evk, const void* d_pkey
     return upload_keys_device_impl(c, (const uint64_t*)d_evk, (const uint64_t*)d_pkey);
 }
 
-int mkacc_is_wide(const mkacc_ctx* c) { return c && c->wide ? 1 : 0; }
+int mkacc_is_wide(const mkacc_ctx* c) { return c && c->wide ? (c->wfp ? 2 : 1) : 0; }
 
 int mkacc_eval_batch_u64(mkacc_ctx* c, const uint32_t* ct, const uint64_t* acc_in, uint64_t* acc_out, size_t B) {
     if (!c || !ct || !acc_in || !acc_out) return fail(MKACC_E_ARG, "null argument");

@@ -77,6 +77,44 @@ def test_wide_evalacc_bitexact(mk_gpu, oracle, method, k, n, baseG, B):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("fp", ["1", "0"])
+@pytest.mark.parametrize("method", ["XZW", "XZW_B"])
+def test_wide_fp64_and_integer_variants(mk_gpu, oracle, monkeypatch, method, fp):
+    """Q < 2^50 runs the FP64 variant (mkacc_widefp.hpp) unless MKACC_WIDE_FP=0
+    keeps the integer kernels: both bit-exact.  The first step's digit
+    decomposition sees chosen coefficients (acc = NTT(coefficients)): 0, 1,
+    Q-1 and the centring boundary Q>>1, (Q>>1)+1 where the FP64 path picks the
+    reference's representative explicitly; keys include all-maximal and
+    balanced-boundary words.  (The device-pointer key upload of this path is
+    exercised by every bench.py --q-bits 50 run, whose oracle check covers it.)"""
+    mk = mk_gpu
+    monkeypatch.setenv("MKACC_WIDE_FP", fp)
+    m = oracle.XZW if method == "XZW" else oracle.XZW_B
+    k, n, B = 2, 3, 3
+    orc, evk, pkey, ct, acc = make_case(oracle, m, k, n, 45181, 1 << 10, B, seed=50 + len(method), Q=Q50)
+    h = Q50 >> 1
+    edge = np.array([0, 1, Q50 - 1, h, h + 1, h - 1, 2, Q50 - 2], dtype=np.uint64)
+    coef = oracle.fill_uniform(N, Q50, 77)
+    coef[:8] = edge
+    coef[-8:] = edge
+    acc[0, 0] = oracle.ntt_forward(coef, Q50, PSI50)
+    acc[1, 1] = oracle.ntt_forward(np.full(N, h, np.uint64), Q50, PSI50)
+    evk.reshape(-1)[:4] = [Q50 - 1, h, h + 1, 0]
+    pkey.reshape(-1)[:4] = [Q50 - 1, h, h + 1, 0]
+    exp = orc.evalacc_batch(evk, pkey, ct, acc, 4)
+    eng = _eng(mk, mk.MKNTRU if method == "XZW" else mk.MKNTRU_LWE, k, n, Q50, 45181, 1 << 10)
+    assert eng.wide
+    eng.upload_keys(evk.astype(np.uint64), pkey.astype(np.uint64))
+    got = eng.eval_batch(ct.astype(np.uint32), acc.astype(np.uint64))
+    assert np.array_equal(got, exp), int(np.count_nonzero(got != exp))
+    # primitives at the same modulus
+    a = np.stack([coef, oracle.fill_uniform(N, Q50, 78)])
+    f = eng.ntt_forward(a)
+    assert np.array_equal(f, np.stack([oracle.ntt_forward(x, Q50, PSI50) for x in a]))
+    assert np.array_equal(eng.ntt_inverse(f), a)
+
+
+@pytest.mark.gpu
 def test_wide_path_matches_fast_path_at_27_bits(mk_gpu, oracle):
     """MKACC_ENGINE=wide forces the 64-bit path on a 27-bit Q: both engines agree bit for bit."""
     mk = mk_gpu
