@@ -242,6 +242,25 @@ __global__ __launch_bounds__(kThreads, MKACC_WFP_WG_PER_CU) void step_kernel(Ste
     double sv[kPer];
 #pragma unroll
     for (int e = 0; e < kPer; ++e) sv[e] = 0.0;
+#ifndef MKACC_WFP_HOIST_MONO
+#define MKACC_WFP_HOIST_MONO 1
+#endif
+    // X^-c at this thread's slots: the same for every digit and party of the step,
+    // gathered once (instead of (k+1) dg times) and kept in 16 VGPRs
+    double mn[kPer];
+    if (METHOD == XZW && MKACC_WFP_HOIST_MONO) {
+#pragma unroll
+        for (int e = 0; e < kPer; ++e) mn[e] = mono(rpsi, cneg, odd_exp(t + kThreads * e));
+    }
+#ifndef MKACC_WFP_HOIST_MC
+#define MKACC_WFP_HOIST_MC 1
+#endif
+    // X^c likewise (the k rotations; the KDM step's key combination)
+    double mc[kPer];
+    if (MKACC_WFP_HOIST_MC) {
+#pragma unroll
+        for (int e = 0; e < kPer; ++e) mc[e] = mono(rpsi, c, odd_exp(t + kThreads * e));
+    }
 
     for (uint32_t tt = 1; tt <= k; ++tt) {
         const uint32_t u = index + tt < k ? index + tt : index + tt - k;
@@ -251,7 +270,7 @@ __global__ __launch_bounds__(kThreads, MKACC_WFP_WG_PER_CU) void step_kernel(Ste
             const uint32_t j = t + kThreads * e;
             double x = ldd(rin, vo, u * polyB + e * slotB);
             uj[e] = FIRST ? 0.0 : x;
-            if (!FIRST) x = mm(x, mono(rpsi, c, odd_exp(j)), m) - x;   // acc * (X^c - 1)  (xzw.cpp:336-338)
+            if (!FIRST) x = mm(x, MKACC_WFP_HOIST_MC ? mc[e] : mono(rpsi, c, odd_exp(j)), m) - x;   // acc (X^c - 1)  (xzw.cpp:336-338)
             tile[j] = x;
         }
         __syncthreads();
@@ -275,8 +294,8 @@ __global__ __launch_bounds__(kThreads, MKACC_WFP_WG_PER_CU) void step_kernel(Ste
             for (int e = 0; e < kPer; ++e) {
                 const uint32_t j = t + kThreads * e, so = e * slotB;
                 const double g = red(tile[j], m);
-                const double tp = FIRST ? mono(rpsi, c, odd_exp(j)) : 0.0;
-                const double tn = METHOD == XZW ? mono(rpsi, cneg, odd_exp(j)) : 0.0;
+                const double tp = FIRST ? (MKACC_WFP_HOIST_MC ? mc[e] : mono(rpsi, c, odd_exp(j))) : 0.0;
+                const double tn = METHOD == XZW ? (MKACC_WFP_HOIST_MONO ? mn[e] : mono(rpsi, cneg, odd_exp(j))) : 0.0;
                 const double d = key_eff<METHOD, FIRST>(ldd(rk1, vo, ko + so), METHOD == XZW ? ldd(rk2, vo, ko + so) : 0.0,
                                                         FIRST ? ldd(rks, vo, ko + so) : 0.0, tp, tn, m);
                 uj[e] = red(uj[e] + mm(g, d, m), m);                    // <g^-1(c), d_i>
@@ -315,8 +334,8 @@ __global__ __launch_bounds__(kThreads, MKACC_WFP_WG_PER_CU) void step_kernel(Ste
 #pragma unroll
         for (int e = 0; e < kPer; ++e) {
             const uint32_t j = t + kThreads * e, so = e * slotB;
-            const double tp = FIRST ? mono(rpsi, c, odd_exp(j)) : 0.0;
-            const double tn = METHOD == XZW ? mono(rpsi, cneg, odd_exp(j)) : 0.0;
+            const double tp = FIRST ? (MKACC_WFP_HOIST_MC ? mc[e] : mono(rpsi, c, odd_exp(j))) : 0.0;
+            const double tn = METHOD == XZW ? (MKACC_WFP_HOIST_MONO ? mn[e] : mono(rpsi, cneg, odd_exp(j))) : 0.0;
             const double f = key_eff<METHOD, FIRST>(ldd(rk1, vo, ko + so), METHOD == XZW ? ldd(rk2, vo, ko + so) : 0.0,
                                                     FIRST ? ldd(rks, vo, ko + so) : 0.0, tp, tn, m);
             keep[e] = red(keep[e] + mm(red(tile[j], m), f, m), m);
