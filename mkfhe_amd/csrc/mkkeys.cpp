@@ -18,6 +18,7 @@
 #include <cstdio>
 #include <cstring>
 #include <random>
+#include <stdexcept>
 #include <string>
 #include <thread>
 #include <vector>
@@ -36,7 +37,11 @@ int fail(int code, const std::string& msg) {
 }
 
 // ---------------------------------------------------------------------------
-// randomness: xoshiro256** streams keyed by SplitMix64(seed, stream ids)
+// randomness.  seed != 0 (tests, reproducible runs): xoshiro256** streams keyed by
+// SplitMix64(seed, stream ids) -- fast, not cryptographic.  seed == 0 (the
+// reference's behaviour: fresh keys every call): ChaCha20 keyed with 256 bits
+// from std::random_device, one stream per (a, b, c) id in the nonce, so no
+// secret is a function of a short seed.
 // ---------------------------------------------------------------------------
 inline uint64_t splitmix(uint64_t& x) {
     uint64_t z = (x += 0x9E3779B97F4A7C15ull);
@@ -45,10 +50,77 @@ inline uint64_t splitmix(uint64_t& x) {
     return z ^ (z >> 31);
 }
 
+struct Seed {
+    uint64_t s = 0;        // explicit seed (xoshiro)
+    bool secure = false;   // ChaCha20 with key[]
+    uint32_t key[8] = {};
+};
+
+Seed resolve_seed(uint64_t seed) {
+    Seed r;
+    if (seed) {
+        r.s = seed;
+        return r;
+    }
+    std::random_device rd;
+    for (auto& w : r.key) w = rd();
+    r.secure = true;
+    return r;
+}
+
+// ChaCha20 block function (RFC 8439 s2.3, 20 rounds; 64-bit block counter and
+// 64-bit nonce as in the original construction)
+struct ChaCha20 {
+    uint32_t st[16];
+    uint32_t buf[16];
+    int pos = 16;
+    ChaCha20(const uint32_t key[8], uint32_t n0, uint32_t n1) {
+        st[0] = 0x61707865u; st[1] = 0x3320646eu; st[2] = 0x79622d32u; st[3] = 0x6b206574u;
+        for (int i = 0; i < 8; ++i) st[4 + i] = key[i];
+        st[12] = st[13] = 0;   // block counter
+        st[14] = n0;
+        st[15] = n1;
+    }
+    static uint32_t rotl(uint32_t v, int k) { return (v << k) | (v >> (32 - k)); }
+    static void qr(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d) {
+        a += b; d ^= a; d = rotl(d, 16);
+        c += d; b ^= c; b = rotl(b, 12);
+        a += b; d ^= a; d = rotl(d, 8);
+        c += d; b ^= c; b = rotl(b, 7);
+    }
+    void refill() {
+        uint32_t x[16];
+        for (int i = 0; i < 16; ++i) x[i] = st[i];
+        for (int r = 0; r < 10; ++r) {
+            qr(x[0], x[4], x[8], x[12]); qr(x[1], x[5], x[9], x[13]);
+            qr(x[2], x[6], x[10], x[14]); qr(x[3], x[7], x[11], x[15]);
+            qr(x[0], x[5], x[10], x[15]); qr(x[1], x[6], x[11], x[12]);
+            qr(x[2], x[7], x[8], x[13]); qr(x[3], x[4], x[9], x[14]);
+        }
+        for (int i = 0; i < 16; ++i) buf[i] = x[i] + st[i];
+        if (++st[12] == 0) ++st[13];
+        pos = 0;
+    }
+    uint64_t next() {
+        if (pos > 14) refill();
+        const uint64_t v = (uint64_t)buf[pos] | ((uint64_t)buf[pos + 1] << 32);
+        pos += 2;
+        return v;
+    }
+};
+
 struct Rng {
     uint64_t s[4];
-    Rng(uint64_t seed, uint64_t a, uint64_t b = 0, uint64_t c = 0) {
-        uint64_t x = seed;
+    bool secure;
+    ChaCha20 cc;
+    // stream ids: a < 2^8 (call kind), b < 2^24, c < 2^32
+    Rng(const Seed& sd, uint64_t a, uint64_t b = 0, uint64_t c = 0)
+        : secure(sd.secure), cc(sd.key, (uint32_t)(a | (b << 8)), (uint32_t)c) {
+        if (secure) {
+            if (a >= 256 || b >= (1u << 24) || c >> 32) throw std::runtime_error("random stream id out of range");
+            return;
+        }
+        uint64_t x = sd.s;
         x ^= splitmix(x) + a * 0xD1B54A32D192ED03ull;
         x ^= splitmix(x) + b * 0xABC98388FB8FAC03ull;
         x ^= splitmix(x) + c * 0x8CB92BA72F3D8DD7ull;
@@ -56,6 +128,7 @@ struct Rng {
     }
     static uint64_t rotl(uint64_t v, int k) { return (v << k) | (v >> (64 - k)); }
     uint64_t next() {
+        if (secure) return cc.next();
         const uint64_t r = rotl(s[1] * 5, 7) * 9, t = s[1] << 17;
         s[2] ^= s[0]; s[3] ^= s[1]; s[1] ^= s[2]; s[0] ^= s[3];
         s[2] ^= t; s[3] = rotl(s[3], 45);
@@ -78,12 +151,6 @@ struct Rng {
     }
     int binary() { return (int)(next() >> 63); }
 };
-
-uint64_t resolve_seed(uint64_t seed) {
-    if (seed) return seed;
-    std::random_device rd;
-    return ((uint64_t)rd() << 32) ^ rd() ^ 0x5EEDull;
-}
 
 // OpenFHE DiscreteGaussianGeneratorImpl, Peikert inversion sampling
 // (reference src/core/include/math/discretegaussiangenerator-impl.h:82-156):
@@ -412,12 +479,12 @@ size_t mkkg_ksk_mklwe_b_words(const mkkg_params* pp) {
 int mkkg_mntru_keygen(const mkkg_params* pp, uint64_t seed, uint32_t* F, uint32_t* Finv) {
     UNPACK(pp, p);
     if (!F || !Finv) return fail(MKACC_E_ARG, "null output");
-    seed = resolve_seed(seed);
+    const Seed sd = resolve_seed(seed);
     const uint32_t n = p.n, q = (uint32_t)p.qKS;
     std::vector<uint32_t> M((size_t)n * n), Mi;
     for (uint32_t u = 0; u < p.k; ++u) {
         for (uint64_t attempt = 0;; ++attempt) {
-            Rng r(seed, 1, u, attempt);
+            Rng r(sd, 1, u, attempt);
             for (auto& v : M) {
                 const int64_t x = pp->lwe_keydist == MKKG_DIST_GAUSSIAN ? (int64_t)r.normal(1.0) : r.ternary();
                 v = to_mod(x, q);
@@ -435,9 +502,9 @@ int mkkg_mntru_keygen(const mkkg_params* pp, uint64_t seed, uint32_t* F, uint32_
 int mkkg_mklwe_keygen(const mkkg_params* pp, uint64_t seed, uint32_t* s) {
     UNPACK(pp, p);
     if (!s) return fail(MKACC_E_ARG, "null output");
-    seed = resolve_seed(seed);
+    const Seed sd = resolve_seed(seed);
     for (uint32_t u = 0; u < p.k; ++u) {
-        Rng r(seed, 2, u);
+        Rng r(sd, 2, u);
         for (uint32_t i = 0; i < p.n; ++i) s[(size_t)u * p.n + i] = (uint32_t)r.binary();
     }
     return MKACC_OK;
@@ -447,11 +514,11 @@ int mkkg_mklwe_keygen(const mkkg_params* pp, uint64_t seed, uint32_t* s) {
 int mkkg_crs(const mkkg_params* pp, uint64_t seed, uint32_t* crs) {
     UNPACK(pp, p);
     if (!crs) return fail(MKACC_E_ARG, "null output");
-    seed = resolve_seed(seed);
+    const Seed sd = resolve_seed(seed);
     const Ring R(p.N, p.Q, p.root);
     const Dgg g(pp->sigma_unienc);
     for (uint32_t i = 0; i < p.dg; ++i) {
-        Rng r(seed, 3, i);
+        Rng r(sd, 3, i);
         sample_poly_eval(R, g, r, crs + (size_t)i * p.N);
     }
     return MKACC_OK;
@@ -464,13 +531,13 @@ int mkkg_ring_secrets(const mkkg_params* pp, uint64_t seed, uint32_t* skN, uint3
                       uint32_t* skNinv_eval) {
     UNPACK(pp, p);
     if (!skN || !skN_eval || !skNinv_eval) return fail(MKACC_E_ARG, "null output");
-    seed = resolve_seed(seed);
+    const Seed sd = resolve_seed(seed);
     const Ring R(p.N, p.Q, p.root);
     const uint32_t N = p.N;
     std::vector<uint32_t> c(N), e(N);
     for (uint32_t u = 0; u < p.k; ++u) {
         for (uint64_t attempt = 0;; ++attempt) {
-            Rng r(seed, 4, u, attempt);
+            Rng r(sd, 4, u, attempt);
             for (uint32_t j = 0; j < N; ++j) {
                 const int64_t x = pp->ring_keydist == MKKG_DIST_TERNARY ? r.ternary() : (int64_t)r.normal(0.5);
                 c[j] = to_mod(x, p.Q);
@@ -491,14 +558,14 @@ int mkkg_ring_secrets(const mkkg_params* pp, uint64_t seed, uint32_t* skN, uint3
 int mkkg_pkey(const mkkg_params* pp, uint64_t seed, const uint32_t* crs, const uint32_t* skN_eval, uint32_t* pkey) {
     UNPACK(pp, p);
     if (!crs || !skN_eval || !pkey) return fail(MKACC_E_ARG, "null argument");
-    seed = resolve_seed(seed);
+    const Seed sd = resolve_seed(seed);
     const Ring R(p.N, p.Q, p.root);
     const Dgg g(pp->sigma_unienc);
     const uint32_t N = p.N;
     std::vector<uint32_t> e(N);
     for (uint32_t u = 0; u < p.k; ++u)
         for (uint32_t i = 0; i < p.dg; ++i) {
-            Rng r(seed, 5, u, i);
+            Rng r(sd, 5, u, i);
             sample_poly_eval(R, g, r, e.data());
             uint32_t* out = pkey + ((size_t)u * p.dg + i) * N;
             for (uint32_t j = 0; j < N; ++j) {
@@ -517,7 +584,7 @@ int mkkg_acc_keygen(const mkkg_params* pp, uint64_t seed, const uint32_t* crs, c
                     const uint32_t* lwe_sk, uint32_t* evk) {
     UNPACK(pp, p);
     if (!crs || !skNinv_eval || !lwe_sk || !evk) return fail(MKACC_E_ARG, "null argument");
-    seed = resolve_seed(seed);
+    const Seed sd = resolve_seed(seed);
     const Ring R(p.N, p.Q, p.root);
     const Dgg dgg(pp->sigma_unienc), dggR(pp->sigma_r);
     const size_t key_words = (size_t)p.dg * 2 * p.N;
@@ -544,7 +611,7 @@ int mkkg_acc_keygen(const mkkg_params* pp, uint64_t seed, const uint32_t* crs, c
             std::memset(out, 0, key_words * 4);
             return;
         }
-        Rng r(seed, 6, idx);
+        Rng r(sd, 6, idx);
         unienc_key(p, R, dgg, dggR, r, crs, sinv, m, kdm, out);
     });
     return MKACC_OK;
@@ -564,7 +631,7 @@ int mkkg_acc_keygen(const mkkg_params* pp, uint64_t seed, const uint32_t* crs, c
 int mkkg_ksk_mntru(const mkkg_params* pp, uint64_t seed, const uint32_t* skN, const uint32_t* Finv, uint32_t* ksk) {
     UNPACK(pp, p);
     if (!skN || !Finv || !ksk) return fail(MKACC_E_ARG, "null argument");
-    seed = resolve_seed(seed);
+    const Seed sd = resolve_seed(seed);
     const uint32_t n = p.n, rows = p.N * p.dks;
     const uint64_t qKS = p.qKS;
     const Dgg dgg(pp->sigma);
@@ -576,7 +643,7 @@ int mkkg_ksk_mntru(const mkkg_params* pp, uint64_t seed, const uint32_t* skN, co
             std::vector<int32_t> e(n);
             std::vector<int32_t> acc(n);
             for (uint32_t row = (uint32_t)blk * 64; row < std::min<uint32_t>(rows, (uint32_t)blk * 64 + 64); ++row) {
-                Rng r(seed, 7, u, row);
+                Rng r(sd, 7, u, row);
                 for (uint32_t l = 0; l < n; ++l) e[l] = dgg.sample(r);
                 const uint32_t i = row / p.dks, t = row % p.dks;
                 uint64_t pw = 1;
@@ -606,7 +673,7 @@ int mkkg_ksk_mklwe(const mkkg_params* pp, uint64_t seed, const uint32_t* skN, co
                    uint32_t* B) {
     UNPACK(pp, p);
     if (!skN || !s || !A || !B) return fail(MKACC_E_ARG, "null argument");
-    seed = resolve_seed(seed);
+    const Seed sd = resolve_seed(seed);
     const uint32_t n = p.n;
     const uint64_t qKS = p.qKS;
     const Dgg dgg(pp->sigma);
@@ -614,7 +681,7 @@ int mkkg_ksk_mklwe(const mkkg_params* pp, uint64_t seed, const uint32_t* skN, co
         const uint32_t u = (uint32_t)(ui / p.N), i = (uint32_t)(ui % p.N);
         const uint32_t svN = switch_mod(skN[(size_t)u * p.N + i], p.Q, qKS);
         const uint32_t* sv = s + (size_t)u * n;
-        Rng r(seed, 8, ui);
+        Rng r(sd, 8, ui);
         for (uint32_t j = 0; j < p.baseKS; ++j) {
             uint64_t dig = 1;
             for (uint32_t t = 0; t < p.dks; ++t, dig *= p.baseKS) {
@@ -663,10 +730,10 @@ int mkkg_mntru_encrypt(const mkkg_params* pp, uint64_t seed, const uint32_t* Fin
     UNPACK(pp, p);
     if (!Finv || !m || !ct) return fail(MKACC_E_ARG, "null argument");
     if (pt < 2) return fail(MKACC_E_ARG, "plaintext modulus must be >= 2");
-    seed = resolve_seed(seed);
+    const Seed sd = resolve_seed(seed);
     const Dgg dgg(pp->sigma);
     parallel_for(count, [&](size_t c) {
-        Rng r(seed, 9, c);
+        Rng r(sd, 9, c);
         const uint32_t delta = (uint32_t)((m[c] % pt) * (p.q / pt));
         mntru_encrypt_one(p, dgg, r, Finv, delta, ct + c * p.k * p.n);
     });
@@ -677,9 +744,9 @@ int mkkg_mntru_encrypt(const mkkg_params* pp, uint64_t seed, const uint32_t* Fin
 int mkkg_mntru_ctgate(const mkkg_params* pp, uint64_t seed, const uint32_t* Finv, uint32_t* ct_nand) {
     UNPACK(pp, p);
     if (!Finv || !ct_nand) return fail(MKACC_E_ARG, "null argument");
-    seed = resolve_seed(seed);
+    const Seed sd = resolve_seed(seed);
     const Dgg dgg(pp->sigma);
-    Rng r(seed, 10);
+    Rng r(sd, 10);
     mntru_encrypt_one(p, dgg, r, Finv, (uint32_t)(5 * p.q / 8), ct_nand);
     return MKACC_OK;
 }
@@ -720,11 +787,11 @@ int mkkg_mklwe_encrypt(const mkkg_params* pp, uint64_t seed, const uint32_t* s, 
     UNPACK(pp, p);
     if (!s || !m || !a || !b) return fail(MKACC_E_ARG, "null argument");
     if (pt < 2) return fail(MKACC_E_ARG, "plaintext modulus must be >= 2");
-    seed = resolve_seed(seed);
+    const Seed sd = resolve_seed(seed);
     const Dgg err(pp->sigma), dga(1.0);
     const uint64_t q = p.q;
     parallel_for(count, [&](size_t c) {
-        Rng r(seed, 11, c);
+        Rng r(sd, 11, c);
         int64_t bb = (int64_t)((m[c] % pt) * (q / pt)) + err.sample(r);
         for (uint32_t u = 0; u < p.k; ++u)
             for (uint32_t i = 0; i < p.n; ++i) {

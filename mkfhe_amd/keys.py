@@ -188,27 +188,28 @@ def ring_secrets(p: MkkgParams, seed: int):
 
 def bt_keygen(p: MkkgParams, sk, seed: int = 0, crs_seed: int | None = None) -> UniEncBTKey:
     """MKKeyGen for an MNTRU (binfhe-base-scheme.cpp:198-277) or MKLWE (:279-338) secret key."""
-    import secrets
-    if seed == 0:
-        seed = secrets.randbits(63) | 1
+    # seed 0: every call below draws its own 256-bit key (ChaCha20, mkkeys.cpp),
+    # the CRS included; a nonzero seed gives reproducible (non-cryptographic) keys
+    def sub(i):
+        return seed + i if seed else 0
     L = load()
     k, n, N, dg, nk, dks = dims(p)
-    c = crs(p, crs_seed if crs_seed is not None else seed ^ 0xC25)
-    skN, skN_eval, skNinv = ring_secrets(p, seed + 1)
+    c = crs(p, crs_seed if crs_seed is not None else (seed ^ 0xC25 if seed else 0))
+    skN, skN_eval, skNinv = ring_secrets(p, sub(1))
     pkey = np.empty((k, dg, N), np.uint32)
-    _check(L.mkkg_pkey(ctypes.byref(p), seed + 2, _p(c), _p(skN_eval), _p(pkey)))
+    _check(L.mkkg_pkey(ctypes.byref(p), sub(2), _p(c), _p(skN_eval), _p(pkey)))
     evk = np.empty((k, nk, n + 1, dg, 2, N), np.uint32)
     lwe_sk = _in(sk.F_col0 if isinstance(sk, MNTRUPrivateKey) else sk.s)
-    _check(L.mkkg_acc_keygen(ctypes.byref(p), seed + 3, _p(c), _p(skNinv), _p(lwe_sk), _p(evk)))
+    _check(L.mkkg_acc_keygen(ctypes.byref(p), sub(3), _p(c), _p(skNinv), _p(lwe_sk), _p(evk)))
     key = UniEncBTKey(c, skN, skN_eval, skNinv, pkey, evk)
     if isinstance(sk, MNTRUPrivateKey):
         key.ksk = np.empty((k, N * dks, n), np.uint32)
-        _check(L.mkkg_ksk_mntru(ctypes.byref(p), seed + 4, _p(skN), _p(_in(sk.Finv)), _p(key.ksk)))
+        _check(L.mkkg_ksk_mntru(ctypes.byref(p), sub(4), _p(skN), _p(_in(sk.Finv)), _p(key.ksk)))
     else:
         B = p.ks.baseKS
         key.ksk_A = np.empty((k, N, B, dks, n), np.uint32)
         key.ksk_B = np.empty((k, N, B, dks), np.uint32)
-        _check(L.mkkg_ksk_mklwe(ctypes.byref(p), seed + 4, _p(skN), _p(_in(sk.s)), _p(key.ksk_A), _p(key.ksk_B)))
+        _check(L.mkkg_ksk_mklwe(ctypes.byref(p), sub(4), _p(skN), _p(_in(sk.s)), _p(key.ksk_A), _p(key.ksk_B)))
     return key
 
 

@@ -94,6 +94,25 @@ def test_keygen_is_deterministic_and_thread_independent(lib):
     assert not np.array_equal(a.F, c.F)
 
 
+def test_seed_zero_draws_fresh_csprng_keys(lib):
+    """seed 0 (the reference's behaviour): each call keys ChaCha20 with 256 fresh bits
+    (mkkeys.cpp), so two key sets differ everywhere, the CRS included, and they are
+    valid keys (s s^-1 = 1, Pkey + CRS s small, encryptions round trip)."""
+    p = K.paramset("STD100_MKNTRU", 0)
+    a, b = K.mntru_keygen(p, 0), K.mntru_keygen(p, 0)
+    assert not np.array_equal(a.F, b.F)
+    bk1, bk2 = K.bt_keygen(p, a), K.bt_keygen(p, a)
+    for f in ("crs", "skN", "pkey", "evk", "ksk"):
+        assert not np.array_equal(getattr(bk1, f), getattr(bk2, f)), f
+    Q = p.acc.Q
+    assert np.all((bk1.skN_eval.astype(np.uint64) * bk1.skNinv_eval) % Q == 1)
+    for u in range(p.acc.k):
+        e_eval = (bk1.pkey[u, 0].astype(np.uint64) + bk1.crs[0].astype(np.uint64) * bk1.skN_eval[u] % Q) % Q
+        assert np.abs(centred(K.ntt_inverse(p, e_eval.astype(np.uint32)), Q)).max() <= 3
+    m = np.random.default_rng(3).integers(0, 2, 64)
+    assert np.array_equal(K.mntru_decrypt(p, a, K.mntru_encrypt(p, a, m), variant=K.DECRYPT2), m)
+
+
 @pytest.fixture(scope="module")
 def mntru_keys(lib):
     p = K.paramset("STD100_MKNTRU", 0)
