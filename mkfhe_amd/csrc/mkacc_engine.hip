@@ -488,6 +488,8 @@ __device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_
 
 template <int DG, int METHOD, bool FIRST, bool DSCR>
 __device__ __forceinline__ void step_body(const StepCtx& s, uint32_t k, uint32_t index);
+template <int DG, int METHOD, bool FIRST>
+__device__ __forceinline__ void f_part(const StepCtx& s, uint32_t index, uint64_t (&w)[kRegs], uint32_t (&x)[kRegs]);
 
 // DSCR: d_i computed once per step and gate (first party pass) and reloaded from
 // a.dscr by the other k - 1 passes (DigitMac DS); the host picks it by k.
@@ -526,6 +528,69 @@ __global__ __launch_bounds__(kThreads, 2) void mk_step_kernel(StepArgs a) {
     step_body<DG, METHOD, FIRST, DSCR>(s, k, a.index);
 }
 
+// Small batches (host: use_lat): one workgroup per gate and one wave per party,
+// so the k party passes of a step run concurrently and only the f-part is
+// serial -- 2 (dg + 1) transforms on a step's critical path instead of
+// (k + 1)(dg + 1).  The same party_pass / f_part code as mk_step_kernel: each
+// wave's sumV covers its own party; it is reduced to [0, 2Q), summed through
+// LDS by the wave of party `index`, which then runs the f-part alone (the
+// sums are exact mod Q, so the grouping is bit-exact).
+constexpr uint32_t kLatMaxK = 8;
+constexpr size_t lat_lds_bytes(uint32_t k) { return (size_t)(kLdsTabWords + k * kLdsWords) * 4; }
+template <int DG, int METHOD, bool FIRST>
+__global__ __launch_bounds__(64 * kLatMaxK, 1) void mk_lat_kernel(StepArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    load_image(smem, a.img);
+    const uint32_t l = threadIdx.x & 63u;
+    const uint32_t u = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // this wave's party
+    const uint32_t gate = blockIdx.x;
+    const uint32_t c = __builtin_amdgcn_readfirstlane(a.cvals[gate]);
+    const uint32_t cneg = (2u * kN - c) & (2u * kN - 1u);
+    const uint32_t k = a.k, index = a.index;
+    const uint32_t polyB = kN * 4u;
+    uint32_t* scratch = smem + kLdsTabWords + u * kLdsWords;
+    const StepCtx s{tables(smem, a.img),
+                    scratch,
+                    a.tw_fwd,
+                    a.tw_inv,
+                    a.m,
+                    a.sd,
+                    make_mono(c, l),
+                    make_mono(FIRST || METHOD != XZW ? cneg : (cneg + kN) & (2u * kN - 1u), l),
+                    l,
+                    l * 16u,
+                    make_rsrc(a.acc_in + (size_t)gate * k * kN, k * polyB),
+                    make_rsrc(a.acc_out + (size_t)gate * k * kN, k * polyB),
+                    make_rsrc(a.key1, DG * 2 * polyB),
+                    make_rsrc(a.key2, DG * 2 * polyB),
+                    make_rsrc(a.keys, DG * 2 * polyB),
+                    make_rsrc(a.pkey, k * DG * polyB),
+                    make_rsrc(a.acc_in, 0u)};
+    const uint32_t Q = s.m.Q;
+    uint64_t sv[kRegs], w[kRegs];
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) sv[r] = 0;
+    if (u == index)
+        party_pass<DG, METHOD, FIRST, true>(s, u, sv, w);
+    else
+        party_pass<DG, METHOD, FIRST, false>(s, u, sv, w);
+    // this party's sumV share, [0, 2Q), into the wave's own (now idle) scratch
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) scratch[r * 64 + l] = redc(sv[r], Q, s.m.qinv);
+    __syncthreads();
+    if (u != index) return;
+    uint32_t x[kRegs];
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) {
+        uint32_t v = 0;
+        for (uint32_t p = 0; p < k; ++p) v += smem[kLdsTabWords + p * kLdsWords + r * 64 + l];   // < 16 Q
+        v = min(v, v - 8u * Q);
+        v = min(v, v - 4u * Q);
+        x[r] = min(v, v - 2u * Q);                                                               // [0, 2Q)
+    }
+    f_part<DG, METHOD, FIRST>(s, index, w, x);
+}
+
 // One accumulator step for one gate per wavefront.
 //   FIRST:  AddToAccXZW0 (mk-acc-xzw.cpp:347-381 / xzw_B.cpp:333-381): acc <- HbProd(acc)
 //   else:   AddToAccXZW  (mk-acc-xzw.cpp:292-345 / xzw_B.cpp:281-330):
@@ -539,8 +604,6 @@ template <int DG, int METHOD, bool FIRST, bool DSCR>
 __device__ __forceinline__ void step_body(const StepCtx& s, uint32_t k, uint32_t index) {
     using Bd = Bounds<DG, METHOD, FIRST>;
     const uint32_t Q = s.m.Q;
-    const uint32_t l = s.l;
-    const uint32_t polyB = kN * 4u;
     uint64_t sv[kRegs];
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) sv[r] = 0;
@@ -569,6 +632,21 @@ __device__ __forceinline__ void step_body(const StepCtx& s, uint32_t k, uint32_t
         grow_sv();
     }
     party_pass<DG, METHOD, FIRST, true, DSCR ? 2 : 0>(s, index, sv, w);
+    uint32_t x[kRegs];
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) x[r] = redc(sv[r], Q, s.m.qinv);
+    f_part<DG, METHOD, FIRST>(s, index, w, x);
+}
+
+// Second half of HbProd for party `index` (mk-acc-xzw.cpp:272-289) and the
+// final store of acc[index]: w = its folded party sum (party_pass LAST),
+// x = sumV in [0, 2Q).  iNTT(sumV) -> SDD -> NTT -> acc[index] += <., f>.
+template <int DG, int METHOD, bool FIRST>
+__device__ __forceinline__ void f_part(const StepCtx& s, uint32_t index, uint64_t (&w)[kRegs], uint32_t (&x)[kRegs]) {
+    using Bd = Bounds<DG, METHOD, FIRST>;
+    const uint32_t Q = s.m.Q;
+    const uint32_t l = s.l;
+    const uint32_t polyB = kN * 4u;
     if constexpr (!Bd::kAccInSum && !FIRST) {
         // acc[index] joins the f-part sum (Bounds: < 4 Q^2 with the folded party sum)
 #pragma unroll
@@ -579,11 +657,7 @@ __device__ __forceinline__ void step_body(const StepCtx& s, uint32_t k, uint32_t
         }
     }
 
-    // second half of HbProd: iNTT(sumV) -> SDD -> NTT -> acc[index] += <., f>
     const StepRes sr = s.res();
-    uint32_t x[kRegs];
-#pragma unroll
-    for (int r = 0; r < kRegs; ++r) x[r] = redc(sv[r], Q, s.m.qinv);
     ntt_inv(x, s.lds, s.tw_inv, s.tb.twi, l, Q);
     PackedDigits<DG> pd;
 #pragma unroll
@@ -777,6 +851,13 @@ StepFn pick_step(int method, bool first, bool dscr) {
 
 StepFn step_fn(int dg, int method, bool first, bool dscr);
 
+template <int DG>
+StepFn pick_lat(int method, bool first) {
+    if (method == XZW) return first ? mk_lat_kernel<DG, XZW, true> : mk_lat_kernel<DG, XZW, false>;
+    return first ? mk_lat_kernel<DG, XZW_B, true> : mk_lat_kernel<DG, XZW_B, false>;
+}
+StepFn lat_fn(int dg, int method, bool first);
+
 }  // namespace
 
 #include "mkacc_gate.hpp"
@@ -825,6 +906,20 @@ StepFn step_fn(int dg, int method, bool first, bool dscr) {
 #endif
 #if !defined(MKACC_ONLY_DG) || MKACC_ONLY_DG == 5
         case 5: return pick_step<5>(method, first, dscr);
+#endif
+        default: return nullptr;
+    }
+}
+StepFn lat_fn(int dg, int method, bool first) {
+    switch (dg) {
+#if !defined(MKACC_ONLY_DG) || MKACC_ONLY_DG == 2
+        case 2: return pick_lat<2>(method, first);
+#endif
+#if !defined(MKACC_ONLY_DG) || MKACC_ONLY_DG == 3
+        case 3: return pick_lat<3>(method, first);
+#endif
+#if !defined(MKACC_ONLY_DG) || MKACC_ONLY_DG == 4
+        case 4: return pick_lat<4>(method, first);
 #endif
         default: return nullptr;
     }
@@ -923,6 +1018,17 @@ bool use_dscr(const mkacc_ctx* c) {
     return c->p.k >= kDscrMinK;
 }
 
+// Small batches take mk_lat_kernel (one wave per party): while B k waves fit
+// the chip's 2048 step-kernel wave slots it lowers the step's critical path;
+// MKACC_LAT=0/1 overrides.  Not built for dg = 5 or k > kLatMaxK.
+constexpr size_t kLatSlots = 2048;
+bool use_lat(const mkacc_ctx* c, size_t B) {
+    if (c->p.k < 2 || c->p.k > kLatMaxK || c->dg > 4) return false;
+    const char* e = std::getenv("MKACC_LAT");
+    if (e && *e) return e[0] != '0';
+    return B * c->p.k <= kLatSlots;
+}
+
 int ensure_ws(mkacc_ctx* c, size_t B) {
     if (B <= c->ws_B) return MKACC_OK;
     if (c->d_acc0) HIP_TRY(hipFree(c->d_acc0));
@@ -952,6 +1058,7 @@ uint32_t* launch_steps(mkacc_ctx* c, size_t B) {
     // workgroup; 10240 leaves one workgroup per CU, the co-residency reference
     const char* dl = std::getenv("MKACC_DBG_LDS");
     const size_t lds = kStepLdsBytes + (dl ? std::strtoul(dl, nullptr, 0) : 0);
+    const bool lat = use_lat(c, B);
     for (uint32_t u = 0; u < k; ++u) {
         for (uint32_t i = 0; i < n; ++i) {
             const bool first = (u == 0 && i == 0);
@@ -972,8 +1079,13 @@ uint32_t* launch_steps(mkacc_ctx* c, size_t B) {
             a.m = c->mod;
             a.sd = c->sd;
             a.dscr = c->d_dscr;
-            StepFn fn = step_fn((int)c->dg, c->method_class, first, !first && c->d_dscr != nullptr);
-            hipLaunchKernelGGL(fn, grid, block, lds, c->stream, a);
+            if (lat) {
+                hipLaunchKernelGGL(lat_fn((int)c->dg, c->method_class, first), dim3((unsigned)B), dim3(64 * k),
+                                   lat_lds_bytes(k), c->stream, a);
+            } else {
+                StepFn fn = step_fn((int)c->dg, c->method_class, first, !first && c->d_dscr != nullptr);
+                hipLaunchKernelGGL(fn, grid, block, lds, c->stream, a);
+            }
             std::swap(cur, nxt);
         }
     }

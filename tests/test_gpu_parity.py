@@ -115,9 +115,32 @@ def test_evalacc_dscr_modes(mk, oracle, case, dscr, monkeypatch):
     picks by k, MKACC_DSCR forces one) give the oracle's accumulators."""
     meth, k, n, q, baseG, B = case
     monkeypatch.setenv("MKACC_DSCR", dscr)   # read when the context sizes its workspace
+    monkeypatch.setenv("MKACC_LAT", "0")     # the batch step kernel (small B would take mk_lat_kernel)
     orc, evk, pkey, ct, acc = make_case(oracle, oracle.XZW, k, n, q, baseG, B + 2, seed=k * 31 + n)
     exp = orc.evalacc_batch(evk, pkey, ct, acc, 8)
     eng = mk.MKAccumulatorEngine(mk.make_params(mk.MKNTRU, k, n, 2048, Q_MK, q, baseG))
+    eng.upload_keys(evk.astype(np.uint32), pkey.astype(np.uint32))
+    got = eng.eval_batch(ct.astype(np.uint32), acc.astype(np.uint32))
+    assert np.array_equal(got, exp.astype(np.uint32))
+
+
+LAT_CASES = [c for c in CASES if 2 <= c[1] <= 8 and c[4] != 1 << 5]
+
+
+@pytest.mark.parametrize("lat", ["1", "0"])
+@pytest.mark.parametrize("case", LAT_CASES,
+                         ids=[f"{c[0]}-k{c[1]}-logB{c[4].bit_length() - 1}" for c in LAT_CASES])
+def test_evalacc_small_batch_kernel(mk, oracle, case, lat, monkeypatch):
+    """The one-wave-per-party step kernel (mk_lat_kernel, chosen for small
+    batches; MKACC_LAT forces it on or off) gives the oracle's accumulators for
+    both methods, k = 2..8 parties and dg = 2..4."""
+    meth, k, n, q, baseG, B = case
+    monkeypatch.setenv("MKACC_LAT", lat)   # read at every launch
+    om = oracle.XZW if meth == "XZW" else oracle.XZW_B
+    em = mk.MKNTRU if meth == "XZW" else mk.MKNTRU_LWE
+    orc, evk, pkey, ct, acc = make_case(oracle, om, k, n, q, baseG, B + 1, seed=k * 13 + n)
+    exp = orc.evalacc_batch(evk, pkey, ct, acc, 8)
+    eng = mk.MKAccumulatorEngine(mk.make_params(em, k, n, 2048, Q_MK, q, baseG))
     eng.upload_keys(evk.astype(np.uint32), pkey.astype(np.uint32))
     got = eng.eval_batch(ct.astype(np.uint32), acc.astype(np.uint32))
     assert np.array_equal(got, exp.astype(np.uint32))
@@ -184,10 +207,13 @@ def test_errors(mk, oracle):
     assert eng.eval_batch(ct[:0], acc[:0]).shape == (0, 2, 2048)
 
 
-def test_evalacc_many_gates_every_wave_slot(mk, oracle):
+@pytest.mark.parametrize("lat", ["0", "1"])
+def test_evalacc_many_gates_every_wave_slot(mk, oracle, lat, monkeypatch):
     """512 gates (every wave slot of every workgroup, all CUs partly busy),
-    three repeated runs: bit-exact and run-to-run identical.  Guards against
-    the nondeterminism seen with 512-thread workgroups."""
+    three repeated runs: bit-exact and run-to-run identical, with the batch
+    step kernel and with the one-wave-per-party kernel.  Guards against the
+    co-resident-workgroup corruption of round 1."""
+    monkeypatch.setenv("MKACC_LAT", lat)
     B = 512
     orc, evk, pkey, ct, acc = make_case(oracle, oracle.XZW, 2, 2, 45181, 1 << 7, B, seed=77)
     exp = orc.evalacc_batch(evk, pkey, ct, acc, 16).astype(np.uint32)
