@@ -932,6 +932,7 @@ StepFn lat_fn(int dg, int method, bool first) {
 struct mkacc_ctx {
     mkacc_params p{};
     int device = 0;
+    int cus = 256;                // compute units of the device (mk_lat_kernel residency)
     int method_class = XZW;   // XZW or XZW_B
     uint32_t dg = 0, nk = 0;
     Mod mod{};
@@ -1018,15 +1019,18 @@ bool use_dscr(const mkacc_ctx* c) {
     return c->p.k >= kDscrMinK;
 }
 
-// Small batches take mk_lat_kernel (one wave per party): while B k waves fit
-// the chip's 2048 step-kernel wave slots it lowers the step's critical path;
-// MKACC_LAT=0/1 overrides.  Not built for dg = 5 or k > kLatMaxK.
-constexpr size_t kLatSlots = 2048;
+// Small batches take mk_lat_kernel (one wave per party) while the whole batch
+// is resident in one round: its workgroups are LDS-bound (tables + k
+// scratches: 2 per CU at k = 2..4, 1 at k = 8), and a second round costs more
+// than the shorter critical path saves (B = 1024, k = 2: 160 ms against 109 ms
+// for the batch kernel, profiles/r2/latency_v2_*.jsonl).  MKACC_LAT=0/1
+// overrides.  Not built for dg = 5 or k > kLatMaxK.
+constexpr size_t kLdsPerCu = 160 * 1024;
 bool use_lat(const mkacc_ctx* c, size_t B) {
     if (c->p.k < 2 || c->p.k > kLatMaxK || c->dg > 4) return false;
     const char* e = std::getenv("MKACC_LAT");
     if (e && *e) return e[0] != '0';
-    return B * c->p.k <= kLatSlots;
+    return B <= (size_t)c->cus * (kLdsPerCu / lat_lds_bytes(c->p.k));
 }
 
 int ensure_ws(mkacc_ctx* c, size_t B) {
@@ -1715,6 +1719,11 @@ int mkacc_create(const mkacc_params* pin, int device, mkacc_ctx** out) {
     auto c = std::make_unique<mkacc_ctx>();
     c->p = p;
     c->device = device;
+    {
+        int ncu = 0;
+        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
+            c->cus = ncu;
+    }
     c->method_class = p.method == MKACC_METHOD_MKNTRU ? XZW : XZW_B;
     c->dg = dg;
     c->nk = c->method_class == XZW ? 2 : 1;
