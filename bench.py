@@ -57,6 +57,8 @@ Q50 = 1125899906826241               # config 5 stress modulus (SURVEY.md s0 ite
 REF_CPU_S_PER_EVALACC = {            # reference EvalAcc, 1 core of the survey container
     "STD100_MKNTRU": 0.274, "STD128_MKNTRU": 0.475, "STD100_MKNTRU_LWE": 0.215,
     "STD100_MKNTRU_LWE_2": 0.721, "STD128_MKNTRU_3": 6.750, "STD100_MKNTRU_3": 2.872}
+# oracle / reference single-thread EvalAcc time on the same container type
+ORACLE_OVER_REF = {"STD128_MKNTRU": 2.97, "STD100_MKNTRU": 2.62, "STD100_MKNTRU_LWE_2": 2.77}
 
 
 def algorithmic_counts(k: int, n: int, dg: int, nk: int, N: int = 2048, B: int = 1, word: int = 4):
@@ -417,6 +419,7 @@ def run_rank(args, env: dict, make_engine, make_checker, torch_device: str, back
                            f"thread on {threads} threads, {dt_c:.2f} s wall; the same gates are the parity check"),
                 "host": cpu,
                 "reference_1core_s_per_evalacc": ref,
+                "oracle_over_reference_1core": ORACLE_OVER_REF.get(args.paramset) if ref else None,
                 "reference_source": "SURVEY.md s6: the reference's own EvalAcc, 1 thread of the survey container",
             }
     if world > 1:

@@ -3,8 +3,10 @@
 TAG=$1; shift
 export TMPDIR=/tmp
 mkdir -p gpurun_out
+# per-GPU batch: 4096, 8192 for config 4 (65536 gates over 8 GPUs)
 for PS in STD100_MKNTRU STD100_MKNTRU_LWE_2 STD128_MKNTRU_3; do
-  timeout -k 10 300 python bench.py --paramset $PS --steps 1 --warmup 1 --cpu-baseline 0 "$@" > gpurun_out/cfg_${TAG}_$PS.json 2> gpurun_out/cfg_${TAG}_$PS.err || { echo "$PS failed"; tail -3 gpurun_out/cfg_${TAG}_$PS.err; exit 1; }
+  B=4096; [ $PS = STD128_MKNTRU_3 ] && B=8192
+  timeout -k 10 300 python bench.py --paramset $PS --batch $B --steps 1 --warmup 1 --cpu-baseline 0 "$@" > gpurun_out/cfg_${TAG}_$PS.json 2> gpurun_out/cfg_${TAG}_$PS.err || { echo "$PS failed"; tail -3 gpurun_out/cfg_${TAG}_$PS.err; exit 1; }
   python3 -c "import json,sys; d=json.load(open('gpurun_out/cfg_${TAG}_$PS.json')); print('$PS', round(d['value'],1), d['unit'], 'per_launch_us', round(d['roofline']['per_launch_us'],1))"
 done
 # config 5 stress: STD100_MKNTRU shape with the 50-bit Q (64-bit word path), with its rocprof summary
