@@ -38,8 +38,18 @@ class OrcParams(ctypes.Structure):
 def build() -> str:
     """Compile the oracle if needed (plain gcc via oracle/Makefile)."""
     src = os.path.join(_HERE, "mkfhe_oracle.c")
-    if (not os.path.exists(_LIB_PATH)) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src):
-        subprocess.check_call(["make", "-s", "-C", _HERE])
+
+    def stale():
+        return (not os.path.exists(_LIB_PATH)) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src)
+
+    if stale():
+        # the N ranks of a multi-GPU bench may all get here at once: one builds
+        import fcntl
+        os.makedirs(os.path.dirname(_LIB_PATH), exist_ok=True)
+        with open(_LIB_PATH + ".lock", "w") as lk:
+            fcntl.flock(lk, fcntl.LOCK_EX)
+            if stale():
+                subprocess.check_call(["make", "-s", "-C", _HERE])
     return _LIB_PATH
 
 
