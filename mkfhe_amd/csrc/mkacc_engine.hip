@@ -75,10 +75,17 @@ constexpr size_t kStepLdsBytes = (size_t)(kLdsTabWords + kWavesPerBlock * kLdsWo
 static_assert(kLdsTabWords % 4 == 0, "LDS tables are copied with dwordx4");
 static_assert(2 * kStepLdsBytes <= 160 * 1024, "two workgroups per CU");
 
-// Bank-spreading position of psi^e in the LDS table: the exponents a wave
-// gathers (c * (2 brv(j) + 1) mod 2N) repeat in their low 5 bits across lanes;
-// xor-ing in the next 5 bits gives ~2.6-way instead of ~10-way conflicts.
-__host__ __device__ __forceinline__ uint32_t psi_pos(uint32_t e) { return e ^ ((e >> 5) & 31u); }
+// Bank-spreading position of psi^e in the LDS table.  A wave gathers
+// e = c (2 brv6(lane) + 1) + 128 c brv5(r) mod 2N (Mono): the low 7 bits are
+// the lane's alone, the register part only moves bits 7..11.  Xor-ing bits 5..6
+// into bits 0..1 touches the low 7 bits only, so the gather address stays
+// additive in r (Mono::at: one add and one and), and it spreads the 64 lanes
+// over all 32 bank pairs of a ds_read_b64 when c is odd or 2 mod 4 -- the best
+// any swizzle of the low bits can do.  Exhaustively over all c and r (model:
+// most distinct dwords per bank, 2 = conflict-free) this averages 3.83 LDS
+// cycles per gather against 4.28 for the earlier e ^ ((e >> 5) & 31), which
+// also cost 6 VALU of address arithmetic per gather instead of 2.
+__host__ __device__ __forceinline__ uint32_t psi_pos(uint32_t e) { return e ^ ((e >> 5) & 3u); }
 
 enum { XZW = 0, XZW_B = 1 };
 
@@ -131,27 +138,31 @@ __device__ __forceinline__ Tables tables(uint32_t* smem, const uint32_t* img) {
 // Monomial X^e at EVAL slot j = (lane << 5) | r: the reference stores
 // a(psi^(2 brv(j) + 1)) at position j (transformnat-impl.h:705-760), so
 // X^c -> psi^(c (2 brv(j) + 1)), with 2 brv(j) + 1 = 128 brv5(r) + (2 brv6(lane) + 1).
-// `co` = c * (2 brv6(lane) + 1) per lane; the r part is wave-uniform.  at()
-// returns the LDS pair of psi^e - 1, i.e. the EVAL slot of X^c - 1.
+// co = c * (2 brv6(lane) + 1) per lane; the r part 128 c brv5(r) is
+// wave-uniform and moves only bits 7..11 of e, which psi_pos leaves in place, so
+// the byte offset of psi_pos(e) is (w + 1024 c brv5(r)) & 0x7fff with the per-lane
+// w = psi_pos(co mod 2N) * 8.  at() returns the LDS pair of psi^e - 1, i.e. the
+// EVAL slot of X^c - 1.
 struct Mono {
-    uint32_t co;        // per-lane c * (2 brv6(l) + 1)
+    uint32_t w;         // per lane: 8 psi_pos(c (2 brv6(l) + 1) mod 2N)
     uint32_t c;         // wave-uniform exponent
     __device__ __forceinline__ uint2 at(const uint2* psi, int r) const {
         constexpr uint32_t kBr5[32] = {0, 16, 8, 24, 4, 20, 12, 28, 2, 18, 10, 26, 6, 22, 14, 30,
                                        1, 17, 9, 25, 5, 21, 13, 29, 3, 19, 11, 27, 7, 23, 15, 31};
-        // opaque: keeps the 32 per-slot exponents from being hoisted out of the
-        // party / digit loops (they would stay live in VGPRs across the NTTs)
         // the wave-uniform part is recomputed per use (one s_mul) rather than
-        // kept as 32 hoisted SGPR constants per monomial
+        // kept as 32 hoisted SGPR constants per monomial; the add is volatile asm
+        // so the 32 per-slot addresses are not hoisted out of the party / digit
+        // loops (they would stay live in VGPRs across the NTTs)
         uint32_t cs = c;
         asm volatile("" : "+s"(cs));
-        const uint32_t e = (opaque_v(co) + cs * (128u * kBr5[r])) & (2u * kN - 1u);
-        return psi[psi_pos(e)];
+        uint32_t a;
+        asm volatile("v_add_u32 %0, %1, %2" : "=v"(a) : "s"(cs * (1024u * kBr5[r])), "v"(w));
+        return *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(psi) + (a & 0x7fffu));
     }
 };
 __device__ __forceinline__ Mono make_mono(uint32_t c, uint32_t l) {
     const uint32_t o = ((__brev(l) >> 26) << 1) | 1u;   // 2 brv6(l) + 1
-    return Mono{(uint32_t)__umul24(c, o), c};
+    return Mono{psi_pos(__umul24(c, o) & (2u * kN - 1u)) << 3, c};
 }
 
 // Lazy Shoup product x*w in [0, 2Q) (x < 2^32)
@@ -577,6 +588,14 @@ __global__ __launch_bounds__(64 * kLatMaxK, 1) void mk_lat_kernel(StepArgs a) {
     // this party's sumV share, [0, 2Q), into the wave's own (now idle) scratch
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) scratch[r * 64 + l] = redc(sv[r], Q, s.m.qinv);
+    // redc's multiply-add is inline asm that writes its carry-out to VCC; hipcc
+    // does not count it as a VALU write of VCC and computed the branch below with
+    // an SALU write of VCC on the very next instruction.  The late VALU write
+    // could land after it, zero VCC and send every wave down the index-party path
+    // (intermittent wrong acc[index]; tools/isa_audit.py checks the distance).
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 7" ::: "vcc");
+    __builtin_amdgcn_sched_barrier(0);
     __syncthreads();
     if (u != index) return;
     uint32_t x[kRegs];

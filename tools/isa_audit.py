@@ -19,6 +19,13 @@ import tempfile
 
 LLVM = "/opt/rocm/lib/llvm/bin"
 WAIT_STATES = 2
+# second check: a v_mad_u64_u32 writing its carry-out to VCC (the pinned inline-asm
+# multiply-adds of mkacc_device.hpp) must be followed by VCC_WAIT wait states before
+# any SALU instruction that writes or reads VCC, or an s_cbranch_vcc*.  hipcc does not
+# count an asm statement as a VALU write of VCC, and a late VALU write of VCC that
+# lands after the SALU's own write sent every wave of mk_lat_kernel down the
+# index-party path (intermittent wrong accumulators).
+VCC_WAIT = 8
 
 _STORE = re.compile(r"^(buffer|global|flat|scratch)_store_(dwordx3|dwordx4|b96|b128)\b")
 _VRANGE = re.compile(r"v\[(\d+):(\d+)\]|v(\d+)\b")
@@ -55,10 +62,25 @@ def writes_vgprs(mnem: str, ops: list[str]) -> set[int]:
 
 def audit(text: str, verbose: bool = False):
     kernel, insts, violations, stores = None, [], [], 0
+    vcc_sites = 0
 
     def flush():
-        nonlocal stores
+        nonlocal stores, vcc_sites
         for i, (mn, ops, line) in enumerate(insts):
+            if mn == "v_mad_u64_u32" and len(ops) > 1 and ops[1] == "vcc":
+                ws = 0
+                for mn2, ops2, line2 in insts[i + 1:]:
+                    if ws >= VCC_WAIT:
+                        break
+                    if mn2 == "s_nop":
+                        ws += int(ops2[0], 0) + 1 if ops2 else 1
+                        continue
+                    if (mn2.startswith("s_cbranch_vcc") or
+                            (mn2.startswith("s_") and any(o in ("vcc", "vcc_lo", "vcc_hi") for o in ops2))):
+                        vcc_sites += 1
+                        violations.append((kernel, line.strip(), line2.strip()))
+                        break
+                    ws += 1
             if not _STORE.match(mn):
                 continue
             stores += 1
@@ -94,15 +116,16 @@ def audit(text: str, verbose: bool = False):
         ops = [o.strip() for o in parts[1].split(",")] if len(parts) > 1 else []
         insts.append((mn, ops, s))
     flush()
-    return stores, violations
+    return stores, violations, vcc_sites
 
 
 def main() -> int:
     lib = sys.argv[1]
-    stores, bad = audit(disassemble(lib), "--verbose" in sys.argv)
+    stores, bad, vcc = audit(disassemble(lib), "--verbose" in sys.argv)
     for k, st, wr in bad[:20]:
         print(f"VIOLATION in {k}:\n    {st}\n    {wr}")
-    print(f"{os.path.basename(lib)}: {stores} stores of more than 8 bytes, {len(bad)} data-register hazards")
+    print(f"{os.path.basename(lib)}: {stores} stores of more than 8 bytes, {len(bad) - vcc} data-register hazards, "
+          f"{vcc} VCC carry-out hazards")
     return 1 if bad else 0
 
 
