@@ -9,4 +9,5 @@ for L in ${SL//,/ }; do
   rc=$?; tail -1 gpurun_out/lat_${TAG}_$(basename $L .so).txt
   [ $rc -ne 0 ] && { echo "lat stress rc=$rc"; exit $rc; }
 done
-[ $# -gt 0 ] && MKACC_LAT=0 bash tools/gpu_ab.sh $TAG "$@"
+if [ $# -gt 0 ]; then MKACC_LAT=0 PARITY_K="${PARITY_K:-logB7}" bash tools/gpu_ab.sh $TAG "$@" || exit $?; fi
+exit 0

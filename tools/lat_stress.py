@@ -21,7 +21,7 @@ def main():
     import pyoracle
     import mkfhe_amd as mk
     from conftest import Q_MK, make_case
-    k, n, q, baseG, B = 2, 16, 45181, 1 << 9, 3
+    k, n, q, baseG, B = 2, 16, 45181, 1 << 7, 3   # STD128_MKNTRU shape: dg = 3
     orc, evk, pkey, ct, acc = make_case(pyoracle, pyoracle.XZW, k, n, q, baseG, B, seed=7)
     exp = orc.evalacc_batch(evk, pkey, ct, acc, 8).astype(np.uint32)
     eng = mk.MKAccumulatorEngine(mk.make_params(mk.MKNTRU, k, n, 2048, Q_MK, q, baseG))
