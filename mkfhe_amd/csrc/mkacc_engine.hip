@@ -85,7 +85,13 @@ static_assert(2 * kStepLdsBytes <= 160 * 1024, "two workgroups per CU");
 // most distinct dwords per bank, 2 = conflict-free) this averages 3.83 LDS
 // cycles per gather against 4.28 for the earlier e ^ ((e >> 5) & 31), which
 // also cost 6 VALU of address arithmetic per gather instead of 2.
-__host__ __device__ __forceinline__ uint32_t psi_pos(uint32_t e) { return e ^ ((e >> 5) & 3u); }
+// MKACC_PSI_HI=1 (A/B): the earlier e ^ ((e >> 5) & 31), gathered with 4 VALU
+#ifndef MKACC_PSI_HI
+#define MKACC_PSI_HI 0
+#endif
+__host__ __device__ __forceinline__ uint32_t psi_pos(uint32_t e) {
+    return MKACC_PSI_HI ? e ^ ((e >> 5) & 31u) : e ^ ((e >> 5) & 3u);
+}
 
 enum { XZW = 0, XZW_B = 1 };
 
@@ -157,12 +163,15 @@ struct Mono {
         asm volatile("" : "+s"(cs));
         uint32_t a;
         asm volatile("v_add_u32 %0, %1, %2" : "=v"(a) : "s"(cs * (1024u * kBr5[r])), "v"(w));
-        return *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(psi) + (a & 0x7fffu));
+        a &= 0x7fffu;
+        if (MKACC_PSI_HI) a ^= (a >> 5) & 0xf8u;   // 8 psi_pos(e) from 8 e
+        return *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(psi) + a);
     }
 };
 __device__ __forceinline__ Mono make_mono(uint32_t c, uint32_t l) {
     const uint32_t o = ((__brev(l) >> 26) << 1) | 1u;   // 2 brv6(l) + 1
-    return Mono{psi_pos(__umul24(c, o) & (2u * kN - 1u)) << 3, c};
+    const uint32_t co = __umul24(c, o) & (2u * kN - 1u);
+    return Mono{(MKACC_PSI_HI ? co : psi_pos(co)) << 3, c};
 }
 
 // Lazy Shoup product x*w in [0, 2Q) (x < 2^32)
