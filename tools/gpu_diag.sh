@@ -13,4 +13,5 @@ for i in 1 2 3 4 5 6; do
   echo "example run $i rc=$rc: $(grep -o '= [01]' gpurun_out/ex_${TAG}_$i.txt | tr -d '= ' | tr -d '\n')"
   case $rc in 0|1) ;; *) exit $rc;; esac
 done
-[ $# -gt 0 ] && bash tools/gpu_ab.sh $TAG "$@"
+if [ $# -gt 0 ]; then bash tools/gpu_ab.sh $TAG "$@" || exit $?; fi
+exit 0
