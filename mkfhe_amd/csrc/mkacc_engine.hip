@@ -246,7 +246,10 @@ __device__ __forceinline__ void digit_range(uint32_t (&x)[kRegs], uint32_t Q) {
 // Key words of one 4-register group of a MAC: software-pipelined kPrefetch
 // groups ahead so the L2 latency of the step's key block overlaps the arithmetic.
 template <int DG>
-struct Prefetch { static constexpr int value = DG <= 3 ? 1 : 0; };
+#ifndef MKACC_PF3
+#define MKACC_PF3 1
+#endif
+struct Prefetch { static constexpr int value = DG <= 3 ? MKACC_PF3 : 0; };
 // accumulator loads: each gate's own rows, written by the previous step launch
 __device__ __forceinline__ u32x4 aload4(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
     return __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
@@ -287,7 +290,11 @@ struct DigitMac {
     using Bd = Bounds<DG, METHOD, FIRST>;
     static_assert(DS == 0 || (METHOD == XZW && !FIRST), "d_i scratch: XZW steps after the first");
     static constexpr bool kAcc = START && Bd::kAccInSum;
-    static constexpr bool kMonoPf = METHOD == XZW && !FIRST && DS != 2;
+    // MKACC_MONO_PF=0 (A/B): gather X^(N-c) - 1 at use instead of with the key group
+#ifndef MKACC_MONO_PF
+#define MKACC_MONO_PF 1
+#endif
+    static constexpr bool kMonoPf = MKACC_MONO_PF && METHOD == XZW && !FIRST && DS != 2;
     // a d_i reload comes from HBM and frees the k2 / psi registers: prefetched
     // 3 groups ahead at DG <= 3, 2 at DG >= 4 (3 spill 10 VGPRs there); 1 group measured
     // 1-4% slower (profiles/r2/ab_dscr.txt)
