@@ -14,6 +14,9 @@
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
+#ifdef __AVX512F__
+#include <immintrin.h>
+#endif
 #ifdef _OPENMP
 #include <omp.h>
 #endif
@@ -204,6 +207,14 @@ void orc_vec_mod(int op, const uint64_t* a, const uint64_t* b, uint64_t* out, si
 /* NTT (transformnat-impl.h)                                                */
 /* ------------------------------------------------------------------------ */
 
+/* the 32-bit word transforms and digit decomposition (defined with the accumulator below) */
+static void ntt_fwd32(uint32_t* restrict a, uint32_t N, uint32_t Q, const uint32_t* restrict w,
+                      const uint32_t* restrict wp);
+static void ntt_inv32(uint32_t* restrict a, uint32_t N, uint32_t Q, const uint32_t* restrict w,
+                      const uint32_t* restrict wp, uint32_t ninv, uint32_t ninvp);
+static void sdd32(const uint32_t* restrict in, uint32_t* restrict out, uint32_t N, uint32_t Q, uint32_t gBits,
+                  uint32_t dg);
+
 static uint32_t brv(uint32_t x, uint32_t bits) {
     uint32_t r = 0;
     for (uint32_t i = 0; i < bits; ++i) r |= ((x >> i) & 1u) << (bits - 1 - i);
@@ -327,17 +338,41 @@ static void ntt_inv_tab(uint64_t* a, uint32_t N, uint64_t Q, const uint64_t* tab
     }
 }
 
+/* Q < 2^30: through the 32-bit word transforms the accumulator uses, so the
+ * reference's known-answer vectors pin that code (tests/test_oracle_kat.py) */
+static void ntt32_entry(uint64_t* a, uint32_t N, uint64_t Q, const uint64_t* tab, uint64_t Ninv, int inverse) {
+    uint32_t* w = (uint32_t*)malloc(sizeof(uint32_t) * N * 3);
+    uint32_t *wp = w + N, *x = w + 2 * N;
+    for (uint32_t i = 0; i < N; ++i) {
+        w[i] = (uint32_t)tab[i];
+        wp[i] = (uint32_t)tab[2 * N + i];
+        x[i] = (uint32_t)a[i];
+    }
+    if (inverse)
+        ntt_inv32(x, N, (uint32_t)Q, w, wp, (uint32_t)Ninv, (uint32_t)((Ninv << 32) / Q));
+    else
+        ntt_fwd32(x, N, (uint32_t)Q, w, wp);
+    for (uint32_t i = 0; i < N; ++i) a[i] = x[i];
+    free(w);
+}
+
 void orc_ntt_forward(uint64_t* a, uint32_t N, uint64_t Q, uint64_t psi) {
     uint64_t* tab = (uint64_t*)malloc(sizeof(uint64_t) * N * 6);
     make_tables(tab, tab + 3 * N, N, Q, psi);
-    ntt_fwd_tab(a, N, Q, tab);
+    if (Q < (1ull << 30))
+        ntt32_entry(a, N, Q, tab, 0, 0);
+    else
+        ntt_fwd_tab(a, N, Q, tab);
     free(tab);
 }
 
 void orc_ntt_inverse(uint64_t* a, uint32_t N, uint64_t Q, uint64_t psi) {
     uint64_t* tab = (uint64_t*)malloc(sizeof(uint64_t) * N * 6);
     make_tables(tab, tab + 3 * N, N, Q, psi);
-    ntt_inv_tab(a, N, Q, tab + 3 * N, orc_modinv(N, Q));
+    if (Q < (1ull << 30))
+        ntt32_entry(a, N, Q, tab + 3 * N, orc_modinv(N, Q), 1);
+    else
+        ntt_inv_tab(a, N, Q, tab + 3 * N, orc_modinv(N, Q));
     free(tab);
 }
 
@@ -375,6 +410,15 @@ static inline int64_t sext_low(int64_t d, uint32_t gBits) {
 void orc_sdd(const uint64_t* in, uint64_t* out, uint32_t N, uint64_t Q, uint32_t baseG, uint32_t dg) {
     uint64_t QHalf = Q >> 1;
     uint32_t gBits = (uint32_t)__builtin_ctz(baseG);
+    if (Q < (1ull << 30) && gBits * (dg + 1) <= 30) {
+        /* through the 32-bit word decomposition the accumulator uses */
+        uint32_t* x = (uint32_t*)calloc((size_t)N * (dg + 1), sizeof(uint32_t));
+        for (uint32_t k = 0; k < N; ++k) x[k] = (uint32_t)in[k];
+        sdd32(x, x + N, N, (uint32_t)Q, gBits, dg);
+        for (size_t k = 0; k < (size_t)N * dg; ++k) out[k] = x[N + k];
+        free(x);
+        return;
+    }
     for (uint32_t k = 0; k < N; ++k) {
         uint64_t t0 = in[k];
         int64_t d0 = t0 < QHalf ? (int64_t)t0 : (int64_t)t0 - (int64_t)Q;
@@ -393,6 +437,230 @@ void orc_sdd(const uint64_t* in, uint64_t* out, uint32_t N, uint64_t Q, uint32_t
 /* accumulator context                                                       */
 /* ------------------------------------------------------------------------ */
 
+/* ------------------------------------------------------------------------ */
+/* 32-bit word path (Q < 2^27: every MK parameter set)                       */
+/* ------------------------------------------------------------------------ */
+/* The reference's README build is NATIVE_SIZE=32: NativeInteger is a 32-bit
+ * word (basicint.h:56-59) and its NTT uses Shoup companions floor(w 2^32 / Q)
+ * (ubintnat.h:1488-1494).  The accumulator runs on u32 words here too, with
+ * lazy (Harvey) butterflies -- values stay below 4Q < 2^32 and are made
+ * canonical once per transform -- and lazy 64-bit sums for the pointwise
+ * multiply-adds, reduced once per slot.  Every reduction is exact, so the
+ * canonical outputs equal the reference's per-operation reductions
+ * (ubintnat.h:1304-1310 ModMulFastEq, mubintvecnat.cpp:246-296 ModAdd/ModSub). */
+typedef struct m32 {
+    uint32_t Q, mu, sh;   /* Barrett: q = ((x >> sh) * mu) >> 32, sh = L - 1, mu = floor(2^(L+31) / Q) */
+} m32;
+
+static m32 make_m32(uint32_t Q) {
+    m32 m;
+    uint32_t L = 32 - (uint32_t)__builtin_clz(Q);
+    m.Q = Q;
+    m.sh = L - 1;
+    m.mu = (uint32_t)((1ull << (L + 31)) / Q);
+    return m;
+}
+/* x < 2^(L+31) (a sum of up to 16 products of residues when L <= 27) -> [0, Q):
+ * the quotient estimate is at most 2 below floor(x / Q) */
+static inline uint32_t bred(uint64_t x, uint32_t Q, uint32_t mu, uint32_t sh) {
+    /* x >> sh < 2^32: a 32 x 32 -> 64-bit product (vpmuludq when vectorized) */
+    const uint32_t q = (uint32_t)(((uint64_t)(uint32_t)(x >> sh) * mu) >> 32);
+    uint32_t r = (uint32_t)x - q * Q; /* < 3Q */
+    r = r >= Q ? r - Q : r;
+    return r >= Q ? r - Q : r;
+}
+/* lazy Shoup product y * w in [0, 2Q) for any 32-bit y (wp = floor(w 2^32 / Q)) */
+static inline uint32_t shoup_lazy32(uint32_t y, uint32_t w, uint32_t wp, uint32_t Q) {
+    const uint32_t q = (uint32_t)(((uint64_t)y * wp) >> 32);
+    return y * w - q * Q;
+}
+static inline uint32_t min32(uint32_t a, uint32_t b) { return a < b ? a : b; }
+
+#ifdef __AVX512F__
+/* 16 lanes of the lazy Shoup product (W, WP broadcast or per lane): the high
+ * words of y * wp from the even and odd 64-bit products, low words by vpmulld */
+static inline __m512i shoup_lazy_v(__m512i y, __m512i W, __m512i WP, __m512i Qv) {
+    const __m512i pe = _mm512_mul_epu32(y, WP);
+    const __m512i po = _mm512_mul_epu32(_mm512_srli_epi64(y, 32), _mm512_srli_epi64(WP, 32));
+    const __m512i q = _mm512_mask_blend_epi32(0xAAAA, _mm512_srli_epi64(pe, 32), po);
+    return _mm512_sub_epi32(_mm512_mullo_epi32(y, W), _mm512_mullo_epi32(q, Qv));
+}
+/* strides t < 16: 32 consecutive words hold 16/t butterfly groups; gather
+ * their x and y halves into two registers (idx_x, idx_y), the twiddle of lane
+ * L is entry L / t of the stage's run (idx_w), and idx_o scatters back */
+typedef struct short_perm { __m512i ix, iy, iw, io0, io1; } short_perm;
+static short_perm make_short_perm(uint32_t t) {
+    uint32_t ix[16], iy[16], iw[16], io[32];
+    for (uint32_t L = 0; L < 16; ++L) {
+        const uint32_t g = L / t, o = L % t;
+        ix[L] = g * 2 * t + o;
+        iy[L] = g * 2 * t + t + o;
+        iw[L] = g;
+    }
+    for (uint32_t P = 0; P < 32; ++P) {
+        const uint32_t g = P / (2 * t), r = P % (2 * t);
+        io[P] = r < t ? g * t + r : 16 + g * t + r - t;
+    }
+    short_perm s;
+    s.ix = _mm512_loadu_si512(ix);
+    s.iy = _mm512_loadu_si512(iy);
+    s.iw = _mm512_loadu_si512(iw);
+    s.io0 = _mm512_loadu_si512(io);
+    s.io1 = _mm512_loadu_si512(io + 16);
+    return s;
+}
+#endif
+
+/* ForwardTransformToBitReverseInPlace (transformnat-impl.h:300-354) on u32
+ * words: the same CT loop and tables, lazy: U in [0, 2Q), V = Shoup in [0, 2Q),
+ * outputs in [0, 4Q); canonical at the end.  Input canonical (or < 4Q). */
+static void ntt_fwd32(uint32_t* restrict a, uint32_t N, uint32_t Q, const uint32_t* restrict w,
+                      const uint32_t* restrict wp) {
+    const uint32_t Q2 = 2 * Q;
+    uint32_t t = N;
+    for (uint32_t m = 1; m < N; m <<= 1) {
+        t >>= 1;
+#ifdef __AVX512F__
+        const __m512i Qv = _mm512_set1_epi32((int)Q), Q2v = _mm512_set1_epi32((int)Q2);
+        if (t >= 16) {
+            for (uint32_t i = 0; i < m; ++i) {
+                const __m512i W = _mm512_set1_epi32((int)w[m + i]), WP = _mm512_set1_epi32((int)wp[m + i]);
+                uint32_t* x = a + 2 * i * t;
+                uint32_t* y = x + t;
+                for (uint32_t j = 0; j < t; j += 16) {
+                    __m512i U = _mm512_loadu_si512(x + j);
+                    U = _mm512_min_epu32(U, _mm512_sub_epi32(U, Q2v));
+                    const __m512i V = shoup_lazy_v(_mm512_loadu_si512(y + j), W, WP, Qv);
+                    _mm512_storeu_si512(x + j, _mm512_add_epi32(U, V));
+                    _mm512_storeu_si512(y + j, _mm512_add_epi32(_mm512_sub_epi32(U, V), Q2v));
+                }
+            }
+            continue;
+        }
+        if (N >= 32) {
+            const short_perm sp = make_short_perm(t);
+            const uint32_t gpb = 16 / t; /* groups per 32 words */
+            for (uint32_t b = 0; b < N; b += 32) {
+                const __m512i A = _mm512_loadu_si512(a + b), Bv = _mm512_loadu_si512(a + b + 16);
+                const uint32_t g0 = m + b / (2 * t);
+                (void)gpb;
+                const __m512i W = _mm512_permutexvar_epi32(sp.iw, _mm512_loadu_si512(w + g0));
+                const __m512i WP = _mm512_permutexvar_epi32(sp.iw, _mm512_loadu_si512(wp + g0));
+                __m512i U = _mm512_permutex2var_epi32(A, sp.ix, Bv);
+                U = _mm512_min_epu32(U, _mm512_sub_epi32(U, Q2v));
+                const __m512i V = shoup_lazy_v(_mm512_permutex2var_epi32(A, sp.iy, Bv), W, WP, Qv);
+                const __m512i X = _mm512_add_epi32(U, V), Y = _mm512_add_epi32(_mm512_sub_epi32(U, V), Q2v);
+                _mm512_storeu_si512(a + b, _mm512_permutex2var_epi32(X, sp.io0, Y));
+                _mm512_storeu_si512(a + b + 16, _mm512_permutex2var_epi32(X, sp.io1, Y));
+            }
+            continue;
+        }
+#endif
+        for (uint32_t i = 0; i < m; ++i) {
+            const uint32_t W = w[m + i], WP = wp[m + i];
+            uint32_t* restrict x = a + 2 * i * t;
+            uint32_t* restrict y = x + t;
+            for (uint32_t j = 0; j < t; ++j) {
+                const uint32_t U = min32(x[j], x[j] - Q2);
+                const uint32_t V = shoup_lazy32(y[j], W, WP, Q);
+                x[j] = U + V;
+                y[j] = U - V + Q2;
+            }
+        }
+    }
+    for (uint32_t j = 0; j < N; ++j) {
+        uint32_t x = min32(a[j], a[j] - Q2);
+        a[j] = min32(x, x - Q);
+    }
+}
+
+/* InverseTransformFromBitReverseInPlace (transformnat-impl.h:492-552) on u32
+ * words: the GS stages of growing stride with the reference's inverse table,
+ * lazy in [0, 2Q); N^-1 (fused into the stride-1 stage there) applied with
+ * the canonical reduction at the end.  Input canonical (or < 2Q). */
+static void ntt_inv32(uint32_t* restrict a, uint32_t N, uint32_t Q, const uint32_t* restrict w,
+                      const uint32_t* restrict wp, uint32_t ninv, uint32_t ninvp) {
+    const uint32_t Q2 = 2 * Q;
+    for (uint32_t m = N >> 1, t = 1; m >= 1; m >>= 1, t <<= 1) {
+#ifdef __AVX512F__
+        const __m512i Qv = _mm512_set1_epi32((int)Q), Q2v = _mm512_set1_epi32((int)Q2);
+        if (t >= 16) {
+            for (uint32_t i = 0; i < m; ++i) {
+                const __m512i W = _mm512_set1_epi32((int)w[m + i]), WP = _mm512_set1_epi32((int)wp[m + i]);
+                uint32_t* x = a + 2 * i * t;
+                uint32_t* y = x + t;
+                for (uint32_t j = 0; j < t; j += 16) {
+                    const __m512i U = _mm512_loadu_si512(x + j), V = _mm512_loadu_si512(y + j);
+                    const __m512i S = _mm512_add_epi32(U, V);
+                    _mm512_storeu_si512(x + j, _mm512_min_epu32(S, _mm512_sub_epi32(S, Q2v)));
+                    _mm512_storeu_si512(y + j, shoup_lazy_v(_mm512_add_epi32(_mm512_sub_epi32(U, V), Q2v), W, WP, Qv));
+                }
+            }
+            continue;
+        }
+        if (N >= 32) {
+            const short_perm sp = make_short_perm(t);
+            for (uint32_t b = 0; b < N; b += 32) {
+                const __m512i A = _mm512_loadu_si512(a + b), Bv = _mm512_loadu_si512(a + b + 16);
+                const uint32_t g0 = m + b / (2 * t);
+                const __m512i W = _mm512_permutexvar_epi32(sp.iw, _mm512_loadu_si512(w + g0));
+                const __m512i WP = _mm512_permutexvar_epi32(sp.iw, _mm512_loadu_si512(wp + g0));
+                const __m512i U = _mm512_permutex2var_epi32(A, sp.ix, Bv);
+                const __m512i V = _mm512_permutex2var_epi32(A, sp.iy, Bv);
+                const __m512i S = _mm512_add_epi32(U, V);
+                const __m512i X = _mm512_min_epu32(S, _mm512_sub_epi32(S, Q2v));
+                const __m512i Y = shoup_lazy_v(_mm512_add_epi32(_mm512_sub_epi32(U, V), Q2v), W, WP, Qv);
+                _mm512_storeu_si512(a + b, _mm512_permutex2var_epi32(X, sp.io0, Y));
+                _mm512_storeu_si512(a + b + 16, _mm512_permutex2var_epi32(X, sp.io1, Y));
+            }
+            continue;
+        }
+#endif
+        for (uint32_t i = 0; i < m; ++i) {
+            const uint32_t W = w[m + i], WP = wp[m + i];
+            uint32_t* restrict x = a + 2 * i * t;
+            uint32_t* restrict y = x + t;
+            for (uint32_t j = 0; j < t; ++j) {
+                const uint32_t U = x[j], V = y[j];
+                x[j] = min32(U + V, U + V - Q2);
+                y[j] = shoup_lazy32(U - V + Q2, W, WP, Q);
+            }
+        }
+    }
+    for (uint32_t j = 0; j < N; ++j) {
+        const uint32_t x = shoup_lazy32(a[j], ninv, ninvp, Q);
+        a[j] = min32(x, x - Q);
+    }
+}
+
+/* SignedDigitDecompose (mk-acc.cpp:54-80) on u32 words, one pass per digit
+ * over the running value d (kept in out's last row until it is overwritten) */
+static void sdd32(const uint32_t* restrict in, uint32_t* restrict out, uint32_t N, uint32_t Q, uint32_t gBits,
+                  uint32_t dg) {
+    const int32_t QHalf = (int32_t)(Q >> 1), half = 1 << (gBits - 1), mask = (1 << gBits) - 1;
+    int32_t* dv = (int32_t*)(out + (size_t)(dg - 1) * N);
+    for (uint32_t k = 0; k < N; ++k) {
+        const int32_t t0 = (int32_t)in[k];
+        const int32_t d0 = t0 < QHalf ? t0 : t0 - (int32_t)Q;
+        const int32_t r0 = ((d0 + half) & mask) - half; /* sign-extended low gBits bits */
+        dv[k] = (d0 - r0) >> gBits;                     /* lowest digit dropped */
+    }
+    for (uint32_t d = 0; d + 1 < dg; ++d) {
+        uint32_t* restrict o = out + (size_t)d * N;
+        for (uint32_t k = 0; k < N; ++k) {
+            const int32_t x = dv[k];
+            const int32_t r0 = ((x + half) & mask) - half;
+            dv[k] = (x - r0) >> gBits;
+            o[k] = (uint32_t)(r0 < 0 ? r0 + (int32_t)Q : r0);
+        }
+    }
+    for (uint32_t k = 0; k < N; ++k) {   /* the last digit replaces the running value */
+        const int32_t x = dv[k];
+        const int32_t r0 = ((x + half) & mask) - half;
+        dv[k] = r0 < 0 ? r0 + (int32_t)Q : r0;
+    }
+}
+
 struct orc_ctx {
     orc_params p;
     uint32_t dg, nk;
@@ -400,7 +668,13 @@ struct orc_ctx {
     modq m;
     uint64_t* tab;   /* forward table [N] + Shoup companions [2N] (make_tables) */
     uint64_t* tabI;  /* inverse table [N] + Shoup companions [2N] */
-    uint64_t* mono;  /* [2N][N] monomials X^m - 1 in EVAL (mk-cryptoparameters.cpp:51-70) */
+    uint64_t* mono;  /* [2N][N] monomials X^m - 1 in EVAL (mk-cryptoparameters.cpp:51-70); 64-bit path */
+    /* 32-bit word path (Q < 2^27) */
+    int w32;
+    m32 b;
+    uint32_t ninv32, ninvp32;
+    uint32_t *tw32, *twp32, *twi32, *twip32;   /* reference tables and Shoup companions */
+    uint32_t* mono32;                          /* [2N][N] monomials, u32 */
 };
 
 orc_ctx* orc_ctx_create(const orc_params* p) {
@@ -419,6 +693,30 @@ orc_ctx* orc_ctx_create(const orc_params* p) {
     c->tab = (uint64_t*)malloc(sizeof(uint64_t) * N * 3);
     c->tabI = (uint64_t*)malloc(sizeof(uint64_t) * N * 3);
     make_tables(c->tab, c->tabI, N, Q, c->p.psi);
+    c->w32 = Q < (1ull << 27);
+    if (c->w32) {
+        c->b = make_m32((uint32_t)Q);
+        c->ninv32 = (uint32_t)c->Ninv;
+        c->ninvp32 = (uint32_t)((c->Ninv << 32) / Q);
+        uint32_t* t = (uint32_t*)malloc(sizeof(uint32_t) * N * 4);
+        c->tw32 = t; c->twp32 = t + N; c->twi32 = t + 2 * N; c->twip32 = t + 3 * N;
+        for (uint32_t i = 0; i < N; ++i) {
+            c->tw32[i] = (uint32_t)c->tab[i];
+            c->twp32[i] = (uint32_t)c->tab[2 * N + i];
+            c->twi32[i] = (uint32_t)c->tabI[i];
+            c->twip32[i] = (uint32_t)c->tabI[2 * N + i];
+        }
+        /* monomials X^i - 1 and -X^i - 1 (= X^(N+i) - 1), mk-cryptoparameters.cpp:51-70 */
+        c->mono32 = (uint32_t*)calloc((size_t)2 * N * N, sizeof(uint32_t));
+        for (uint32_t i = 0; i < 2 * N; ++i) {
+            uint32_t* a = c->mono32 + (size_t)i * N;
+            const uint32_t e = i % N;
+            a[0] = (uint32_t)Q - 1;
+            a[e] = i < N ? (uint32_t)addmod(a[e], 1, Q) : (uint32_t)submod(a[e], 1, Q);
+            ntt_fwd32(a, N, (uint32_t)Q, c->tw32, c->twp32);
+        }
+        return c;
+    }
     c->mono = (uint64_t*)calloc((size_t)2 * N * N, sizeof(uint64_t));
     for (uint32_t i = 0; i < N; ++i) {               /* X^i - 1 */
         uint64_t* a = c->mono + (size_t)i * N;
@@ -437,7 +735,7 @@ orc_ctx* orc_ctx_create(const orc_params* p) {
 
 void orc_ctx_destroy(orc_ctx* c) {
     if (!c) return;
-    free(c->tab); free(c->tabI); free(c->mono); free(c);
+    free(c->tab); free(c->tabI); free(c->mono); free(c->tw32); free(c->mono32); free(c);
 }
 
 size_t orc_evk_words(const orc_params* p) {
@@ -493,6 +791,140 @@ static void hbprod(const orc_ctx* c, const uint64_t* d, const uint64_t* f, uint3
             w = addmod(w, mm(&c->m, dct[(size_t)i * N + s], f[(size_t)i * N + s]), Q);
         out[s] = addmod(out[s], w, Q);
     }
+}
+
+/* HbProd (mk-acc-xzw.cpp:231-290) on u32 words: the same loop nest as hbprod();
+ * the per-slot sums over the digits are lazy 64-bit (at most 2 dg products of
+ * residues below Q < 2^27) and reduced once. */
+static void hbprod32(const orc_ctx* c, const uint32_t* restrict d, const uint32_t* restrict f, uint32_t index,
+                     const uint32_t* restrict pkey, uint32_t* restrict acc, uint32_t* restrict scratch) {
+    const uint32_t N = c->p.N, k = c->p.k, dg = c->dg, Q = (uint32_t)c->p.Q;
+    const uint32_t mu = c->b.mu, sh = c->b.sh, gBits = (uint32_t)__builtin_ctz(c->p.baseG);
+    uint32_t* ct = scratch;                    /* N */
+    uint32_t* dct = ct + N;                    /* dg*N */
+    uint32_t* sumV = dct + (size_t)dg * N;     /* N */
+    uint64_t* sU = (uint64_t*)(sumV + N);      /* N lazy sums (u64) */
+    uint64_t* sVv = sU + N;                    /* N */
+    memset(sumV, 0, sizeof(uint32_t) * N);
+    for (uint32_t u = 0; u < k; ++u) {
+        memcpy(ct, acc + (size_t)u * N, sizeof(uint32_t) * N);
+        ntt_inv32(ct, N, Q, c->twi32, c->twip32, c->ninv32, c->ninvp32);
+        sdd32(ct, dct, N, Q, gBits, dg);
+        for (uint32_t i = 0; i < dg; ++i) ntt_fwd32(dct + (size_t)i * N, N, Q, c->tw32, c->twp32);
+        uint32_t* out = acc + (size_t)u * N;
+        const uint32_t* Pu = pkey + (size_t)u * dg * N;
+        for (uint32_t s = 0; s < N; ++s) {
+            sU[s] = 0;
+            sVv[s] = 0;
+        }
+        for (uint32_t i = 0; i < dg; ++i) {
+            const uint32_t* restrict g = dct + (size_t)i * N;
+            const uint32_t* restrict di = d + (size_t)i * N;
+            const uint32_t* restrict pi = Pu + (size_t)i * N;
+            for (uint32_t s = 0; s < N; ++s) {
+                sU[s] += (uint64_t)g[s] * di[s];
+                sVv[s] += (uint64_t)g[s] * pi[s];
+            }
+        }
+        for (uint32_t s = 0; s < N; ++s) {
+            const uint32_t sv = sumV[s] + bred(sVv[s], Q, mu, sh);
+            sumV[s] = min32(sv, sv - Q);
+            out[s] = bred(sU[s], Q, mu, sh);
+        }
+    }
+    ntt_inv32(sumV, N, Q, c->twi32, c->twip32, c->ninv32, c->ninvp32);
+    sdd32(sumV, dct, N, Q, gBits, dg);
+    for (uint32_t i = 0; i < dg; ++i) ntt_fwd32(dct + (size_t)i * N, N, Q, c->tw32, c->twp32);
+    uint32_t* out = acc + (size_t)index * N;
+    for (uint32_t s = 0; s < N; ++s) sU[s] = out[s];
+    for (uint32_t i = 0; i < dg; ++i) {
+        const uint32_t* restrict g = dct + (size_t)i * N;
+        const uint32_t* restrict fi = f + (size_t)i * N;
+        for (uint32_t s = 0; s < N; ++s) sU[s] += (uint64_t)g[s] * fi[s];
+    }
+    for (uint32_t s = 0; s < N; ++s) out[s] = bred(sU[s], Q, mu, sh);
+}
+
+/* EvalAcc (mk-acc-xzw.cpp:89-130 / mk-acc-xzw_B.cpp:103-132) on u32 words: the
+ * loop of evalacc_one() with the same key combinations (xzw.cpp:322-325,
+ * 375-378; xzw_B.cpp:311-314, 368-371), reduced once per slot. */
+static int evalacc_one32(const orc_ctx* c, const uint64_t* evk, const uint32_t* pkey, const uint64_t* ct,
+                         uint64_t* acc64, uint32_t* work) {
+    const uint32_t N = c->p.N, k = c->p.k, n = c->p.n, dg = c->dg, Q = (uint32_t)c->p.Q;
+    const uint32_t mu = c->b.mu, sh = c->b.sh;
+    const uint64_t M = 2ull * N;
+    uint32_t* acc = work;                         /* k*N */
+    uint32_t* d = acc + (size_t)k * N;            /* dg*N */
+    uint32_t* f = d + (size_t)dg * N;             /* dg*N */
+    uint32_t* acctemp = f + (size_t)dg * N;       /* k*N */
+    uint32_t* scratch = acctemp + (size_t)k * N;  /* (dg+2)*N u32 + 2N u64 */
+    for (size_t s = 0; s < (size_t)k * N; ++s) {
+        if (acc64[s] >= Q) return 2;
+        acc[s] = (uint32_t)acc64[s];
+    }
+    for (uint32_t u = 0; u < k; ++u) {
+        for (uint32_t i = 0; i < n; ++i) {
+            uint64_t raw = ct[(size_t)u * n + i];
+            uint64_t cval;
+            if (c->p.method == ORC_XZW) {
+                if (raw >= c->p.q) return 2;
+                cval = raw * 2 * N / c->p.q;          /* mk-acc-xzw.cpp:110,125: floor(ct*2N/q) */
+            } else {
+                if (raw > M) return 2;
+                cval = raw;                           /* mk-acc-xzw_B.cpp:119,124 */
+            }
+            uint32_t ipos = (uint32_t)(cval == M ? 0 : cval);
+            uint32_t ineg = (uint32_t)(cval == 0 ? 0 : M - cval); /* ModSubFast(0 - c) mod 2N */
+            if (ineg == M) ineg = 0;
+            const uint32_t* restrict mono = c->mono32 + (size_t)ipos * N;
+            const uint32_t* restrict monoN = c->mono32 + (size_t)ineg * N;
+            const int first = (u == 0 && i == 0);
+            for (uint32_t dgt = 0; dgt < dg; ++dgt) {
+                for (uint32_t part = 0; part < 2; ++part) {
+                    uint32_t* restrict out = (part == 0 ? d : f) + (size_t)dgt * N;
+                    const uint64_t* restrict e1 = keyp(c, evk, u, 0, i, dgt, part);
+                    if (c->p.method == ORC_XZW) {
+                        const uint64_t* restrict e2 = keyp(c, evk, u, 1, i, dgt, part);
+                        if (first) {
+                            /* AddToAccXZW0 xzw.cpp:375-378: evs + ev1*(X^c-1) + ev2*(X^-c-1) */
+                            const uint64_t* restrict es = keyp(c, evk, u, 0, n, dgt, part);
+                            for (uint32_t s = 0; s < N; ++s)
+                                out[s] = bred(es[s] + (uint64_t)(uint32_t)e1[s] * mono[s] + (uint64_t)(uint32_t)e2[s] * monoN[s], Q, mu, sh);
+                        } else {
+                            /* AddToAccXZW xzw.cpp:322-325: ev1 - ev2*(X^-c-1) - ev2
+                             * = ev1 + ev2 * (Q - (X^-c - 1) - 1), a sum below 2 Q^2 */
+                            for (uint32_t s = 0; s < N; ++s)
+                                out[s] = bred(e1[s] + (uint64_t)(uint32_t)e2[s] * (Q - 1 - monoN[s]), Q, mu, sh);
+                        }
+                    } else {
+                        if (first) {
+                            /* AddToAccXZW0 xzw_B.cpp:368-371: evs + ev1*(X^c-1) */
+                            const uint64_t* restrict es = keyp(c, evk, u, 0, n, dgt, part);
+                            for (uint32_t s = 0; s < N; ++s) out[s] = bred(es[s] + (uint64_t)(uint32_t)e1[s] * mono[s], Q, mu, sh);
+                        } else {
+                            /* AddToAccXZW xzw_B.cpp:311-314: d = ev1 */
+                            for (uint32_t s = 0; s < N; ++s) out[s] = (uint32_t)e1[s];
+                        }
+                    }
+                }
+            }
+            if (first) {
+                hbprod32(c, d, f, u, pkey, acc, scratch); /* acc is REPLACED (xzw.cpp:380) */
+            } else {
+                /* acctemp = acc * (X^c - 1); HbProd(acctemp); acc += acctemp (xzw.cpp:327-344) */
+                for (uint32_t w = 0; w < k; ++w)
+                    for (uint32_t s = 0; s < N; ++s)
+                        acctemp[(size_t)w * N + s] = bred((uint64_t)acc[(size_t)w * N + s] * mono[s], Q, mu, sh);
+                hbprod32(c, d, f, u, pkey, acctemp, scratch);
+                for (size_t s = 0; s < (size_t)k * N; ++s) {
+                    const uint32_t x = acc[s] + acctemp[s];
+                    acc[s] = x >= Q ? x - Q : x;
+                }
+            }
+        }
+    }
+    for (size_t s = 0; s < (size_t)k * N; ++s) acc64[s] = acc[s];
+    return 0;
 }
 
 static int evalacc_one(const orc_ctx* c, const uint64_t* evk, const uint64_t* pkey, const uint64_t* ct,
@@ -566,14 +998,39 @@ static int evalacc_one(const orc_ctx* c, const uint64_t* evk, const uint64_t* pk
 }
 
 static size_t work_words(const orc_ctx* c) {
-    return (size_t)c->p.N * (2 * c->dg + c->p.k + c->dg + 2);
+    /* 64-bit path in u64 words; the 32-bit path (u32 words) also holds the
+     * accumulator and two u64 rows of lazy sums */
+    return (size_t)c->p.N * (2 * c->dg + c->p.k + c->dg + 2) + (size_t)c->p.k * c->p.N + 2 * (size_t)c->p.N;
+}
+
+/* one gate through the word path of the context; pk32 = pkey narrowed (32-bit path) */
+static int evalacc_dispatch(const orc_ctx* c, const uint64_t* evk, const uint64_t* pkey, const uint32_t* pk32,
+                            const uint64_t* ct, uint64_t* acc, uint64_t* work) {
+    if (c->w32) return evalacc_one32(c, evk, pk32, ct, acc, (uint32_t*)work);
+    return evalacc_one(c, evk, pkey, ct, acc, work);
+}
+
+/* pkey as u32 words for the 32-bit path (NULL on the 64-bit path, or on a non-canonical word) */
+static uint32_t* narrow_pkey(const orc_ctx* c, const uint64_t* pkey, int* bad) {
+    *bad = 0;
+    if (!c->w32) return NULL;
+    const size_t w = (size_t)c->p.k * c->dg * c->p.N;
+    uint32_t* p = (uint32_t*)malloc(sizeof(uint32_t) * w);
+    for (size_t i = 0; i < w; ++i) {
+        if (pkey[i] >= c->p.Q) *bad = 1;
+        p[i] = (uint32_t)pkey[i];
+    }
+    return p;
 }
 
 int orc_evalacc(const orc_ctx* c, const uint64_t* evk, const uint64_t* pkey, const uint64_t* ct, uint64_t* acc) {
     if (!c) return 1;
+    int bad;
+    uint32_t* pk32 = narrow_pkey(c, pkey, &bad);
     uint64_t* work = (uint64_t*)malloc(sizeof(uint64_t) * work_words(c));
-    int rc = evalacc_one(c, evk, pkey, ct, acc, work);
+    int rc = bad ? 2 : evalacc_dispatch(c, evk, pkey, pk32, ct, acc, work);
     free(work);
+    free(pk32);
     return rc;
 }
 
@@ -582,21 +1039,29 @@ int orc_evalacc_batch(const orc_ctx* c, const uint64_t* evk, const uint64_t* pke
     if (!c) return 1;
     int rc = 0;
     const size_t ctw = (size_t)c->p.k * c->p.n, accw = (size_t)c->p.k * c->p.N;
+    int bad;
+    uint32_t* pk32 = narrow_pkey(c, pkey, &bad);
+    if (bad) {
+        free(pk32);
+        return 2;
+    }
 #ifdef _OPENMP
     if (threads < 1) threads = 1;
 #pragma omp parallel num_threads(threads) reduction(| : rc)
     {
         uint64_t* work = (uint64_t*)malloc(sizeof(uint64_t) * work_words(c));
 #pragma omp for schedule(dynamic, 1)
-        for (long g = 0; g < (long)B; ++g) rc |= evalacc_one(c, evk, pkey, ct + g * ctw, acc + g * accw, work);
+        for (long g = 0; g < (long)B; ++g)
+            rc |= evalacc_dispatch(c, evk, pkey, pk32, ct + g * ctw, acc + g * accw, work);
         free(work);
     }
 #else
     (void)threads;
     uint64_t* work = (uint64_t*)malloc(sizeof(uint64_t) * work_words(c));
-    for (size_t g = 0; g < B; ++g) rc |= evalacc_one(c, evk, pkey, ct + g * ctw, acc + g * accw, work);
+    for (size_t g = 0; g < B; ++g) rc |= evalacc_dispatch(c, evk, pkey, pk32, ct + g * ctw, acc + g * accw, work);
     free(work);
 #endif
+    free(pk32);
     return rc;
 }
 
