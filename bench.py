@@ -13,9 +13,9 @@ KeySwitch); --stage evalacc runs the accumulator alone.
 Multi-GPU: one process per GPU.  Under torch.distributed.run the ranks come
 from the environment; `--gpus N` without WORLD_SIZE launches the N ranks
 itself (a child torch.distributed.run, before anything touches a GPU).  Rank 0
-draws the bootstrapping keys and broadcasts them once over RCCL; every rank
-uploads them straight from the received device buffer
-(mkacc_upload_keys_device).  Gates are sharded by rank with no collective on
+draws the bootstrapping and key-switching keys and broadcasts them once over
+RCCL; every rank uploads them straight from the received device buffer
+(mkacc_upload_keys_device, mkacc_upload_ksk_*_device).  Gates are sharded by rank with no collective on
 the data path ("weak" scaling: B gates per GPU).
 
 Proof of the timed run: after timing, every rank copies back the outputs of
@@ -238,20 +238,23 @@ def run_rank(args, env: dict, make_engine, make_checker, torch_device: str, back
     dks = int(np.ceil(np.log(qKS) / np.log(baseKS)))
 
     # ---- keys: drawn on rank 0, broadcast once (RCCL over xGMI), uploaded from the device buffer ----
+    # dist.broadcast on NCCL only orders torch's current stream; the engine converts the
+    # keys on its own stream, so the host waits for the received buffer first
     evk_n, pkey_n = int(np.prod(eng.evk_shape)), int(np.prod(eng.pkey_shape))
     keys = shard.broadcast_keys(evk_n + pkey_n, p.Q, seed=12345, device=torch_device)
+    sync_dev()
     eng.upload_keys_device(keys[:evk_n], keys[evk_n:])
-    ksk = None
+    ksk_d = None
     if stage == "gate":
         if lwe:
             na, nb = p.k * p.N * baseKS * dks * n_out, p.k * p.N * baseKS * dks
-            t = shard.broadcast_keys(na + nb, qKS, seed=23456, device=torch_device).cpu().numpy().view(np.uint32)
-            ksk = (t[:na], t[na:])
-            eng.upload_ksk_mklwe(ksk[0], ksk[1], qKS, baseKS, n_out)
+            ksk_d = shard.broadcast_keys(na + nb, qKS, seed=23456, device=torch_device)
+            sync_dev()
+            eng.upload_ksk_device(qKS, baseKS, n_out, d_A=ksk_d[:na], d_B=ksk_d[na:])
         else:
-            ksk = shard.broadcast_keys(p.k * p.N * dks * n_out, qKS, seed=23456,
-                                       device=torch_device).cpu().numpy().view(np.uint32)
-            eng.upload_ksk_mntru(ksk, qKS, baseKS, n_out)
+            ksk_d = shard.broadcast_keys(p.k * p.N * dks * n_out, qKS, seed=23456, device=torch_device)
+            sync_dev()
+            eng.upload_ksk_device(qKS, baseKS, n_out, d_ksk=ksk_d)
 
     # ---- this rank's shard of synthetic gates, resident in device memory ----
     rng = np.random.Generator(np.random.PCG64(1000 + rank))
@@ -342,7 +345,9 @@ def run_rank(args, env: dict, make_engine, make_checker, torch_device: str, back
     t_c = time.perf_counter()
     if stage == "gate":
         sub = {key: (v[idx] if key != "nand" else v) for key, v in h.items()}
-        ksk64 = (tuple(x.astype(np.uint64) for x in ksk) if lwe else ksk)
+        ksk_h = ksk_d.cpu().numpy().view(np.uint32)   # the checker's host copy, after the timed region
+        del ksk_d
+        ksk64 = ((ksk_h[:na].astype(np.uint64), ksk_h[na:].astype(np.uint64)) if lwe else ksk_h)
         exp_a, exp_b = chk.gates((evk_h, pkey_h), ksk64, sub, threads, (qKS, baseKS, n_out))
         dt_c = time.perf_counter() - t_c
         got_a = d_oa[idx_d].cpu().numpy().view(np.uint32).astype(np.uint64)

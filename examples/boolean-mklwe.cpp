@@ -51,5 +51,14 @@ int main(int argc, char** argv) {
                       << std::endl;
             bad += result != !(m0 & m1);
         }
-    return bad ? 1 : 0;
+    if (bad) {
+        // seed material of every key and ciphertext above (seed-0 entropy journal):
+        // MKFHE_ENTROPY=<master> replays this run; tools/replay_entropy.py recomputes
+        // its gates on the CPU oracle
+        uint64_t calls = 0;
+        const std::string master = BinFHEContext::GetEntropy(&calls);
+        std::cout << "replay: MKFHE_ENTROPY=" << master << " (" << calls << " seed-0 calls)" << std::endl;
+        return 1;
+    }
+    return 0;
 }

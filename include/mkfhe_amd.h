@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define MKACC_ABI_VERSION 1
+#define MKACC_ABI_VERSION 2
 
 /* status codes */
 #define MKACC_OK            0
@@ -151,6 +151,13 @@ int mkacc_upload_ksk_mntru(mkacc_ctx* ctx, const mkacc_ks_params* ks, const uint
  * B [k][N][baseKS][dks] (GetElementsA / GetElementsB). */
 int mkacc_upload_ksk_mklwe(mkacc_ctx* ctx, const mkacc_ks_params* ks, const uint32_t* A, const uint32_t* B);
 
+/* Same two uploads from DEVICE memory on the context's device (u32 words in the
+ * layouts above), e.g. the buffer of the one-time key broadcast of a multi-GPU
+ * run: converted on the GPU, no host round trip.  Synchronous; MKACC_E_RANGE
+ * (and no key-switching keys) if a word is not a canonical residue mod qKS. */
+int mkacc_upload_ksk_mntru_device(mkacc_ctx* ctx, const mkacc_ks_params* ks, const void* d_ksk);
+int mkacc_upload_ksk_mklwe_device(mkacc_ctx* ctx, const mkacc_ks_params* ks, const void* d_A, const void* d_B);
+
 /* B NAND gates, MK-NTRU.  ct_nand [k][n] (ctGateGen), ct1/ct2 [B][k][n] mod q
  * -> out [B][k][n_out] mod qKS.  Host buffers, synchronous. */
 int mkacc_eval_nand_mntru(mkacc_ctx* ctx, const uint32_t* ct_nand, const uint32_t* ct1, const uint32_t* ct2,
@@ -181,9 +188,43 @@ int mkacc_ntt_forward_u64(mkacc_ctx* ctx, const uint64_t* in, uint64_t* out, siz
 int mkacc_ntt_inverse_u64(mkacc_ctx* ctx, const uint64_t* in, uint64_t* out, size_t count);
 int mkacc_sdd_u64(mkacc_ctx* ctx, const uint64_t* in, uint64_t* out, size_t count);
 
+/* ---- multi-device groups ----------------------------------------------------
+ * A batch of independent gates shards across the GPUs of one node
+ * (BinFHEContext::EvalBinGate over a batch, binfhecontext.cpp:415-426, has no
+ * multi-device form in the reference): a group holds one context per entry of
+ * devices[] (a device may repeat).  Keys are converted once on member 0 and
+ * copied device to device (hipMemcpyPeer, xGMI) to the others; a batch is split
+ * into contiguous shards (mkacc_shard_range), each member runs its shard on
+ * its own stream from its own host thread, and the calls return when every
+ * shard is done.  Outputs are bit-identical to one context's. */
+typedef struct mkacc_group mkacc_group;
+int mkacc_group_create(const mkacc_params* p, const int* devices, uint32_t count, mkacc_group** out);
+void mkacc_group_destroy(mkacc_group* g);
+uint32_t mkacc_group_size(const mkacc_group* g);
+/* member i (owned by the group), e.g. for mkacc_stream / mkacc_get_params */
+mkacc_ctx* mkacc_group_member(mkacc_group* g, uint32_t i);
+/* [*begin, *end) of shard i of B gates over `parts` members; sizes differ by at most one */
+void mkacc_shard_range(size_t B, uint32_t parts, uint32_t i, size_t* begin, size_t* end);
+int mkacc_group_upload_keys(mkacc_group* g, const uint32_t* evk, const uint32_t* pkey);
+int mkacc_group_upload_keys_u64(mkacc_group* g, const uint64_t* evk, const uint64_t* pkey);
+int mkacc_group_upload_ksk_mntru(mkacc_group* g, const mkacc_ks_params* ks, const uint32_t* ksk);
+int mkacc_group_upload_ksk_mklwe(mkacc_group* g, const mkacc_ks_params* ks, const uint32_t* A, const uint32_t* B);
+/* host-buffer forms of mkacc_eval_batch / _u64 / mkacc_eval_nand_mntru / _mklwe over the group */
+int mkacc_group_eval_batch(mkacc_group* g, const uint32_t* ct, const uint32_t* acc_in, uint32_t* acc_out, size_t B);
+int mkacc_group_eval_batch_u64(mkacc_group* g, const uint32_t* ct, const uint64_t* acc_in, uint64_t* acc_out,
+                               size_t B);
+int mkacc_group_eval_nand_mntru(mkacc_group* g, const uint32_t* ct_nand, const uint32_t* ct1, const uint32_t* ct2,
+                                uint32_t* out, size_t B);
+int mkacc_group_eval_nand_mklwe(mkacc_group* g, const uint32_t* a1, const uint32_t* b1, const uint32_t* a2,
+                                const uint32_t* b2, uint32_t* out_a, uint32_t* out_b, size_t B);
+
 /* Per-thread text of the last error ("" if none). */
 const char* mkacc_last_error(void);
 int mkacc_abi_version(void);
+/* "abi=..;header=<id>;source=<id>;dg=<digit counts built>;flags=<A/B switches>":
+ * SHA-256 prefixes of this header and of the engine sources the library was
+ * built from (mkfhe_amd/build.py); loaders refuse a mismatch. */
+const char* mkacc_build_info(void);
 
 #ifdef __cplusplus
 }

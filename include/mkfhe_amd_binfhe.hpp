@@ -25,6 +25,7 @@
 #define MKFHE_AMD_BINFHE_HPP
 
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -216,6 +217,25 @@ private:
     mkacc_params m_p{};
 };
 
+// A multi-device group (mkacc_group_*): one context per device, keys converted
+// once and copied device to device, batches sharded across the members.
+class GroupContext {
+public:
+    GroupContext(const mkacc_params& p, const std::vector<int>& devices) {
+        check(mkacc_group_create(&p, devices.data(), (uint32_t)devices.size(), &m_g));
+        check(mkacc_get_params(mkacc_group_member(m_g, 0), &m_p));
+    }
+    ~GroupContext() { mkacc_group_destroy(m_g); }
+    GroupContext(const GroupContext&) = delete;
+    GroupContext& operator=(const GroupContext&) = delete;
+    mkacc_group* get() const { return m_g; }
+    const mkacc_params& params() const { return m_p; }
+
+private:
+    mkacc_group* m_g = nullptr;
+    mkacc_params m_p{};
+};
+
 // ---- the accumulator plugin seam (mk-acc.h:55-80) -----------------------------------
 class UniEncAccumulator {
 public:
@@ -320,19 +340,30 @@ public:
     // Flatten ek [k][nk][n+1] x [dg][2] x N and Pkey [k][dg] x N into the C-ABI
     // layout and upload them once per key object and Pkey content.
     static void upload(DeviceContext& dc, ConstUniEncACCKey& ek, const std::vector<std::vector<NativePoly>>& Pkey) {
-        const mkacc_params& p = dc.params();
-        const uint32_t dg = p.digitsG - 1, nk = p.method == MKACC_METHOD_MKNTRU ? 2 : 1, N = p.N;
+        std::vector<uint32_t> pk = flatten_pkey(dc.params(), Pkey);
+        if (dc.key_ref == ek && dc.pkey_words == pk) return;   // keys already on the device
+        std::vector<uint32_t> evk = flatten_evk(dc.params(), ek);
+        dc.key_ref.reset();
+        check(mkacc_upload_keys(dc.get(), evk.data(), pk.data()));
+        dc.key_ref = ek;
+        dc.pkey_words = std::move(pk);
+    }
+    static std::vector<uint32_t> flatten_pkey(const mkacc_params& p, const std::vector<std::vector<NativePoly>>& Pkey) {
+        const uint32_t dg = p.digitsG - 1, N = p.N;
         if (Pkey.size() != p.k) throw config_error("Pkey must have k parties");
-        std::vector<uint32_t> pk(mkacc_pkey_words(dc.get()));
+        std::vector<uint32_t> pk((size_t)p.k * dg * N);
         for (uint32_t u = 0; u < p.k; ++u) {
             if (Pkey[u].size() != dg) throw config_error("Pkey must have digitsG-1 polys per party");
             for (uint32_t d = 0; d < dg; ++d)
                 for (uint32_t s = 0; s < N; ++s) pk[((size_t)u * dg + d) * N + s] = (uint32_t)Pkey[u][d][s];
         }
-        if (dc.key_ref == ek && dc.pkey_words == pk) return;   // keys already on the device
+        return pk;
+    }
+    static std::vector<uint32_t> flatten_evk(const mkacc_params& p, ConstUniEncACCKey& ek) {
+        const uint32_t dg = p.digitsG - 1, nk = p.method == MKACC_METHOD_MKNTRU ? 2 : 1, N = p.N;
         const auto& K = ek->GetElements();
         if (K.size() != p.k) throw config_error("accumulator key must have k parties");
-        std::vector<uint32_t> evk(mkacc_evk_words(dc.get()));
+        std::vector<uint32_t> evk((size_t)p.k * nk * (p.n + 1) * dg * 2 * N);
         size_t o = 0;
         for (uint32_t u = 0; u < p.k; ++u) {
             if (K[u].size() < nk) throw config_error("accumulator key has too few key sets");
@@ -347,10 +378,7 @@ public:
                 }
             }
         }
-        dc.key_ref.reset();
-        check(mkacc_upload_keys(dc.get(), evk.data(), pk.data()));
-        dc.key_ref = ek;
-        dc.pkey_words = std::move(pk);
+        return evk;
     }
 
 private:
@@ -567,13 +595,20 @@ struct UniEncBTKey {
 class BinFHEContext {
 public:
     void GenerateBinFHEContext(BINFHE_PARAMSET set, BINFHE_METHOD method, int device = 0) {
+        GenerateBinFHEContext(set, method, std::vector<int>{device});
+    }
+    // Multi-device extension: batches of gates (EvalBinGate over vectors) shard
+    // across `devices` (one GPU each, a device may repeat); keys are converted
+    // once and copied device to device (mkacc_group).  Results are bit-identical.
+    void GenerateBinFHEContext(BINFHE_PARAMSET set, BINFHE_METHOD method, const std::vector<int>& devices) {
         if (method != MKNTRU && method != MKNTRU_B && method != MKNTRU_LWE)
             throw config_error("method is invalid");
+        if (devices.empty()) throw config_error("no device");
         m_method = method;
         m_params = UniEncCryptoParams::FromParamSet(ParamSetName(set), method);
         check(mkkg_paramset(ParamSetName(set), to_abi_method(method), &m_kp));
         m_have_kp = true;
-        reset(device);
+        reset(devices);
     }
     // custom parameters (the reference's explicit-parameter overload, binfhecontext.h:94);
     // key generation then needs SetKeyParams.
@@ -581,7 +616,7 @@ public:
         m_method = params.GetMethod();
         m_params = std::make_shared<UniEncCryptoParams>(params);
         m_have_kp = false;
-        reset(device);
+        reset(std::vector<int>{device});
         dc();  // validates the parameters and derives digitsG / root (mkacc_create)
     }
     void SetKeyParams(const mkkg_params& kp) {
@@ -590,6 +625,17 @@ public:
     }
     // Extension: seed of the key/encryption sampler (0 = random, the reference's behaviour).
     void SetSeed(uint64_t seed) { m_seed = seed; }
+    // Extension: the seed-0 entropy journal of this process (mkfhe_keys.h): the
+    // 64-hex-digit master key and the number of seed-0 calls made under it.  A
+    // run started with MKFHE_ENTROPY=<master> repeats every seed-0 key and
+    // encryption of a run that made the same calls (tools/replay_entropy.py).
+    static std::string GetEntropy(uint64_t* calls = nullptr) {
+        uint32_t m[8];
+        check(mkkg_entropy_get(m, calls));
+        char buf[65];
+        for (int i = 0; i < 8; ++i) std::snprintf(buf + 8 * i, 9, "%08x", m[i]);
+        return std::string(buf, 64);
+    }
     const std::shared_ptr<UniEncCryptoParams>& GetParams() const { return m_params; }
     // modKS = mod and baseKS = 32 in every MK set (binfhecontext.cpp:129-144)
     mkacc_ks_params GetKSParams() const {
@@ -622,8 +668,7 @@ public:
         UniEncBTKey ek = common_btkey(col0);
         ek.ksk.resize(mkkg_ksk_mntru_words(&m_kp));
         check(mkkg_ksk_mntru(&m_kp, next_seed(), ek.fvec.data(), sk->Finv().data(), ek.ksk.data()));
-        const mkacc_ks_params ks = GetKSParams();
-        check(mkacc_upload_ksk_mntru(dc().get(), &ks, ek.ksk.data()));
+        up_ksk_mntru(ek.ksk.data());
         m_BTKey = std::move(ek);
         m_keys = true;
     }
@@ -634,8 +679,7 @@ public:
         ek.ksk_b.resize(mkkg_ksk_mklwe_b_words(&m_kp));
         check(mkkg_ksk_mklwe(&m_kp, next_seed(), ek.fvec.data(), sk->flat().data(), ek.ksk_a.data(),
                              ek.ksk_b.data()));
-        const mkacc_ks_params ks = GetKSParams();
-        check(mkacc_upload_ksk_mklwe(dc().get(), &ks, ek.ksk_a.data(), ek.ksk_b.data()));
+        up_ksk_mklwe(ek.ksk_a.data(), ek.ksk_b.data());
         m_BTKey = std::move(ek);
         m_keys = true;
     }
@@ -686,12 +730,11 @@ public:
         get("pkey", ek.pkey); get("evk", ek.evk); get("ksk", ek.ksk); get("ksk_a", ek.ksk_a); get("ksk_b", ek.ksk_b);
         if (ek.evk.size() != mkkg_evk_words(&m_kp) || ek.pkey.size() != mkkg_pkey_words(&m_kp))
             throw config_error(path + ": key sizes do not match the context");
-        check(mkacc_upload_keys(dc().get(), ek.evk.data(), ek.pkey.data()));
-        const mkacc_ks_params ks = GetKSParams();
+        up_keys(ek.evk.data(), ek.pkey.data());
         if (m_method == MKNTRU_LWE)
-            check(mkacc_upload_ksk_mklwe(dc().get(), &ks, ek.ksk_a.data(), ek.ksk_b.data()));
+            up_ksk_mklwe(ek.ksk_a.data(), ek.ksk_b.data());
         else
-            check(mkacc_upload_ksk_mntru(dc().get(), &ks, ek.ksk.data()));
+            up_ksk_mntru(ek.ksk.data());
         m_BTKey = std::move(ek);
         m_keys = true;
     }
@@ -768,7 +811,13 @@ public:
     void BTKeyLoad(const UniEncBTKey& ek) {
         need_context();
         if (!ek.BSkey) throw config_error("BSkey is empty");
-        UniEncAccumulator::upload(dc(), ek.BSkey, ek.Pkey);
+        if (grouped()) {
+            const std::vector<uint32_t> evk = UniEncAccumulator::flatten_evk(gc().params(), ek.BSkey);
+            const std::vector<uint32_t> pk = UniEncAccumulator::flatten_pkey(gc().params(), ek.Pkey);
+            up_keys(evk.data(), pk.data());
+        } else {
+            UniEncAccumulator::upload(dc(), ek.BSkey, ek.Pkey);
+        }
         const mkacc_ks_params ks = GetKSParams();
         const uint32_t k = m_params->Getk(), N = m_params->GetN(), n = ks.n_out;
         const uint32_t dks = mkacc_ks_digits(&ks);
@@ -786,7 +835,7 @@ public:
                     for (uint32_t i = 0; i < n; ++i) h[((size_t)u * N * dks + l) * n + i] = (uint32_t)row[i];
                 }
             }
-            check(mkacc_upload_ksk_mntru(dc().get(), &ks, h.data()));
+            up_ksk_mntru(h.data());
         } else {
             if (!ek.LKSkey) throw config_error("LKSkey is empty");
             const auto& A = ek.LKSkey->GetElementsA();
@@ -803,7 +852,7 @@ public:
                             for (uint32_t i = 0; i < n; ++i) ha[r * n + i] = (uint32_t)row[i];
                             hb[r] = (uint32_t)Bk.at(u).at(j).at(d).at(t);
                         }
-            check(mkacc_upload_ksk_mklwe(dc().get(), &ks, ha.data(), hb.data()));
+            up_ksk_mklwe(ha.data(), hb.data());
         }
         m_keys = true;
     }
@@ -836,7 +885,10 @@ public:
             pack(*ct1[b], a1.data() + b * k * n, k, n);
             pack(*ct2[b], a2.data() + b * k * n, k, n);
         }
-        check(mkacc_eval_nand_mntru(dc().get(), nand.data(), a1.data(), a2.data(), out.data(), B));
+        if (grouped())
+            check(mkacc_group_eval_nand_mntru(gc().get(), nand.data(), a1.data(), a2.data(), out.data(), B));
+        else
+            check(mkacc_eval_nand_mntru(dc().get(), nand.data(), a1.data(), a2.data(), out.data(), B));
         std::vector<MNTRUCiphertext> res(B);
         for (size_t b = 0; b < B; ++b) res[b] = unpack_mntru(out.data() + b * k * n, k, n, GetKSParams().qKS);
         return res;
@@ -855,8 +907,12 @@ public:
             b1[b] = (uint32_t)ct1[b]->GetB();
             b2[b] = (uint32_t)ct2[b]->GetB();
         }
-        check(mkacc_eval_nand_mklwe(dc().get(), a1.data(), b1.data(), a2.data(), b2.data(), oa.data(), ob.data(),
-                                    B));
+        if (grouped())
+            check(mkacc_group_eval_nand_mklwe(gc().get(), a1.data(), b1.data(), a2.data(), b2.data(), oa.data(),
+                                              ob.data(), B));
+        else
+            check(mkacc_eval_nand_mklwe(dc().get(), a1.data(), b1.data(), a2.data(), b2.data(), oa.data(), ob.data(),
+                                        B));
         std::vector<MKLWECiphertext> res(B);
         for (size_t b = 0; b < B; ++b) {
             std::vector<NativeVector> a(k, NativeVector(n));
@@ -868,20 +924,52 @@ public:
     }
 
 private:
-    void reset(int device) {
-        m_device = device;
+    void reset(const std::vector<int>& devices) {
+        m_devices = devices;
         m_dc.reset();
+        m_gc.reset();
         m_keys = false;
         m_ctNAND.reset();
         m_BTKey = UniEncBTKey{};
     }
+    bool grouped() const { return m_devices.size() > 1; }
     DeviceContext& dc() const {
         need_context();
+        if (grouped()) throw config_error("a multi-device context has no single device context");
         if (!m_dc) {
-            m_dc = std::make_unique<DeviceContext>(m_params->abi(), m_device);
+            m_dc = std::make_unique<DeviceContext>(m_params->abi(), m_devices[0]);
             m_params->set_abi(m_dc->params());
         }
         return *m_dc;
+    }
+    GroupContext& gc() const {
+        need_context();
+        if (!m_gc) {
+            m_gc = std::make_unique<GroupContext>(m_params->abi(), m_devices);
+            m_params->set_abi(m_gc->params());
+        }
+        return *m_gc;
+    }
+    // uploads through the single context or the group
+    void up_keys(const uint32_t* evk, const uint32_t* pkey) const {
+        if (grouped())
+            check(mkacc_group_upload_keys(gc().get(), evk, pkey));
+        else
+            check(mkacc_upload_keys(dc().get(), evk, pkey));
+    }
+    void up_ksk_mntru(const uint32_t* ksk) const {
+        const mkacc_ks_params ks = GetKSParams();
+        if (grouped())
+            check(mkacc_group_upload_ksk_mntru(gc().get(), &ks, ksk));
+        else
+            check(mkacc_upload_ksk_mntru(dc().get(), &ks, ksk));
+    }
+    void up_ksk_mklwe(const uint32_t* A, const uint32_t* B) const {
+        const mkacc_ks_params ks = GetKSParams();
+        if (grouped())
+            check(mkacc_group_upload_ksk_mklwe(gc().get(), &ks, A, B));
+        else
+            check(mkacc_upload_ksk_mklwe(dc().get(), &ks, A, B));
     }
     void need_context() const {
         if (!m_params) throw config_error("call GenerateBinFHEContext first");
@@ -907,7 +995,7 @@ private:
         check(mkkg_ring_secrets(&m_kp, next_seed(), ek.fvec.data(), ek.f_eval.data(), ek.finv_eval.data()));
         check(mkkg_pkey(&m_kp, next_seed(), ek.crs.data(), ek.f_eval.data(), ek.pkey.data()));
         check(mkkg_acc_keygen(&m_kp, next_seed(), ek.crs.data(), ek.finv_eval.data(), lwe_sk.data(), ek.evk.data()));
-        check(mkacc_upload_keys(dc().get(), ek.evk.data(), ek.pkey.data()));
+        up_keys(ek.evk.data(), ek.pkey.data());
         return ek;
     }
     static MNTRUCiphertext unpack_mntru(const uint32_t* c, uint32_t k, uint32_t n, uint64_t q) {
@@ -967,7 +1055,8 @@ private:
     BINFHE_METHOD m_method = MKNTRU;
     std::shared_ptr<UniEncCryptoParams> m_params;
     mutable std::unique_ptr<DeviceContext> m_dc;
-    int m_device = 0;
+    mutable std::unique_ptr<GroupContext> m_gc;
+    std::vector<int> m_devices{0};
     bool m_keys = false;
     MNTRUCiphertext m_ctNAND;
     mkkg_params m_kp{};

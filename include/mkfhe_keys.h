@@ -35,10 +35,18 @@
  * Sampling follows the reference's distributions (OpenFHE's Peikert-inversion
  * discrete Gaussian, std::normal_distribution truncated to an integer where
  * the reference assigns a double to an NTL ZZ_p, uniform ternary / binary).
- * The reference seeds from the clock, so its keys are not reproducible; here
- * every call takes a 64-bit seed (0 = draw one from std::random_device) and
- * the output is a deterministic function of it, independent of the thread
- * count.  Randomness is xoshiro256** keyed by SplitMix64 -- NOT a CSPRNG.
+ * The reference seeds from the clock, so its keys are not reproducible
+ * (binfhe-base-scheme.cpp:111, mntru-pke.cpp:27).  Here every call takes a
+ * 64-bit seed:
+ *   seed != 0  reproducible test keys: xoshiro256** streams keyed by
+ *              SplitMix64(seed) -- NOT a CSPRNG;
+ *   seed == 0  fresh keys, the reference's behaviour: ChaCha20 streams under a
+ *              256-bit call key derived from the process's entropy journal
+ *              (a master key from std::random_device, or MKFHE_ENTROPY = 64
+ *              hex digits, and a counter of seed-0 calls).  mkkg_entropy_get
+ *              reports the master, so a run with a wrong gate can be replayed
+ *              exactly (tools/replay_entropy.py).
+ * Outputs are independent of the thread count.
  *
  * Layouts (row-major, canonical residues):
  *   F, Finv  [k][n][n] mod qKS: F[u][l][j] = row l, column j of party u's
@@ -63,7 +71,7 @@
 extern "C" {
 #endif
 
-#define MKKG_ABI_VERSION 1
+#define MKKG_ABI_VERSION 2
 
 /* SecretKeyDist values used by the MK parameter sets (binfhe-constants.h) */
 #define MKKG_DIST_TERNARY  0  /* UNIFORM_TERNARY */
@@ -168,8 +176,20 @@ int mkkg_file_read_section(const char* path, const char* name, uint32_t* out, ui
 int mkkg_ntt_forward(const mkkg_params* p, const uint32_t* in, uint32_t* out, size_t count);
 int mkkg_ntt_inverse(const mkkg_params* p, const uint32_t* in, uint32_t* out, size_t count);
 
+/* ---- seed-0 entropy journal --------------------------------------------------
+ * master: 8 words = the 64 hex digits of MKFHE_ENTROPY, word 0 first.
+ * mkkg_entropy_get: the master (drawn now if no seed-0 call has drawn it yet)
+ *   and the number of seed-0 calls made since it was set.
+ * mkkg_entropy_set: restart the journal at (master, calls); master NULL draws
+ *   a fresh master from std::random_device. */
+int mkkg_entropy_get(uint32_t master[8], uint64_t* calls);
+int mkkg_entropy_set(const uint32_t master[8], uint64_t calls);
+
 const char* mkkg_last_error(void);
 int mkkg_abi_version(void);
+/* "abi=..;header=<id>;source=<id>;flags=": SHA-256 prefixes of mkfhe_keys.h +
+ * mkfhe_amd.h and of the library's sources (mkfhe_amd/build.py). */
+const char* mkkg_build_info(void);
 
 #ifdef __cplusplus
 }

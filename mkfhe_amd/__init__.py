@@ -12,6 +12,7 @@ from .accumulator import (  # noqa: F401
     MKNTRU_LWE,
     PARAMSETS,
     MKAccumulatorEngine,
+    MKAccumulatorGroup,
     UniEncAccumulator,
     UniEncAccumulatorXZW,
     UniEncAccumulatorXZW_B,
@@ -22,6 +23,6 @@ from .accumulator import (  # noqa: F401
 
 __all__ = [
     "LIB_PATH", "MkaccError", "MkaccParams", "MKNTRU", "MKNTRU_B", "MKNTRU_LWE", "PARAMSETS",
-    "MKAccumulatorEngine", "UniEncAccumulator", "UniEncAccumulatorXZW", "UniEncAccumulatorXZW_B",
+    "MKAccumulatorEngine", "MKAccumulatorGroup", "UniEncAccumulator", "UniEncAccumulatorXZW", "UniEncAccumulatorXZW_B",
     "accumulator_for", "make_params", "paramset",
 ]

@@ -200,6 +200,18 @@ class MKAccumulatorEngine:
         check(_lib.load().mkacc_upload_ksk_mklwe(self._h, ctypes.byref(ks), _u32(a), _u32(b)))
         self.ks = ks
 
+    def upload_ksk_device(self, qKS: int, baseKS: int, n_out: int, d_ksk=None, d_A=None, d_B=None):
+        """Key-switching keys from device memory (torch tensors or ints on this
+        context's device, u32 words in the host layouts); converted on the GPU."""
+        def ptr(t):
+            return ctypes.c_void_p(t if isinstance(t, int) else t.data_ptr())
+        ks = _lib.MkaccKsParams(qKS, baseKS, n_out)
+        if self.method == MKNTRU:
+            check(_lib.load().mkacc_upload_ksk_mntru_device(self._h, ctypes.byref(ks), ptr(d_ksk)))
+        else:
+            check(_lib.load().mkacc_upload_ksk_mklwe_device(self._h, ctypes.byref(ks), ptr(d_A), ptr(d_B)))
+        self.ks = ks
+
     def _need_ksk(self):
         if self.ks is None:
             raise MkaccError(_lib.MKACC_E_NOKEYS, "Key-switching keys have not been uploaded")
@@ -273,6 +285,110 @@ class MKAccumulatorEngine:
         """SignedDigitDecompose (mk-acc.cpp:54-80): rows -> [rows][dg][N]."""
         out = self._prim("mkacc_sdd", a, self.dg)
         return out.reshape(-1, self.dg, self.N)
+
+
+def shard_range_c(B: int, parts: int, i: int) -> tuple[int, int]:
+    """mkacc_shard_range: the group's split of B gates (same as shard.shard_range)."""
+    b, e = ctypes.c_size_t(), ctypes.c_size_t()
+    _lib.load().mkacc_shard_range(B, parts, i, ctypes.byref(b), ctypes.byref(e))
+    return b.value, e.value
+
+
+class MKAccumulatorGroup:
+    """A multi-device group (mkacc_group): one context per entry of `devices` (a
+    device may repeat), keys converted once and copied device to device, batches
+    split into contiguous shards that run concurrently.  Same batch interface as
+    MKAccumulatorEngine; outputs are bit-identical to one context's."""
+
+    def __init__(self, params: MkaccParams, devices):
+        L = _lib.load()
+        devs = (ctypes.c_int * len(devices))(*devices)
+        h = ctypes.c_void_p()
+        check(L.mkacc_group_create(ctypes.byref(params), devs, len(devices), ctypes.byref(h)))
+        self._h = h
+        self.devices = list(devices)
+        eff = MkaccParams()
+        check(L.mkacc_get_params(L.mkacc_group_member(h, 0), ctypes.byref(eff)))
+        self.params = eff
+        self.method, self.k, self.n, self.N = eff.method, eff.k, eff.n, eff.N
+        self.Q, self.q, self.baseG, self.digitsG = eff.Q, eff.q, eff.baseG, eff.digitsG
+        self.dg = eff.digitsG - 1
+        self.nk = 2 if eff.method == MKNTRU else 1
+        self.ks = None
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.load().mkacc_group_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    @property
+    def size(self) -> int:
+        return int(_lib.load().mkacc_group_size(self._h))
+
+    def upload_keys(self, evk: np.ndarray, pkey: np.ndarray):
+        L = _lib.load()
+        if evk.dtype == np.uint64 or pkey.dtype == np.uint64:
+            e = np.ascontiguousarray(evk, dtype=np.uint64)
+            p = np.ascontiguousarray(pkey, dtype=np.uint64)
+            check(L.mkacc_group_upload_keys_u64(self._h, e.ctypes.data_as(_u64p), p.ctypes.data_as(_u64p)))
+        else:
+            e = np.ascontiguousarray(evk, dtype=np.uint32)
+            p = np.ascontiguousarray(pkey, dtype=np.uint32)
+            check(L.mkacc_group_upload_keys(self._h, _u32(e), _u32(p)))
+
+    def eval_batch(self, ct: np.ndarray, acc: np.ndarray) -> np.ndarray:
+        ct32 = np.ascontiguousarray(ct, dtype=np.uint32)
+        use64 = acc.dtype == np.uint64 or self.Q >= (1 << 32)
+        accw = np.ascontiguousarray(acc, dtype=np.uint64 if use64 else np.uint32)
+        B = ct32.shape[0]
+        if ct32.shape != (B, self.k, self.n) or accw.shape != (B, self.k, self.N):
+            raise MkaccError(_lib.MKACC_E_ARG, "ct must be [B][k][n] and acc [B][k][N]")
+        out = np.empty_like(accw)
+        if use64:
+            check(_lib.load().mkacc_group_eval_batch_u64(self._h, _u32(ct32), accw.ctypes.data_as(_u64p),
+                                                         out.ctypes.data_as(_u64p), B))
+        else:
+            check(_lib.load().mkacc_group_eval_batch(self._h, _u32(ct32), _u32(accw), _u32(out), B))
+        return out
+
+    def upload_ksk_mntru(self, ksk: np.ndarray, qKS: int, baseKS: int, n_out: int):
+        ks = _lib.MkaccKsParams(qKS, baseKS, n_out)
+        check(_lib.load().mkacc_group_upload_ksk_mntru(self._h, ctypes.byref(ks),
+                                                       _u32(np.ascontiguousarray(ksk, dtype=np.uint32))))
+        self.ks = ks
+
+    def upload_ksk_mklwe(self, A: np.ndarray, B: np.ndarray, qKS: int, baseKS: int, n_out: int):
+        ks = _lib.MkaccKsParams(qKS, baseKS, n_out)
+        check(_lib.load().mkacc_group_upload_ksk_mklwe(self._h, ctypes.byref(ks),
+                                                       _u32(np.ascontiguousarray(A, dtype=np.uint32)),
+                                                       _u32(np.ascontiguousarray(B, dtype=np.uint32))))
+        self.ks = ks
+
+    def eval_nand_mntru(self, ct_nand, ct1, ct2) -> np.ndarray:
+        if self.ks is None:
+            raise MkaccError(_lib.MKACC_E_NOKEYS, "Key-switching keys have not been uploaded")
+        c1 = np.ascontiguousarray(ct1, dtype=np.uint32)
+        c2 = np.ascontiguousarray(ct2, dtype=np.uint32)
+        cn = np.ascontiguousarray(ct_nand, dtype=np.uint32)
+        B = c1.shape[0]
+        out = np.empty((B, self.k, self.ks.n_out), dtype=np.uint32)
+        check(_lib.load().mkacc_group_eval_nand_mntru(self._h, _u32(cn), _u32(c1), _u32(c2), _u32(out), B))
+        return out
+
+    def eval_nand_mklwe(self, a1, b1, a2, b2):
+        if self.ks is None:
+            raise MkaccError(_lib.MKACC_E_NOKEYS, "Key-switching keys have not been uploaded")
+        a1, a2 = np.ascontiguousarray(a1, dtype=np.uint32), np.ascontiguousarray(a2, dtype=np.uint32)
+        b1, b2 = np.ascontiguousarray(b1, dtype=np.uint32), np.ascontiguousarray(b2, dtype=np.uint32)
+        B = a1.shape[0]
+        oa = np.empty((B, self.k, self.ks.n_out), dtype=np.uint32)
+        ob = np.empty(B, dtype=np.uint32)
+        check(_lib.load().mkacc_group_eval_nand_mklwe(self._h, _u32(a1), _u32(b1), _u32(a2), _u32(b2), _u32(oa),
+                                                      _u32(ob), B))
+        return oa, ob
 
 
 class UniEncAccumulator:

@@ -22,7 +22,7 @@ from __future__ import annotations
 import numpy as np
 
 from . import keys as K
-from .accumulator import MKNTRU, MKNTRU_B, MKNTRU_LWE, MKAccumulatorEngine
+from .accumulator import MKNTRU, MKNTRU_B, MKNTRU_LWE, MKAccumulatorEngine, MKAccumulatorGroup
 
 NAND = 3  # BINGATE value (binfhe-constants.h)
 
@@ -43,7 +43,9 @@ class BinFHEContext:
         self.ctNAND = None
 
     # ---- context ------------------------------------------------------------------
-    def GenerateBinFHEContext(self, paramset: str, method: int = MKNTRU, device: int = 0):
+    def GenerateBinFHEContext(self, paramset: str, method: int = MKNTRU, device=0):
+        """device: one HIP device, or a list of devices -- batches of gates then shard
+        across them (mkacc_group; keys converted once and copied device to device)."""
         if method not in (MKNTRU, MKNTRU_B, MKNTRU_LWE):
             raise ConfigError("method is invalid")
         self.kp = K.paramset(paramset, method)
@@ -64,9 +66,12 @@ class BinFHEContext:
         self._calls += 1
         return (self._seed + self._calls * 0x9E3779B97F4A7C15) & ((1 << 64) - 1) or 1
 
-    def engine(self) -> MKAccumulatorEngine:
+    def engine(self):
         if self._eng is None:
-            self._eng = MKAccumulatorEngine(self.kp.acc, self.device)
+            if isinstance(self.device, (list, tuple)):
+                self._eng = MKAccumulatorGroup(self.kp.acc, list(self.device))
+            else:
+                self._eng = MKAccumulatorEngine(self.kp.acc, self.device)
         return self._eng
 
     @property

@@ -3,12 +3,20 @@
     mkfhe_amd/lib/libmkfhe_keys.so  host key material (g++, include/mkfhe_keys.h)
 
     python -m mkfhe_amd.build [--force]
+    python -m mkfhe_amd.build --variant NAME [-DFLAG ...]   # A/B engine build -> lib/variants/NAME.so
 
 Plain hipcc invocation -- no JIT cache, so the .so travels with the repo
 snapshot to the GPU box.
+
+Every library carries its build identity (mkacc_build_info / mkkg_build_info):
+the SHA-256 prefix of its public header and of all of its sources, and the
+extra compile flags.  The Python loaders (_lib.load, keys.load) refuse a
+library whose ABI version or header id differs from the tree they run in, and
+the default libraries must also match the sources (a stale build is refused).
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import subprocess
 import sys
@@ -24,6 +32,30 @@ KEYS_HEADERS = [os.path.join(_HERE, "csrc", "mkacc_host_math.hpp"), os.path.join
                 os.path.join(ROOT, "include", "mkfhe_amd.h")]
 KEYS_OUT = os.path.join(_HERE, "lib", "libmkfhe_keys.so")
 ARCH = os.environ.get("MKFHE_OFFLOAD_ARCH", "gfx950")
+ENGINE_HEADER = os.path.join(ROOT, "include", "mkfhe_amd.h")
+KEYS_HEADER = os.path.join(ROOT, "include", "mkfhe_keys.h")
+
+
+def file_id(paths) -> str:
+    """SHA-256 prefix (16 hex digits) of the concatenated file contents."""
+    h = hashlib.sha256()
+    for p in paths:
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def engine_ids() -> dict:
+    return {"header": file_id([ENGINE_HEADER]), "source": file_id(SOURCES + HEADERS)}
+
+
+def keys_ids() -> dict:
+    return {"header": file_id([KEYS_HEADER, ENGINE_HEADER]), "source": file_id(KEYS_SOURCES + KEYS_HEADERS)}
+
+
+def _id_defines(prefix: str, ids: dict, flags: list[str]) -> list[str]:
+    return [f'-D{prefix}_HEADER_ID="{ids["header"]}"', f'-D{prefix}_SOURCE_ID="{ids["source"]}"',
+            f'-D{prefix}_BUILD_FLAGS="{" ".join(flags)}"']
 
 
 def _stale(out, deps) -> bool:
@@ -43,7 +75,7 @@ def build_keys(force: bool = False, verbose: bool = False) -> str:
     cmd = [cxx, "-O3", "-march=x86-64-v3", "-std=c++17", "-fPIC", "-shared", "-pthread",
            "-fvisibility-inlines-hidden", "-Wl,-Bsymbolic",
            "-I", os.path.join(ROOT, "include"), "-I", os.path.join(_HERE, "csrc"),
-           "-o", KEYS_OUT + ".tmp"] + KEYS_SOURCES
+           *_id_defines("MKKG", keys_ids(), []), "-o", KEYS_OUT + ".tmp"] + KEYS_SOURCES
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)
@@ -51,24 +83,40 @@ def build_keys(force: bool = False, verbose: bool = False) -> str:
     return KEYS_OUT
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    build_keys(force, verbose)
-    if not force and not _stale(OUT, SOURCES + HEADERS):
-        return OUT
-    os.makedirs(os.path.dirname(OUT), exist_ok=True)
+def compile_engine(out: str, flags: list[str], report: str, verbose: bool = False) -> str:
+    """hipcc the engine into `out` with extra `flags` (-D switches of A/B builds)."""
+    os.makedirs(os.path.dirname(out), exist_ok=True)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-fvisibility-inlines-hidden", "-Wl,-Bsymbolic",
            "-Wno-unused-result", "-Wno-pass-failed", "-I", os.path.join(ROOT, "include"),
-           "-Rpass-analysis=kernel-resource-usage", "-o", OUT + ".tmp"] + SOURCES
+           *_id_defines("MKACC", engine_ids(), flags), *flags,
+           "-Rpass-analysis=kernel-resource-usage", "-o", out + ".tmp"] + SOURCES
     if verbose:
         print(" ".join(cmd))
     # per-kernel VGPR / spill / occupancy report next to the library
-    with open(os.path.join(os.path.dirname(OUT), "resource_usage.txt"), "w") as rep:
+    with open(report, "w") as rep:
         subprocess.check_call(cmd, stderr=rep)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(out + ".tmp", out)
+    return out
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    build_keys(force, verbose)
+    if not force and not _stale(OUT, SOURCES + HEADERS):
+        return OUT
+    return compile_engine(OUT, [], os.path.join(os.path.dirname(OUT), "resource_usage.txt"), verbose)
+
+
+def build_variant(name: str, flags: list[str], verbose: bool = False) -> str:
+    """An A/B build of the engine with extra -D switches: lib/variants/NAME.so."""
+    out = os.path.join(_HERE, "lib", "variants", name + ".so")
+    return compile_engine(out, flags, out[:-3] + ".res", verbose)
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    if "--variant" in sys.argv:
+        i = sys.argv.index("--variant")
+        print(build_variant(sys.argv[i + 1], sys.argv[i + 2:], verbose=True))
+    else:
+        print(build(force="--force" in sys.argv, verbose=True))

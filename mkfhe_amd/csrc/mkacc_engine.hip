@@ -927,37 +927,73 @@ __global__ void wide_key_layout_kernel(const W* __restrict__ src, uint64_t* __re
     }
 }
 
-// MKACC_ONLY_DG=d (developer builds for ISA studies): instantiate one digit count
+// Every digit count is instantiated.  (Round 2's MKACC_ONLY_DG=3 A/B builds
+// returned null here for other digit counts and the launch of a null kernel
+// produced the segfault / all-wrong records of ab_l1, lat_l1 and ab_d1,
+// DESIGN.md s2; a null kernel is now refused at mkacc_create and launch.)
 StepFn step_fn(int dg, int method, bool first, bool dscr) {
     switch (dg) {
-#if !defined(MKACC_ONLY_DG) || MKACC_ONLY_DG == 2
         case 2: return pick_step<2>(method, first, dscr);
-#endif
-#if !defined(MKACC_ONLY_DG) || MKACC_ONLY_DG == 3
         case 3: return pick_step<3>(method, first, dscr);
-#endif
-#if !defined(MKACC_ONLY_DG) || MKACC_ONLY_DG == 4
         case 4: return pick_step<4>(method, first, dscr);
-#endif
-#if !defined(MKACC_ONLY_DG) || MKACC_ONLY_DG == 5
         case 5: return pick_step<5>(method, first, dscr);
-#endif
         default: return nullptr;
     }
 }
 StepFn lat_fn(int dg, int method, bool first) {
     switch (dg) {
-#if !defined(MKACC_ONLY_DG) || MKACC_ONLY_DG == 2
         case 2: return pick_lat<2>(method, first);
-#endif
-#if !defined(MKACC_ONLY_DG) || MKACC_ONLY_DG == 3
         case 3: return pick_lat<3>(method, first);
-#endif
-#if !defined(MKACC_ONLY_DG) || MKACC_ONLY_DG == 4
         case 4: return pick_lat<4>(method, first);
-#endif
         default: return nullptr;
     }
+}
+
+// Key-switching keys from device memory (mkacc_upload_ksk_*_device): the host
+// conversions of mkacc_upload_ksk_mntru / _mklwe on the GPU.  MNTRU: reference row
+// l = j dks + t of [k][N dks][n] -> device row t N + j of [k][dks N][n_pad], u16;
+// MK-LWE: u32 -> u16 in place order.  A word >= qKS raises `bad`.
+__global__ void ksk_mntru_layout_kernel(const uint32_t* __restrict__ src, uint16_t* __restrict__ dst, uint32_t k,
+                                        uint32_t dks, uint32_t n, uint32_t npad, uint32_t qKS,
+                                        uint32_t* __restrict__ bad) {
+    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t L = (size_t)dks * kN;
+    if (idx >= (size_t)k * L * npad) return;
+    const uint32_t i = (uint32_t)(idx % npad);
+    const size_t row = (idx / npad) % L, u = idx / npad / L;
+    const uint32_t t = (uint32_t)(row / kN), j = (uint32_t)(row % kN);
+    uint32_t v = 0;
+    if (i < n) {
+        v = src[((u * kN + j) * dks + t) * n + i];
+        if (v >= qKS) {
+            *bad = 1u;
+            v = 0;
+        }
+    }
+    dst[idx] = (uint16_t)v;
+}
+__global__ void ksk_narrow_kernel(const uint32_t* __restrict__ src, uint16_t* __restrict__ dst, size_t count,
+                                  uint32_t qKS, uint32_t* __restrict__ bad) {
+    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= count) return;
+    uint32_t v = src[idx];
+    if (v >= qKS) {
+        *bad = 1u;
+        v = 0;
+    }
+    dst[idx] = (uint16_t)v;
+}
+
+__global__ void wide_copy_check_kernel(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, size_t count,
+                                       uint64_t Q, uint32_t* __restrict__ bad) {
+    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= count) return;
+    uint64_t x = in[idx];
+    if (x >= Q) {
+        *bad = 1u;
+        x = 0;
+    }
+    out[idx] = x;
 }
 
 }  // namespace
@@ -1028,7 +1064,7 @@ struct mkacc_ctx {
     uint32_t* d_wcvals = nullptr;
     uint32_t* d_wct = nullptr;     // host-pointer API staging
     uint64_t* d_wio = nullptr;
-    uint32_t* d_bad = nullptr;     // input-range flag of the device entry points (mkacc_sync)
+    uint32_t* d_bad = nullptr;     // [0] input-range flag of the device batches (mkacc_sync), [1] device key upload
     std::mutex mu;
 };
 
@@ -1087,7 +1123,7 @@ int ensure_ws(mkacc_ctx* c, size_t B) {
 
 // The k*n accumulator steps over a batch whose monomial exponents are in
 // d_cvals and whose C4 accumulators are in d_acc0; returns the buffer holding
-// the result.
+// the result (nullptr if the build has no kernel for the context's digit count).
 uint32_t* launch_steps(mkacc_ctx* c, size_t B) {
     const uint32_t k = c->p.k, n = c->p.n;
     uint32_t* cur = c->d_acc0;
@@ -1118,11 +1154,14 @@ uint32_t* launch_steps(mkacc_ctx* c, size_t B) {
             a.m = c->mod;
             a.sd = c->sd;
             a.dscr = c->d_dscr;
+            // a null kernel must never reach hipLaunchKernelGGL (mkacc_create checks the set)
             if (lat) {
-                hipLaunchKernelGGL(lat_fn((int)c->dg, c->method_class, first), dim3((unsigned)B), dim3(64 * k),
-                                   lat_lds_bytes(k), c->stream, a);
+                const StepFn fn = lat_fn((int)c->dg, c->method_class, first);
+                if (!fn) return nullptr;
+                hipLaunchKernelGGL(fn, dim3((unsigned)B), dim3(64 * k), lat_lds_bytes(k), c->stream, a);
             } else {
-                StepFn fn = step_fn((int)c->dg, c->method_class, first, !first && c->d_dscr != nullptr);
+                const StepFn fn = step_fn((int)c->dg, c->method_class, first, !first && c->d_dscr != nullptr);
+                if (!fn) return nullptr;
                 hipLaunchKernelGGL(fn, grid, block, lds, c->stream, a);
             }
             std::swap(cur, nxt);
@@ -1152,6 +1191,7 @@ int launch_batch(mkacc_ctx* c, const uint32_t* d_ct, const uint32_t* d_in, uint3
                            c->d_acc0, npoly, c->ninv, c->ninvp, c->mod.Q, c->d_bad);
     }
     uint32_t* cur = launch_steps(c, B);
+    if (!cur) return fail(MKACC_E_UNSUPPORTED, "no step kernel for this digit count in this build");
     {
         const size_t tw = npoly * kN;
         hipLaunchKernelGGL(c4_to_eval_kernel, dim3((unsigned)((tw + tpb - 1) / tpb)), dim3(tpb), 0, c->stream, cur,
@@ -1267,6 +1307,7 @@ int launch_gates(mkacc_ctx* c, const uint32_t* d_nand, const uint32_t* d_a1, con
     hipLaunchKernelGGL(acc_init_kernel, dim3((unsigned)((tw + 255) / 256)), dim3(256), 0, c->stream, c->d_acc0,
                        c->d_tv, c->method_class == XZW ? nullptr : c->d_bh, psi_image(c), (uint32_t)B, k, c->mod.Q);
     uint32_t* cur = launch_steps(c, B);
+    if (!cur) return fail(MKACC_E_UNSUPPORTED, "no step kernel for this digit count in this build");
     launch_tail(c, cur, d_out_a, d_out_b, B);
     HIP_TRY(hipGetLastError());
     return MKACC_OK;
@@ -1336,7 +1377,10 @@ int upload_keys_device_impl(mkacc_ctx* c, const W* d_evk, const W* d_pkey) {
     const unsigned tpb = 256;
     auto grid = [&](size_t np) { return dim3((unsigned)((np * kN + tpb - 1) / tpb)); };
     HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipMemsetAsync(c->d_bad, 0, 4, c->stream));
+    // the key check has its own flag word (d_bad[1]): a pending input-range error
+    // of an earlier device batch (d_bad[0]) stays for mkacc_sync to report
+    uint32_t* kbad = c->d_bad + 1;
+    HIP_TRY(hipMemsetAsync(kbad, 0, 4, c->stream));
     c->have_keys = false;
     if (c->wide) {
         const uint64_t Q = c->p.Q, R = (uint64_t)(((unsigned __int128)1 << 64) % Q);
@@ -1344,25 +1388,22 @@ int upload_keys_device_impl(mkacc_ctx* c, const W* d_evk, const W* d_pkey) {
         if (!c->d_wkeys) HIP_TRY(hipMalloc(&c->d_wkeys, ep * kN * 8));
         if (!c->d_wpkey) HIP_TRY(hipMalloc(&c->d_wpkey, pp * kN * 8));
         hipLaunchKernelGGL(wide_key_layout_kernel<W>, grid(ep), dim3(tpb), 0, c->stream, d_evk, c->d_wkeys, ep, nk,
-                           n1, dg * 2, Q, R, Rp, c->wfp, c->d_bad);
+                           n1, dg * 2, Q, R, Rp, c->wfp, kbad);
         hipLaunchKernelGGL(wide_key_layout_kernel<W>, grid(pp), dim3(tpb), 0, c->stream, d_pkey, c->d_wpkey, pp, 1u,
-                           1u, dg, Q, R, Rp, c->wfp, c->d_bad);
+                           1u, dg, Q, R, Rp, c->wfp, kbad);
     } else {
         if (!c->d_keys) HIP_TRY(hipMalloc(&c->d_keys, ep * kN * 4));
         if (!c->d_pkey) HIP_TRY(hipMalloc(&c->d_pkey, pp * kN * 4));
         hipLaunchKernelGGL(key_layout_kernel<W>, grid(ep), dim3(tpb), 0, c->stream, d_evk, c->d_keys, ep, nk, n1,
-                           dg * 2, c->mod.Q, c->kscale, c->kscalep, c->d_bad);
+                           dg * 2, c->mod.Q, c->kscale, c->kscalep, kbad);
         hipLaunchKernelGGL(key_layout_kernel<W>, grid(pp), dim3(tpb), 0, c->stream, d_pkey, c->d_pkey, pp, 1u, 1u,
-                           dg, c->mod.Q, c->kscale, c->kscalep, c->d_bad);
+                           dg, c->mod.Q, c->kscale, c->kscalep, kbad);
     }
     HIP_TRY(hipGetLastError());
     uint32_t bad = 0;
-    HIP_TRY(hipMemcpyAsync(&bad, c->d_bad, 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(&bad, kbad, 4, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    if (bad) {
-        HIP_TRY(hipMemset(c->d_bad, 0, 4));
-        return fail(MKACC_E_RANGE, "evk/pkey word not a canonical residue mod Q");
-    }
+    if (bad) return fail(MKACC_E_RANGE, "evk/pkey word not a canonical residue mod Q");
     c->have_keys = true;
     return MKACC_OK;
 }
@@ -1540,7 +1581,8 @@ int wide_launch_batch(mkacc_ctx* c, const uint32_t* d_ct, const uint64_t* d_in, 
         const dim3 g((unsigned)((words + 255) / 256));
         double* cur = reinterpret_cast<double*>(c->d_wacc0);
         double* nxt = reinterpret_cast<double*>(c->d_wacc1);
-        hipLaunchKernelGGL(widefp::to_balanced_kernel, g, dim3(256), 0, c->stream, d_in, cur, words, c->wfm);
+        hipLaunchKernelGGL(widefp::to_balanced_kernel, g, dim3(256), 0, c->stream, d_in, cur, words, c->wfm,
+                           c->p.Q, c->d_bad);
         auto dk = [](const uint64_t* p) { return reinterpret_cast<const double*>(p); };
         for (uint32_t u = 0; u < k; ++u)
             for (uint32_t i = 0; i < n; ++i) {
@@ -1573,7 +1615,11 @@ int wide_launch_batch(mkacc_ctx* c, const uint32_t* d_ct, const uint64_t* d_in, 
         HIP_TRY(hipGetLastError());
         return MKACC_OK;
     }
-    HIP_TRY(hipMemcpyAsync(c->d_wacc0, d_in, accb, hipMemcpyDeviceToDevice, c->stream));
+    {   // copy into the working buffer with the range check of the device entry point
+        const size_t words = accb / 8;
+        hipLaunchKernelGGL(wide_copy_check_kernel, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, c->stream, d_in,
+                           c->d_wacc0, words, c->p.Q, c->d_bad);
+    }
     uint64_t* cur = c->d_wacc0;
     uint64_t* nxt = c->d_wacc1;
     for (uint32_t u = 0; u < k; ++u)
@@ -1696,6 +1742,31 @@ extern "C" {
 
 int mkacc_abi_version(void) { return MKACC_ABI_VERSION; }
 
+// Build identity (mkfhe_amd/build.py passes the ids): SHA-256 prefixes of
+// include/mkfhe_amd.h and of every engine source, and the extra -D switches of
+// an A/B build.  mkfhe_amd._lib.load refuses a library whose abi or header id
+// does not match the tree it runs in.
+#ifndef MKACC_HEADER_ID
+#define MKACC_HEADER_ID "unknown"
+#endif
+#ifndef MKACC_SOURCE_ID
+#define MKACC_SOURCE_ID "unknown"
+#endif
+#ifndef MKACC_BUILD_FLAGS
+#define MKACC_BUILD_FLAGS ""
+#endif
+const char* mkacc_build_info(void) {
+    static const std::string info = [] {
+        std::string dgs;
+        for (int dg = 2; dg <= 5; ++dg)
+            if (step_fn(dg, XZW, true, false) && step_fn(dg, XZW_B, false, false))
+                dgs += (dgs.empty() ? "" : ",") + std::to_string(dg);
+        return "abi=" + std::to_string(MKACC_ABI_VERSION) + ";header=" MKACC_HEADER_ID ";source=" MKACC_SOURCE_ID
+               ";dg=" + dgs + ";flags=" MKACC_BUILD_FLAGS;
+    }();
+    return info.c_str();
+}
+
 const char* mkacc_last_error(void) { return g_last_error.c_str(); }
 
 int mkacc_paramset(const char* name, uint32_t method, mkacc_params* out) {
@@ -1763,11 +1834,13 @@ int mkacc_create(const mkacc_params* pin, int device, mkacc_ctx** out) {
     c->dg = dg;
     c->nk = c->method_class == XZW ? 2 : 1;
     c->wide = wide;
+    if (!wide && !step_fn((int)dg, c->method_class, true, false))
+        return fail(MKACC_E_UNSUPPORTED, "this build has no step kernel for dg = " + std::to_string(dg));
     if (wide) {
         HIP_TRY(hipSetDevice(device));
         HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-        HIP_TRY(hipMalloc(&c->d_bad, 4));
-        HIP_TRY(hipMemset(c->d_bad, 0, 4));
+        HIP_TRY(hipMalloc(&c->d_bad, 8));   // [0] batch inputs, [1] device key upload
+        HIP_TRY(hipMemset(c->d_bad, 0, 8));
         const int rc = wide_setup(c.get());
         if (rc) {
             mkacc_destroy(c.release());
@@ -1806,8 +1879,8 @@ int mkacc_create(const mkacc_params* pin, int device, mkacc_ctx** out) {
 
     HIP_TRY(hipSetDevice(device));
     HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    HIP_TRY(hipMalloc(&c->d_bad, 4));
-    HIP_TRY(hipMemset(c->d_bad, 0, 4));
+    HIP_TRY(hipMalloc(&c->d_bad, 8));   // [0] batch inputs, [1] device key upload
+    HIP_TRY(hipMemset(c->d_bad, 0, 8));
     // forward NTT table in the reference's order (transformnat-impl.h:705-760),
     // powers psi^e and psi^-e (e < 2N) for the inverse transform and the monomials
     const uint64_t Q = p.Q, psi = p.root, psii = modinv(psi, Q);
@@ -2068,6 +2141,74 @@ int mkacc_upload_ksk_mklwe(mkacc_ctx* c, const mkacc_ks_params* ks, const uint32
     return MKACC_OK;
 }
 
+}  // extern "C"
+
+namespace {
+// the device key-switching uploads: layout kernel(s) on the context stream, then
+// the range flag (d_bad[1]) read back; no keys are kept if a word is out of range
+template <class L>
+int ksk_device_finish(mkacc_ctx* c, L&& launch) {
+    uint32_t* kbad = c->d_bad + 1;
+    HIP_TRY(hipMemsetAsync(kbad, 0, 4, c->stream));
+    c->have_ksk = false;
+    int rc = launch(kbad);
+    if (rc) return rc;
+    HIP_TRY(hipGetLastError());
+    uint32_t bad = 0;
+    HIP_TRY(hipMemcpyAsync(&bad, kbad, 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (bad) return fail(MKACC_E_RANGE, "key-switching key word not a canonical residue mod qKS");
+    c->have_ksk = true;
+    return MKACC_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int mkacc_upload_ksk_mntru_device(mkacc_ctx* c, const mkacc_ks_params* ks, const void* d_ksk) {
+    if (!c || !d_ksk) return fail(MKACC_E_ARG, "null argument");
+    std::lock_guard<std::mutex> g(c->mu);
+    if (c->wide) return fail(MKACC_E_UNSUPPORTED, "the 64-bit word path covers EvalAcc only; NAND gates need Q < 2^27");
+    if (c->method_class != XZW) return fail(MKACC_E_ARG, "KeySwitch2 keys belong to the MKNTRU method");
+    int rc = check_ks(c, ks);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t w = (size_t)c->p.k * c->dks * kN * c->n_pad;
+    if (c->d_ksk) HIP_TRY(hipFree(c->d_ksk));
+    c->d_ksk = nullptr;
+    HIP_TRY(hipMalloc(&c->d_ksk, w * 2));
+    return ksk_device_finish(c, [&](uint32_t* kbad) {
+        hipLaunchKernelGGL(ksk_mntru_layout_kernel, dim3((unsigned)((w + 255) / 256)), dim3(256), 0, c->stream,
+                           (const uint32_t*)d_ksk, c->d_ksk, c->p.k, c->dks, c->ks.n_out, c->n_pad,
+                           (uint32_t)c->ks.qKS, kbad);
+        return MKACC_OK;
+    });
+}
+
+int mkacc_upload_ksk_mklwe_device(mkacc_ctx* c, const mkacc_ks_params* ks, const void* d_A, const void* d_B) {
+    if (!c || !d_A || !d_B) return fail(MKACC_E_ARG, "null argument");
+    std::lock_guard<std::mutex> g(c->mu);
+    if (c->wide) return fail(MKACC_E_UNSUPPORTED, "the 64-bit word path covers EvalAcc only; NAND gates need Q < 2^27");
+    if (c->method_class != XZW_B) return fail(MKACC_E_ARG, "MK-LWE KeySwitch keys belong to the MKNTRU_LWE method");
+    if (int rc = reject_mkntru_b(c)) return rc;
+    int rc = check_ks(c, ks);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t rows = (size_t)c->p.k * kN * ks->baseKS * c->dks, wa = rows * ks->n_out;
+    if (c->d_lweA) HIP_TRY(hipFree(c->d_lweA));
+    if (c->d_lweB) HIP_TRY(hipFree(c->d_lweB));
+    c->d_lweA = c->d_lweB = nullptr;
+    HIP_TRY(hipMalloc(&c->d_lweA, wa * 2));
+    HIP_TRY(hipMalloc(&c->d_lweB, rows * 2));
+    return ksk_device_finish(c, [&](uint32_t* kbad) {
+        hipLaunchKernelGGL(ksk_narrow_kernel, dim3((unsigned)((wa + 255) / 256)), dim3(256), 0, c->stream,
+                           (const uint32_t*)d_A, c->d_lweA, wa, (uint32_t)ks->qKS, kbad);
+        hipLaunchKernelGGL(ksk_narrow_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, c->stream,
+                           (const uint32_t*)d_B, c->d_lweB, rows, (uint32_t)ks->qKS, kbad);
+        return MKACC_OK;
+    });
+}
+
 namespace {
 // host-buffer gate staging: [ct_nand | a1 | a2 | b1 | b2] in, [out_a | out_b] out
 int gate_host(mkacc_ctx* c, const uint32_t* nand, const uint32_t* a1, const uint32_t* b1, const uint32_t* a2,
@@ -2246,6 +2387,220 @@ int mkacc_ntt_inverse_u64(mkacc_ctx* c, const uint64_t* in, uint64_t* out, size_
 }
 int mkacc_sdd_u64(mkacc_ctx* c, const uint64_t* in, uint64_t* out, size_t count) {
     return prim_u64(c, in, out, count, 2);
+}
+
+}  // extern "C"
+
+// ---- multi-device groups (include/mkfhe_amd.h) -------------------------------------
+
+struct mkacc_group {
+    std::vector<mkacc_ctx*> m;
+};
+
+extern "C" void mkacc_shard_range(size_t B, uint32_t parts, uint32_t i, size_t* begin, size_t* end) {
+    // the split of mkfhe_amd/shard.py:shard_range: contiguous, sizes differ by at most one
+    size_t b = 0, e = 0;
+    if (parts && i < parts) {
+        const size_t q = B / parts, r = B % parts;
+        b = (size_t)i * q + std::min<size_t>(i, r);
+        e = b + q + (i < r ? 1 : 0);
+    }
+    if (begin) *begin = b;
+    if (end) *end = e;
+}
+
+namespace {
+
+// dst <- src device buffer (bytes), on dst's stream: a peer copy over xGMI
+// between devices, a device-to-device copy within one device
+int dev_copy(mkacc_ctx* dst, void* d, const mkacc_ctx* src, const void* s, size_t bytes) {
+    if (!bytes) return MKACC_OK;
+    HIP_TRY(hipSetDevice(dst->device));
+    if (dst->device == src->device)
+        HIP_TRY(hipMemcpyAsync(d, s, bytes, hipMemcpyDeviceToDevice, dst->stream));
+    else
+        HIP_TRY(hipMemcpyPeerAsync(d, dst->device, s, src->device, bytes, dst->stream));
+    return MKACC_OK;
+}
+template <typename T>
+int ensure_like(mkacc_ctx* dst, T*& d, size_t words) {
+    if (d) return MKACC_OK;
+    HIP_TRY(hipSetDevice(dst->device));
+    HIP_TRY(hipMalloc(&d, words * sizeof(T)));
+    return MKACC_OK;
+}
+
+// member i > 0 takes member 0's converted keys (device layout) by device copy
+int share_keys(mkacc_ctx* dst, const mkacc_ctx* src) {
+    const size_t kw = (size_t)src->p.k * (src->p.n + 1) * key_block_words(src), pw = (size_t)src->p.k * src->dg * kN;
+    int rc;
+    if (src->wide) {
+        if ((rc = ensure_like(dst, dst->d_wkeys, kw)) || (rc = ensure_like(dst, dst->d_wpkey, pw))) return rc;
+        if ((rc = dev_copy(dst, dst->d_wkeys, src, src->d_wkeys, kw * 8)) ||
+            (rc = dev_copy(dst, dst->d_wpkey, src, src->d_wpkey, pw * 8)))
+            return rc;
+    } else {
+        if ((rc = ensure_like(dst, dst->d_keys, kw)) || (rc = ensure_like(dst, dst->d_pkey, pw))) return rc;
+        if ((rc = dev_copy(dst, dst->d_keys, src, src->d_keys, kw * 4)) ||
+            (rc = dev_copy(dst, dst->d_pkey, src, src->d_pkey, pw * 4)))
+            return rc;
+    }
+    HIP_TRY(hipStreamSynchronize(dst->stream));
+    dst->have_keys = true;
+    return MKACC_OK;
+}
+
+int share_ksk(mkacc_ctx* dst, const mkacc_ctx* src) {
+    dst->ks = src->ks;
+    dst->dks = src->dks;
+    dst->n_pad = src->n_pad;
+    const size_t L = (size_t)src->dks * kN;
+    int rc;
+    if (src->method_class == XZW) {
+        const size_t w = (size_t)src->p.k * L * src->n_pad;
+        if (dst->d_ksk) HIP_TRY(hipFree(dst->d_ksk));
+        dst->d_ksk = nullptr;
+        if ((rc = ensure_like(dst, dst->d_ksk, w)) || (rc = dev_copy(dst, dst->d_ksk, src, src->d_ksk, w * 2)))
+            return rc;
+    } else {
+        const size_t rows = (size_t)src->p.k * kN * src->ks.baseKS * src->dks;
+        if (dst->d_lweA) HIP_TRY(hipFree(dst->d_lweA));
+        if (dst->d_lweB) HIP_TRY(hipFree(dst->d_lweB));
+        dst->d_lweA = dst->d_lweB = nullptr;
+        if ((rc = ensure_like(dst, dst->d_lweA, rows * src->ks.n_out)) || (rc = ensure_like(dst, dst->d_lweB, rows)) ||
+            (rc = dev_copy(dst, dst->d_lweA, src, src->d_lweA, rows * src->ks.n_out * 2)) ||
+            (rc = dev_copy(dst, dst->d_lweB, src, src->d_lweB, rows * 2)))
+            return rc;
+    }
+    HIP_TRY(hipStreamSynchronize(dst->stream));
+    dst->have_ksk = true;
+    return MKACC_OK;
+}
+
+// upload through member 0 (its host-side conversion and checks), then share
+template <class F, class S>
+int group_upload(mkacc_group* g, F&& upload0, S&& share) {
+    if (!g || g->m.empty()) return fail(MKACC_E_ARG, "null group");
+    int rc = upload0(g->m[0]);
+    if (rc) return rc;
+    for (size_t i = 1; i < g->m.size(); ++i) {
+        std::lock_guard<std::mutex> lk(g->m[i]->mu);
+        if ((rc = share(g->m[i], g->m[0]))) return rc;
+    }
+    return MKACC_OK;
+}
+
+// run f(member, begin, count) for every non-empty shard, one host thread per
+// member; the first failure (status and its message) is reported
+template <class F>
+int group_run(mkacc_group* g, size_t B, F&& f) {
+    if (!g || g->m.empty()) return fail(MKACC_E_ARG, "null group");
+    const uint32_t P = (uint32_t)g->m.size();
+    std::vector<int> rcs(P, MKACC_OK);
+    std::vector<std::string> msgs(P);
+    std::vector<std::thread> th;
+    for (uint32_t i = 0; i < P; ++i) {
+        size_t b, e;
+        mkacc_shard_range(B, P, i, &b, &e);
+        if (e == b) continue;
+        th.emplace_back([&, i, b, e] {
+            rcs[i] = f(g->m[i], b, e - b);
+            if (rcs[i]) msgs[i] = mkacc_last_error();
+        });
+    }
+    for (auto& t : th) t.join();
+    for (uint32_t i = 0; i < P; ++i)
+        if (rcs[i]) return fail(rcs[i], "group member " + std::to_string(i) + ": " + msgs[i]);
+    return MKACC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mkacc_group_create(const mkacc_params* p, const int* devices, uint32_t count, mkacc_group** out) {
+    if (!p || !devices || !out || count == 0) return fail(MKACC_E_ARG, "null argument or empty device list");
+    *out = nullptr;
+    auto g = std::make_unique<mkacc_group>();
+    for (uint32_t i = 0; i < count; ++i) {
+        mkacc_ctx* c = nullptr;
+        const int rc = mkacc_create(p, devices[i], &c);
+        if (rc) {
+            const std::string msg = mkacc_last_error();
+            mkacc_group_destroy(g.release());
+            return fail(rc, msg);
+        }
+        g->m.push_back(c);
+    }
+    // direct xGMI access between the member devices where the runtime offers it
+    for (uint32_t i = 0; i < count; ++i)
+        for (uint32_t j = 0; j < count; ++j) {
+            int can = 0;
+            if (devices[i] != devices[j] && hipDeviceCanAccessPeer(&can, devices[i], devices[j]) == hipSuccess && can) {
+                (void)hipSetDevice(devices[i]);
+                (void)hipDeviceEnablePeerAccess(devices[j], 0);   // "already enabled" is fine
+                (void)hipGetLastError();
+            }
+        }
+    *out = g.release();
+    return MKACC_OK;
+}
+
+void mkacc_group_destroy(mkacc_group* g) {
+    if (!g) return;
+    for (mkacc_ctx* c : g->m) mkacc_destroy(c);
+    delete g;
+}
+
+uint32_t mkacc_group_size(const mkacc_group* g) { return g ? (uint32_t)g->m.size() : 0; }
+
+mkacc_ctx* mkacc_group_member(mkacc_group* g, uint32_t i) { return g && i < g->m.size() ? g->m[i] : nullptr; }
+
+int mkacc_group_upload_keys(mkacc_group* g, const uint32_t* evk, const uint32_t* pkey) {
+    return group_upload(g, [&](mkacc_ctx* c) { return mkacc_upload_keys(c, evk, pkey); }, share_keys);
+}
+int mkacc_group_upload_keys_u64(mkacc_group* g, const uint64_t* evk, const uint64_t* pkey) {
+    return group_upload(g, [&](mkacc_ctx* c) { return mkacc_upload_keys_u64(c, evk, pkey); }, share_keys);
+}
+int mkacc_group_upload_ksk_mntru(mkacc_group* g, const mkacc_ks_params* ks, const uint32_t* ksk) {
+    return group_upload(g, [&](mkacc_ctx* c) { return mkacc_upload_ksk_mntru(c, ks, ksk); }, share_ksk);
+}
+int mkacc_group_upload_ksk_mklwe(mkacc_group* g, const mkacc_ks_params* ks, const uint32_t* A, const uint32_t* B) {
+    return group_upload(g, [&](mkacc_ctx* c) { return mkacc_upload_ksk_mklwe(c, ks, A, B); }, share_ksk);
+}
+
+int mkacc_group_eval_batch(mkacc_group* g, const uint32_t* ct, const uint32_t* acc_in, uint32_t* acc_out, size_t B) {
+    if (!g || g->m.empty() || !ct || !acc_in || !acc_out) return fail(MKACC_E_ARG, "null argument");
+    const size_t ctw = (size_t)g->m[0]->p.k * g->m[0]->p.n, accw = (size_t)g->m[0]->p.k * kN;
+    return group_run(g, B, [&](mkacc_ctx* c, size_t b, size_t cnt) {
+        return mkacc_eval_batch(c, ct + b * ctw, acc_in + b * accw, acc_out + b * accw, cnt);
+    });
+}
+int mkacc_group_eval_batch_u64(mkacc_group* g, const uint32_t* ct, const uint64_t* acc_in, uint64_t* acc_out,
+                               size_t B) {
+    if (!g || g->m.empty() || !ct || !acc_in || !acc_out) return fail(MKACC_E_ARG, "null argument");
+    const size_t ctw = (size_t)g->m[0]->p.k * g->m[0]->p.n, accw = (size_t)g->m[0]->p.k * kN;
+    return group_run(g, B, [&](mkacc_ctx* c, size_t b, size_t cnt) {
+        return mkacc_eval_batch_u64(c, ct + b * ctw, acc_in + b * accw, acc_out + b * accw, cnt);
+    });
+}
+int mkacc_group_eval_nand_mntru(mkacc_group* g, const uint32_t* ct_nand, const uint32_t* ct1, const uint32_t* ct2,
+                                uint32_t* out, size_t B) {
+    if (!g || g->m.empty() || !ct_nand || !ct1 || !ct2 || !out) return fail(MKACC_E_ARG, "null argument");
+    if (ct1 == ct2) return fail(MKACC_E_ARG, "Input ciphertexts should be independant");
+    const size_t kn = (size_t)g->m[0]->p.k * g->m[0]->p.n, kno = (size_t)g->m[0]->p.k * g->m[0]->ks.n_out;
+    return group_run(g, B, [&](mkacc_ctx* c, size_t b, size_t cnt) {
+        return mkacc_eval_nand_mntru(c, ct_nand, ct1 + b * kn, ct2 + b * kn, out + b * kno, cnt);
+    });
+}
+int mkacc_group_eval_nand_mklwe(mkacc_group* g, const uint32_t* a1, const uint32_t* b1, const uint32_t* a2,
+                                const uint32_t* b2, uint32_t* out_a, uint32_t* out_b, size_t B) {
+    if (!g || g->m.empty() || !a1 || !b1 || !a2 || !b2 || !out_a || !out_b) return fail(MKACC_E_ARG, "null argument");
+    if (a1 == a2) return fail(MKACC_E_ARG, "Input ciphertexts should be independant");
+    const size_t kn = (size_t)g->m[0]->p.k * g->m[0]->p.n, kno = (size_t)g->m[0]->p.k * g->m[0]->ks.n_out;
+    return group_run(g, B, [&](mkacc_ctx* c, size_t b, size_t cnt) {
+        return mkacc_eval_nand_mklwe(c, a1 + b * kn, b1 + b, a2 + b * kn, b2 + b, out_a + b * kno, out_b + b, cnt);
+    });
 }
 
 }  // extern "C"

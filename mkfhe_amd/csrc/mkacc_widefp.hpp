@@ -346,9 +346,18 @@ __global__ __launch_bounds__(kThreads, MKACC_WFP_WG_PER_CU) void step_kernel(Ste
 }
 
 // batch prologue / epilogue: canonical u64 words <-> balanced doubles
-__global__ void to_balanced_kernel(const uint64_t* __restrict__ in, double* __restrict__ out, size_t count, FMod m) {
+// device entry point: a word >= Q raises `bad` (mkacc_sync reports MKACC_E_RANGE)
+// and is replaced by 0, so every value stays inside the exactness bounds
+__global__ void to_balanced_kernel(const uint64_t* __restrict__ in, double* __restrict__ out, size_t count, FMod m,
+                                   uint64_t Q, uint32_t* __restrict__ bad) {
     const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx < count) out[idx] = balanced(in[idx], m);
+    if (idx >= count) return;
+    uint64_t x = in[idx];
+    if (x >= Q) {
+        *bad = 1u;
+        x = 0;
+    }
+    out[idx] = balanced(x, m);
 }
 __global__ void to_canonical_kernel(const double* __restrict__ in, uint64_t* __restrict__ out, size_t count, FMod m) {
     const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;

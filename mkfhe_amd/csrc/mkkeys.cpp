@@ -17,6 +17,8 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <exception>
+#include <mutex>
 #include <random>
 #include <stdexcept>
 #include <string>
@@ -39,9 +41,15 @@ int fail(int code, const std::string& msg) {
 // ---------------------------------------------------------------------------
 // randomness.  seed != 0 (tests, reproducible runs): xoshiro256** streams keyed by
 // SplitMix64(seed, stream ids) -- fast, not cryptographic.  seed == 0 (the
-// reference's behaviour: fresh keys every call): ChaCha20 keyed with 256 bits
-// from std::random_device, one stream per (a, b, c) id in the nonce, so no
-// secret is a function of a short seed.
+// reference's behaviour: fresh keys every call): ChaCha20 with a 256-bit call
+// key, one stream per (a, b, c) id in the nonce, so no secret is a function of
+// a short seed.  The call keys come from the process's entropy journal: a
+// 256-bit master key (MKFHE_ENTROPY, 64 hex digits, or std::random_device when
+// first needed) and a counter of seed-0 calls; call key = ChaCha20 block of the
+// master at nonce = counter.  mkkg_entropy_get reports the master, so a run
+// whose gates decrypt wrong can be replayed exactly (mkkg_entropy_set or
+// MKFHE_ENTROPY) -- the reference's clock-seeded keys (binfhe-base-scheme.cpp:111,
+// mntru-pke.cpp:27) cannot be.
 // ---------------------------------------------------------------------------
 inline uint64_t splitmix(uint64_t& x) {
     uint64_t z = (x += 0x9E3779B97F4A7C15ull);
@@ -56,14 +64,63 @@ struct Seed {
     uint32_t key[8] = {};
 };
 
+struct ChaCha20;
+void chacha_block(const uint32_t key[8], uint32_t n0, uint32_t n1, uint32_t out[16]);
+
+struct Entropy {
+    std::mutex mu;
+    bool init = false;
+    uint32_t master[8] = {};
+    uint64_t calls = 0;
+};
+Entropy& entropy() {
+    static Entropy e;
+    return e;
+}
+bool parse_hex256(const char* h, uint32_t out[8]) {
+    if (!h || std::strlen(h) != 64) return false;
+    for (int i = 0; i < 8; ++i) {
+        uint32_t w = 0;
+        for (int j = 0; j < 8; ++j) {
+            const char ch = h[8 * i + j];
+            const int v = ch >= '0' && ch <= '9' ? ch - '0' : ch >= 'a' && ch <= 'f' ? ch - 'a' + 10
+                        : ch >= 'A' && ch <= 'F' ? ch - 'A' + 10 : -1;
+            if (v < 0) return false;
+            w = (w << 4) | (uint32_t)v;
+        }
+        out[i] = w;
+    }
+    return true;
+}
+// caller holds e.mu
+void entropy_init_locked(Entropy& e) {
+    if (e.init) return;
+    if (!parse_hex256(std::getenv("MKFHE_ENTROPY"), e.master)) {
+        std::random_device rd;
+        for (auto& w : e.master) w = rd();
+    }
+    e.calls = 0;
+    e.init = true;
+}
+
 Seed resolve_seed(uint64_t seed) {
     Seed r;
     if (seed) {
         r.s = seed;
         return r;
     }
-    std::random_device rd;
-    for (auto& w : r.key) w = rd();
+    Entropy& e = entropy();
+    uint64_t call;
+    uint32_t master[8];
+    {
+        std::lock_guard<std::mutex> lk(e.mu);
+        entropy_init_locked(e);
+        call = e.calls++;
+        std::memcpy(master, e.master, sizeof master);
+    }
+    uint32_t blk[16];
+    chacha_block(master, (uint32_t)call, (uint32_t)(call >> 32) | 0x80000000u, blk);
+    std::memcpy(r.key, blk, sizeof r.key);
     r.secure = true;
     return r;
 }
@@ -108,6 +165,11 @@ struct ChaCha20 {
         return v;
     }
 };
+void chacha_block(const uint32_t key[8], uint32_t n0, uint32_t n1, uint32_t out[16]) {
+    ChaCha20 c(key, n0, n1);
+    c.refill();
+    std::memcpy(out, c.buf, 16 * sizeof(uint32_t));
+}
 
 struct Rng {
     uint64_t s[4];
@@ -180,6 +242,9 @@ struct Dgg {
     }
 };
 
+// encryptions per call: the item index is the 24-bit stream id b of Rng
+constexpr size_t kMaxPerCall = (size_t)1 << 24;
+
 inline uint32_t to_mod(int64_t v, uint64_t m) {
     int64_t r = v % (int64_t)m;
     return (uint32_t)(r < 0 ? r + (int64_t)m : r);
@@ -211,11 +276,20 @@ void parallel_for(size_t n, F&& f) {
     }
     std::atomic<size_t> next{0};
     std::vector<std::thread> th;
+    std::exception_ptr err;
+    std::mutex emu;
     for (unsigned t = 0; t < T; ++t)
         th.emplace_back([&] {
-            for (size_t i; (i = next.fetch_add(1)) < n;) f(i);
+            try {
+                for (size_t i; (i = next.fetch_add(1)) < n;) f(i);
+            } catch (...) {   // an exception must not leave a worker thread (std::terminate)
+                std::lock_guard<std::mutex> lk(emu);
+                if (!err) err = std::current_exception();
+                next = n;
+            }
         });
     for (auto& t : th) t.join();
+    if (err) std::rethrow_exception(err);
 }
 
 // ---------------------------------------------------------------------------
@@ -416,9 +490,52 @@ void unienc_key(const P& p, const Ring& R, const Dgg& dgg, const Dgg& dggR, Rng&
 extern "C" {
 
 int mkkg_abi_version(void) { return MKKG_ABI_VERSION; }
+
+#ifndef MKKG_HEADER_ID
+#define MKKG_HEADER_ID "unknown"
+#endif
+#ifndef MKKG_SOURCE_ID
+#define MKKG_SOURCE_ID "unknown"
+#endif
+#ifndef MKKG_BUILD_FLAGS
+#define MKKG_BUILD_FLAGS ""
+#endif
+const char* mkkg_build_info(void) {
+    static const std::string info = "abi=" + std::to_string(MKKG_ABI_VERSION) +
+                                    ";header=" MKKG_HEADER_ID ";source=" MKKG_SOURCE_ID ";flags=" MKKG_BUILD_FLAGS;
+    return info.c_str();
+}
+
+int mkkg_entropy_get(uint32_t master[8], uint64_t* calls) try {
+    if (!master) return fail(MKACC_E_ARG, "null argument");
+    Entropy& e = entropy();
+    std::lock_guard<std::mutex> lk(e.mu);
+    entropy_init_locked(e);
+    std::memcpy(master, e.master, sizeof e.master);
+    if (calls) *calls = e.calls;
+    return MKACC_OK;
+} catch (const std::exception& e) {
+    return fail(MKACC_E_ARG, std::string("mkkg_entropy_get: ") + e.what());
+}
+
+int mkkg_entropy_set(const uint32_t master[8], uint64_t calls) try {
+    Entropy& e = entropy();
+    std::lock_guard<std::mutex> lk(e.mu);
+    if (master) {
+        std::memcpy(e.master, master, sizeof e.master);
+    } else {
+        std::random_device rd;
+        for (auto& w : e.master) w = rd();
+    }
+    e.calls = calls;
+    e.init = true;
+    return MKACC_OK;
+} catch (const std::exception& e) {
+    return fail(MKACC_E_ARG, std::string("mkkg_entropy_set: ") + e.what());
+}
 const char* mkkg_last_error(void) { return g_err.c_str(); }
 
-int mkkg_paramset(const char* name, uint32_t method, mkkg_params* out) {
+int mkkg_paramset(const char* name, uint32_t method, mkkg_params* out) try {
     if (!name || !out) return fail(MKACC_E_ARG, "null argument");
     const ParamRow* row = find_paramset(name);
     if (!row) return fail(MKACC_E_ARG, std::string("unknown parameter set ") + name);
@@ -445,6 +562,8 @@ int mkkg_paramset(const char* name, uint32_t method, mkkg_params* out) {
     p.ring_keydist = method == MKACC_METHOD_MKNTRU_LWE ? MKKG_DIST_TERNARY : MKKG_DIST_GAUSSIAN;
     *out = p;
     return MKACC_OK;
+} catch (const std::exception& e) {
+    return fail(MKACC_E_ARG, std::string("mkkg_paramset: ") + e.what());
 }
 
 size_t mkkg_evk_words(const mkkg_params* pp) {
@@ -476,7 +595,7 @@ size_t mkkg_ksk_mklwe_b_words(const mkkg_params* pp) {
 // MNTRUEncryptionScheme::KeyGen / KeyGenGaussian (mntru-pke.cpp:124-156) with
 // Get_invertible_Matrix (:19-106): entries uniform ternary, or N(0,1) assigned
 // to a ZZ_p (truncated toward zero); resampled until invertible mod qKS.
-int mkkg_mntru_keygen(const mkkg_params* pp, uint64_t seed, uint32_t* F, uint32_t* Finv) {
+int mkkg_mntru_keygen(const mkkg_params* pp, uint64_t seed, uint32_t* F, uint32_t* Finv) try {
     UNPACK(pp, p);
     if (!F || !Finv) return fail(MKACC_E_ARG, "null output");
     const Seed sd = resolve_seed(seed);
@@ -496,10 +615,12 @@ int mkkg_mntru_keygen(const mkkg_params* pp, uint64_t seed, uint32_t* F, uint32_
         std::memcpy(Finv + (size_t)u * n * n, Mi.data(), Mi.size() * 4);
     }
     return MKACC_OK;
+} catch (const std::exception& e) {
+    return fail(MKACC_E_ARG, std::string("mkkg_mntru_keygen: ") + e.what());
 }
 
 // MKLWEEncryptionScheme::KeyGenBinary (mklwe-pke.cpp:19-34)
-int mkkg_mklwe_keygen(const mkkg_params* pp, uint64_t seed, uint32_t* s) {
+int mkkg_mklwe_keygen(const mkkg_params* pp, uint64_t seed, uint32_t* s) try {
     UNPACK(pp, p);
     if (!s) return fail(MKACC_E_ARG, "null output");
     const Seed sd = resolve_seed(seed);
@@ -508,10 +629,12 @@ int mkkg_mklwe_keygen(const mkkg_params* pp, uint64_t seed, uint32_t* s) {
         for (uint32_t i = 0; i < p.n; ++i) s[(size_t)u * p.n + i] = (uint32_t)r.binary();
     }
     return MKACC_OK;
+} catch (const std::exception& e) {
+    return fail(MKACC_E_ARG, std::string("mkkg_mklwe_keygen: ") + e.what());
 }
 
 // m_CRS = dg polys NativePoly(m_dgg, COEFFICIENT) -> EVALUATION (mk-cryptoparameters.h:173-178)
-int mkkg_crs(const mkkg_params* pp, uint64_t seed, uint32_t* crs) {
+int mkkg_crs(const mkkg_params* pp, uint64_t seed, uint32_t* crs) try {
     UNPACK(pp, p);
     if (!crs) return fail(MKACC_E_ARG, "null output");
     const Seed sd = resolve_seed(seed);
@@ -522,13 +645,15 @@ int mkkg_crs(const mkkg_params* pp, uint64_t seed, uint32_t* crs) {
         sample_poly_eval(R, g, r, crs + (size_t)i * p.N);
     }
     return MKACC_OK;
+} catch (const std::exception& e) {
+    return fail(MKACC_E_ARG, std::string("mkkg_crs: ") + e.what());
 }
 
 // Get_invertible_NativeVector (binfhe-base-scheme.cpp:104-195): coefficients
 // from N(0, 0.5) assigned to ZZ_p (truncated; GAUSSIAN) or uniform ternary,
 // resampled until s is a unit mod (X^N+1, Q).
 int mkkg_ring_secrets(const mkkg_params* pp, uint64_t seed, uint32_t* skN, uint32_t* skN_eval,
-                      uint32_t* skNinv_eval) {
+                      uint32_t* skNinv_eval) try {
     UNPACK(pp, p);
     if (!skN || !skN_eval || !skNinv_eval) return fail(MKACC_E_ARG, "null output");
     const Seed sd = resolve_seed(seed);
@@ -552,10 +677,12 @@ int mkkg_ring_secrets(const mkkg_params* pp, uint64_t seed, uint32_t* skN, uint3
         for (uint32_t j = 0; j < N; ++j) skNinv_eval[(size_t)u * N + j] = (uint32_t)modinv(e[j], p.Q);
     }
     return MKACC_OK;
+} catch (const std::exception& e) {
+    return fail(MKACC_E_ARG, std::string("mkkg_ring_secrets: ") + e.what());
 }
 
 // Pkey[u][i] = e_i - CRS[i] * s_u, e_i <- NTT(m_dgg) (binfhe-base-scheme.cpp:255-268)
-int mkkg_pkey(const mkkg_params* pp, uint64_t seed, const uint32_t* crs, const uint32_t* skN_eval, uint32_t* pkey) {
+int mkkg_pkey(const mkkg_params* pp, uint64_t seed, const uint32_t* crs, const uint32_t* skN_eval, uint32_t* pkey) try {
     UNPACK(pp, p);
     if (!crs || !skN_eval || !pkey) return fail(MKACC_E_ARG, "null argument");
     const Seed sd = resolve_seed(seed);
@@ -574,6 +701,8 @@ int mkkg_pkey(const mkkg_params* pp, uint64_t seed, const uint32_t* crs, const u
             }
         }
     return MKACC_OK;
+} catch (const std::exception& e) {
+    return fail(MKACC_E_ARG, std::string("mkkg_pkey: ") + e.what());
 }
 
 // KeyGenAcc (mk-acc-xzw.cpp:38-87 / mk-acc-xzw_B.cpp:38-101):
@@ -581,7 +710,7 @@ int mkkg_pkey(const mkkg_params* pp, uint64_t seed, const uint32_t* crs, const u
 //          is KDM, plus ek[0][0][n] = KDM-Enc(1).  Unset slots are zero.
 //   XZW_B: ek[u][0][i] = Enc(s == 1); slot (0,0) KDM, ek[0][0][n] = KDM-Enc(1).
 int mkkg_acc_keygen(const mkkg_params* pp, uint64_t seed, const uint32_t* crs, const uint32_t* skNinv_eval,
-                    const uint32_t* lwe_sk, uint32_t* evk) {
+                    const uint32_t* lwe_sk, uint32_t* evk) try {
     UNPACK(pp, p);
     if (!crs || !skNinv_eval || !lwe_sk || !evk) return fail(MKACC_E_ARG, "null argument");
     const Seed sd = resolve_seed(seed);
@@ -615,6 +744,8 @@ int mkkg_acc_keygen(const mkkg_params* pp, uint64_t seed, const uint32_t* crs, c
         unienc_key(p, R, dgg, dggR, r, crs, sinv, m, kdm, out);
     });
     return MKACC_OK;
+} catch (const std::exception& e) {
+    return fail(MKACC_E_ARG, std::string("mkkg_acc_keygen: ") + e.what());
 }
 
 // KeySwitchGen2 (mntru-pke.cpp:624-760), the j = 1 table KSK2[u][1] = KSK[u]:
@@ -628,7 +759,7 @@ int mkkg_acc_keygen(const mkkg_params* pp, uint64_t seed, const uint32_t* crs, c
 // set decrypts at random.  Each row gets its own noise vector here.  The key's
 // shape, its decryption relation and the KeySwitch2 that consumes it are the
 // reference's.
-int mkkg_ksk_mntru(const mkkg_params* pp, uint64_t seed, const uint32_t* skN, const uint32_t* Finv, uint32_t* ksk) {
+int mkkg_ksk_mntru(const mkkg_params* pp, uint64_t seed, const uint32_t* skN, const uint32_t* Finv, uint32_t* ksk) try {
     UNPACK(pp, p);
     if (!skN || !Finv || !ksk) return fail(MKACC_E_ARG, "null argument");
     const Seed sd = resolve_seed(seed);
@@ -665,12 +796,14 @@ int mkkg_ksk_mntru(const mkkg_params* pp, uint64_t seed, const uint32_t* skN, co
         });
     }
     return MKACC_OK;
+} catch (const std::exception& e) {
+    return fail(MKACC_E_ARG, std::string("mkkg_ksk_mntru: ") + e.what());
 }
 
 // MKLWEEncryptionScheme::KeySwitchGen (mklwe-pke.cpp:176-258):
 //   A[u][i][j][t] <- dgg(sigma)^n,  B = dggKS + svN[i] * j * baseKS^t + <A, s_u>  (mod qKS)
 int mkkg_ksk_mklwe(const mkkg_params* pp, uint64_t seed, const uint32_t* skN, const uint32_t* s, uint32_t* A,
-                   uint32_t* B) {
+                   uint32_t* B) try {
     UNPACK(pp, p);
     if (!skN || !s || !A || !B) return fail(MKACC_E_ARG, "null argument");
     const Seed sd = resolve_seed(seed);
@@ -699,6 +832,8 @@ int mkkg_ksk_mklwe(const mkkg_params* pp, uint64_t seed, const uint32_t* skN, co
         }
     });
     return MKACC_OK;
+} catch (const std::exception& e) {
+    return fail(MKACC_E_ARG, std::string("mkkg_ksk_mklwe: ") + e.what());
 }
 
 namespace {
@@ -726,10 +861,11 @@ void mntru_encrypt_one(const P& p, const Dgg& dgg, Rng& r, const uint32_t* Finv,
 
 // MNTRUEncryptionScheme::Encrypt (mntru-pke.cpp:158-206): e[0] += (m % p) * (q / p)
 int mkkg_mntru_encrypt(const mkkg_params* pp, uint64_t seed, const uint32_t* Finv, const uint32_t* m, uint32_t pt,
-                       size_t count, uint32_t* ct) {
+                       size_t count, uint32_t* ct) try {
     UNPACK(pp, p);
     if (!Finv || !m || !ct) return fail(MKACC_E_ARG, "null argument");
     if (pt < 2) return fail(MKACC_E_ARG, "plaintext modulus must be >= 2");
+    if (count >= kMaxPerCall) return fail(MKACC_E_ARG, "at most 2^24 - 1 encryptions per call");
     const Seed sd = resolve_seed(seed);
     const Dgg dgg(pp->sigma);
     parallel_for(count, [&](size_t c) {
@@ -738,10 +874,12 @@ int mkkg_mntru_encrypt(const mkkg_params* pp, uint64_t seed, const uint32_t* Fin
         mntru_encrypt_one(p, dgg, r, Finv, delta, ct + c * p.k * p.n);
     });
     return MKACC_OK;
+} catch (const std::exception& e) {
+    return fail(MKACC_E_ARG, std::string("mkkg_mntru_encrypt: ") + e.what());
 }
 
 // ctGateGen(sk, NAND) (binfhe-base-scheme.cpp:340-376): e[0] += 5q/8
-int mkkg_mntru_ctgate(const mkkg_params* pp, uint64_t seed, const uint32_t* Finv, uint32_t* ct_nand) {
+int mkkg_mntru_ctgate(const mkkg_params* pp, uint64_t seed, const uint32_t* Finv, uint32_t* ct_nand) try {
     UNPACK(pp, p);
     if (!Finv || !ct_nand) return fail(MKACC_E_ARG, "null argument");
     const Seed sd = resolve_seed(seed);
@@ -749,12 +887,14 @@ int mkkg_mntru_ctgate(const mkkg_params* pp, uint64_t seed, const uint32_t* Finv
     Rng r(sd, 10);
     mntru_encrypt_one(p, dgg, r, Finv, (uint32_t)(5 * p.q / 8), ct_nand);
     return MKACC_OK;
+} catch (const std::exception& e) {
+    return fail(MKACC_E_ARG, std::string("mkkg_mntru_ctgate: ") + e.what());
 }
 
 // Decrypt / Decrypt2 / DecryptNAND (mntru-pke.cpp:208-357):
 //   inner = sum_u <c_u, F_u[:,0]> mod q, then the variant's offset and scale.
 int mkkg_mntru_decrypt(const mkkg_params* pp, const uint32_t* F, const uint32_t* ct, uint64_t mod, uint32_t pt,
-                       uint32_t variant, size_t count, uint32_t* m) {
+                       uint32_t variant, size_t count, uint32_t* m) try {
     UNPACK(pp, p);
     if (!F || !ct || !m) return fail(MKACC_E_ARG, "null argument");
     if (pt < 2 || variant > MKKG_DECRYPT_NAND) return fail(MKACC_E_ARG, "bad plaintext modulus or variant");
@@ -778,15 +918,18 @@ int mkkg_mntru_decrypt(const mkkg_params* pp, const uint32_t* F, const uint32_t*
         m[c] = (uint32_t)(scale * inner / mod);
     }
     return MKACC_OK;
+} catch (const std::exception& e) {
+    return fail(MKACC_E_ARG, std::string("mkkg_mntru_decrypt: ") + e.what());
 }
 
 // MKLWEEncryptionScheme::Encrypt (mklwe-pke.cpp:36-64): a_u <- DGG(sigma = 1)
 // (a default-constructed generator), b = (m % p)(q/p) + dgg(sigma) + sum <a_u, s_u>
 int mkkg_mklwe_encrypt(const mkkg_params* pp, uint64_t seed, const uint32_t* s, const uint32_t* m, uint32_t pt,
-                       size_t count, uint32_t* a, uint32_t* b) {
+                       size_t count, uint32_t* a, uint32_t* b) try {
     UNPACK(pp, p);
     if (!s || !m || !a || !b) return fail(MKACC_E_ARG, "null argument");
     if (pt < 2) return fail(MKACC_E_ARG, "plaintext modulus must be >= 2");
+    if (count >= kMaxPerCall) return fail(MKACC_E_ARG, "at most 2^24 - 1 encryptions per call");
     const Seed sd = resolve_seed(seed);
     const Dgg err(pp->sigma), dga(1.0);
     const uint64_t q = p.q;
@@ -802,12 +945,14 @@ int mkkg_mklwe_encrypt(const mkkg_params* pp, uint64_t seed, const uint32_t* s, 
         b[c] = to_mod(bb, q);
     });
     return MKACC_OK;
+} catch (const std::exception& e) {
+    return fail(MKACC_E_ARG, std::string("mkkg_mklwe_encrypt: ") + e.what());
 }
 
 // Decrypt (mklwe-pke.cpp:66-113): r = b - sum <a_u, s_u> + q/(2p); floor(p r / q)
 // DecryptNAND (:115-158):          r = b - sum <a_u, s_u> + q/p;     floor(p/2 r / q)
 int mkkg_mklwe_decrypt(const mkkg_params* pp, const uint32_t* s, const uint32_t* a, const uint32_t* b, uint64_t mod,
-                       uint32_t pt, uint32_t variant, size_t count, uint32_t* m) {
+                       uint32_t pt, uint32_t variant, size_t count, uint32_t* m) try {
     UNPACK(pp, p);
     if (!s || !a || !b || !m) return fail(MKACC_E_ARG, "null argument");
     if (pt < 2 || (variant != MKKG_DECRYPT && variant != MKKG_DECRYPT_NAND))
@@ -830,6 +975,8 @@ int mkkg_mklwe_decrypt(const mkkg_params* pp, const uint32_t* s, const uint32_t*
         }
     }
     return MKACC_OK;
+} catch (const std::exception& e) {
+    return fail(MKACC_E_ARG, std::string("mkkg_mklwe_decrypt: ") + e.what());
 }
 
 }  // extern "C"
@@ -922,7 +1069,7 @@ int seek_section(File& fl, const char* name, uint64_t* words) {
 extern "C" {
 
 int mkkg_file_write(const char* path, uint32_t kind, const mkkg_params* p, const mkkg_section* sections,
-                    uint32_t count) {
+                    uint32_t count) try {
     if (!path || !p || (count && !sections)) return fail(MKACC_E_ARG, "null argument");
     File fl(path, "wb");
     if (!fl.f) return fail(MKACC_E_ARG, std::string("cannot create ") + path);
@@ -940,11 +1087,15 @@ int mkkg_file_write(const char* path, uint32_t kind, const mkkg_params* p, const
     }
     if (!ok) return fail(MKACC_E_ARG, std::string("write failed: ") + path);
     return MKACC_OK;
+} catch (const std::exception& e) {
+    return fail(MKACC_E_ARG, std::string("mkkg_file_write: ") + e.what());
 }
 
-int mkkg_file_info(const char* path, uint32_t* kind, mkkg_params* p, uint32_t* count) {
+int mkkg_file_info(const char* path, uint32_t* kind, mkkg_params* p, uint32_t* count) try {
     File fl(path, "rb");
     return read_header(fl, kind, p, count);
+} catch (const std::exception& e) {
+    return fail(MKACC_E_ARG, std::string("mkkg_file_info: ") + e.what());
 }
 
 uint64_t mkkg_file_section_words(const char* path, const char* name) {
@@ -954,7 +1105,7 @@ uint64_t mkkg_file_section_words(const char* path, const char* name) {
     return seek_section(fl, name, &w) ? 0 : w;
 }
 
-int mkkg_file_read_section(const char* path, const char* name, uint32_t* out, uint64_t words) {
+int mkkg_file_read_section(const char* path, const char* name, uint32_t* out, uint64_t words) try {
     if (!name || (words && !out)) return fail(MKACC_E_ARG, "null argument");
     File fl(path, "rb");
     uint64_t w = 0;
@@ -965,9 +1116,11 @@ int mkkg_file_read_section(const char* path, const char* name, uint32_t* out, ui
     if (!fl.get(out, words * 4) || !fl.get(&h, 8)) return fail(MKACC_E_ARG, "truncated key file");
     if (h != fnv1a(out, words * 4)) return fail(MKACC_E_ARG, std::string("checksum mismatch in section ") + name);
     return MKACC_OK;
+} catch (const std::exception& e) {
+    return fail(MKACC_E_ARG, std::string("mkkg_file_read_section: ") + e.what());
 }
 
-int mkkg_ntt_forward(const mkkg_params* pp, const uint32_t* in, uint32_t* out, size_t count) {
+int mkkg_ntt_forward(const mkkg_params* pp, const uint32_t* in, uint32_t* out, size_t count) try {
     UNPACK(pp, p);
     if (!in || !out) return fail(MKACC_E_ARG, "null argument");
     const Ring R(p.N, p.Q, p.root);
@@ -980,9 +1133,11 @@ int mkkg_ntt_forward(const mkkg_params* pp, const uint32_t* in, uint32_t* out, s
         R.fwd(o);
     }
     return MKACC_OK;
+} catch (const std::exception& e) {
+    return fail(MKACC_E_ARG, std::string("mkkg_ntt_forward: ") + e.what());
 }
 
-int mkkg_ntt_inverse(const mkkg_params* pp, const uint32_t* in, uint32_t* out, size_t count) {
+int mkkg_ntt_inverse(const mkkg_params* pp, const uint32_t* in, uint32_t* out, size_t count) try {
     UNPACK(pp, p);
     if (!in || !out) return fail(MKACC_E_ARG, "null argument");
     const Ring R(p.N, p.Q, p.root);
@@ -995,6 +1150,8 @@ int mkkg_ntt_inverse(const mkkg_params* pp, const uint32_t* in, uint32_t* out, s
         R.inv(o);
     }
     return MKACC_OK;
+} catch (const std::exception& e) {
+    return fail(MKACC_E_ARG, std::string("mkkg_ntt_inverse: ") + e.what());
 }
 
 }  // extern "C"

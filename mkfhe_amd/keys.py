@@ -70,26 +70,58 @@ SIGNATURES = {
     "mkkg_file_read_section": (_int, [ctypes.c_char_p, ctypes.c_char_p, _u32p, _u64]),
     "mkkg_ntt_forward": (_int, [_pp, _u32p, _u32p, _sz]),
     "mkkg_ntt_inverse": (_int, [_pp, _u32p, _u32p, _sz]),
+    "mkkg_entropy_get": (_int, [_u32p, ctypes.POINTER(_u64)]),
+    "mkkg_entropy_set": (_int, [_u32p, _u64]),
     "mkkg_last_error": (ctypes.c_char_p, []),
     "mkkg_abi_version": (_int, []),
+    "mkkg_build_info": (ctypes.c_char_p, []),
 }
 
 _lib = None
 
 
 def load():
-    """Load libmkfhe_keys.so (raises if it has not been built)."""
+    """Load libmkfhe_keys.so (raises if it has not been built, or was built from another tree)."""
     global _lib
     if _lib is None:
+        from . import build as _build
+        from ._lib import DEFAULT_LIB_PATH, LibraryMismatch, verify_build
         if not os.path.exists(KEYS_LIB_PATH):
             raise RuntimeError(f"{KEYS_LIB_PATH} not found: build it first (python -m mkfhe_amd.build)")
         L = ctypes.CDLL(KEYS_LIB_PATH)
+        if not hasattr(L, "mkkg_build_info"):
+            raise LibraryMismatch(f"refusing {KEYS_LIB_PATH}: no mkkg_build_info (a library older than ABI 2)")
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
+        default = os.path.realpath(KEYS_LIB_PATH) == os.path.realpath(
+            os.path.join(os.path.dirname(DEFAULT_LIB_PATH), "libmkfhe_keys.so"))
+        L.build_info = verify_build(KEYS_LIB_PATH, L.mkkg_build_info().decode(), L.mkkg_abi_version(),
+                                    _build.KEYS_HEADER, _build.keys_ids(), default)
         _lib = L
     return _lib
+
+
+# ---- seed-0 entropy journal (mkkg_entropy_get / _set) -------------------------------------
+
+def entropy_get() -> tuple[str, int]:
+    """(master key as 64 hex digits = MKFHE_ENTROPY, seed-0 calls since it was set)"""
+    m = np.zeros(8, np.uint32)
+    calls = _u64()
+    _check(load().mkkg_entropy_get(_p(m), ctypes.byref(calls)))
+    return "".join(f"{int(w):08x}" for w in m), calls.value
+
+
+def entropy_set(master_hex: str | None, calls: int = 0):
+    """Restart the journal at (master, calls); None draws a fresh master from std::random_device."""
+    if master_hex is None:
+        _check(load().mkkg_entropy_set(None, calls))
+        return
+    if len(master_hex) != 64:
+        raise ValueError("master key: 64 hex digits")
+    m = np.array([int(master_hex[8 * i:8 * i + 8], 16) for i in range(8)], np.uint32)
+    _check(load().mkkg_entropy_set(_p(m), calls))
 
 
 def _check(rc: int):

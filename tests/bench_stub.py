@@ -41,10 +41,8 @@ class StubEngine:
         assert d_evk.numel() == int(np.prod(self.evk_shape)) and d_pkey.numel() == int(np.prod(self.pkey_shape))
         self.kd = int((d_evk.to(torch.int64).sum() + d_pkey.to(torch.int64).sum()).item() % Q)
 
-    def upload_ksk_mntru(self, ksk, qKS, baseKS, n_out):
-        self.ks = (qKS, baseKS, n_out)
-
-    def upload_ksk_mklwe(self, A, B, qKS, baseKS, n_out):
+    def upload_ksk_device(self, qKS, baseKS, n_out, d_ksk=None, d_A=None, d_B=None):
+        assert (d_ksk is not None) != (d_A is not None and d_B is not None)
         self.ks = (qKS, baseKS, n_out)
 
     def ntt_forward(self, a):

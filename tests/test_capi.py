@@ -36,7 +36,7 @@ def test_python_binding_covers_header():
 
 
 def test_abi_version(lib):
-    assert lib.mkacc_abi_version() == 1
+    assert lib.mkacc_abi_version() == 2
 
 
 @pytest.mark.parametrize("name,k,n,q,logB,dg", [

@@ -182,3 +182,85 @@ def test_bench_shape_b4096_full_n(mk, oracle):
     assert not bad, f"{len(bad)} gates differ from the oracle, first {bad[:16]}"
     assert make_golden.digest(r1) == g["sha256"]
     assert np.array_equal(r1, r2)
+
+
+@pytest.mark.parametrize("ps,method", [("STD100_MKNTRU", 0), ("STD100_MKNTRU_LWE", 2)])
+def test_upload_ksk_device_matches_host_upload(mk, ps, method):
+    """mkacc_upload_ksk_*_device (bench.py's broadcast buffer) == the host upload, and a
+    word >= qKS is refused without leaving a key behind."""
+    import torch
+    from mkfhe_amd import keys as K
+    p = K.paramset(ps, method)
+    k, n = p.acc.k, p.acc.n
+    rng = np.random.default_rng(17)
+    dks = 4 if method == 0 else 3
+    outs = []
+    for dev_upload in (False, True):
+        eng = mk.MKAccumulatorEngine(p.acc)
+        eng.upload_keys(rng.integers(0, Q_MK, size=eng.evk_shape, dtype=np.uint32) * 0 + 5,
+                        rng.integers(0, Q_MK, size=eng.pkey_shape, dtype=np.uint32) * 0 + 7)
+        r2 = np.random.default_rng(18)
+        if method == 0:
+            ksk = r2.integers(0, p.ks.qKS, size=(k, 2048 * dks, n), dtype=np.uint32)
+            if dev_upload:
+                eng.upload_ksk_device(p.ks.qKS, p.ks.baseKS, n, d_ksk=_t(ksk))
+            else:
+                eng.upload_ksk_mntru(ksk, p.ks.qKS, p.ks.baseKS, n)
+            a1 = r2.integers(0, p.acc.q, size=(3, k, n), dtype=np.uint32)
+            a2 = r2.integers(0, p.acc.q, size=(3, k, n), dtype=np.uint32)
+            outs.append(eng.eval_nand_mntru(r2.integers(0, p.acc.q, size=(k, n), dtype=np.uint32), a1, a2))
+        else:
+            A = r2.integers(0, p.ks.qKS, size=(k, 2048, 32, dks, n), dtype=np.uint32)
+            Bk = r2.integers(0, p.ks.qKS, size=(k, 2048, 32, dks), dtype=np.uint32)
+            if dev_upload:
+                eng.upload_ksk_device(p.ks.qKS, p.ks.baseKS, n, d_A=_t(A), d_B=_t(Bk))
+            else:
+                eng.upload_ksk_mklwe(A, Bk, p.ks.qKS, p.ks.baseKS, n)
+            a1 = r2.integers(0, p.acc.q, size=(3, k, n), dtype=np.uint32)
+            a2 = r2.integers(0, p.acc.q, size=(3, k, n), dtype=np.uint32)
+            b = r2.integers(0, p.acc.q, size=3, dtype=np.uint32)
+            outs.append(np.concatenate([x.reshape(-1) for x in eng.eval_nand_mklwe(a1, b, a2, b)]))
+    assert np.array_equal(outs[0], outs[1])
+    eng = mk.MKAccumulatorEngine(p.acc)
+    if method == 0:
+        bad = torch.full((k * 2048 * dks * n,), int(p.ks.qKS), dtype=torch.int32, device="cuda:0")
+        with pytest.raises(mk.MkaccError) as e:
+            eng.upload_ksk_device(p.ks.qKS, p.ks.baseKS, n, d_ksk=bad)
+        assert e.value.code == -5
+
+
+def test_key_upload_keeps_a_pending_batch_error(mk, oracle):
+    """a device key upload must not clear an input-range error of an
+    earlier device batch that mkacc_sync has not reported yet."""
+    import torch
+    orc, evk, pkey, ct, acc = make_case(oracle, oracle.XZW, 2, 3, 45181, 1 << 7, 2, seed=12)
+    eng = _engine(mk, mk.MKNTRU, 2, 3, 45181, 1 << 7)
+    eng.upload_keys(evk.astype(np.uint32), pkey.astype(np.uint32))
+    ct_bad = ct.astype(np.uint32).copy()
+    ct_bad[0, 0, 0] = 45181
+    d_in = _t(acc.astype(np.uint32))
+    eng.eval_batch_device(_t(ct_bad), d_in, torch.empty_like(d_in), 2)
+    eng.upload_keys_device(_t(evk.astype(np.uint32)), _t(pkey.astype(np.uint32)))
+    with pytest.raises(mk.MkaccError) as e:
+        eng.sync()
+    assert e.value.code == -5
+
+
+def test_wide_device_entry_reports_out_of_range_inputs(mk, oracle):
+    """the 64-bit word path range-checks device accumulator words too
+    (FP64 kernels for Q < 2^50, integer kernels above)."""
+    import torch
+    for Q, fp in ((1125899906826241, True), (1152921504606830593, False)):
+        if not oracle.is_prime(Q):
+            continue
+        orc, evk, pkey, ct, acc = make_case(oracle, oracle.XZW, 2, 2, 45181, 1 << 10, 2, seed=13, Q=Q)
+        eng = _engine(mk, mk.MKNTRU, 2, 2, 45181, 1 << 10, Q=Q)
+        assert eng.wide and eng.wide_fp == fp
+        eng.upload_keys(evk.astype(np.uint64), pkey.astype(np.uint64))
+        acc_bad = acc.astype(np.uint64).copy()
+        acc_bad[1, 1, 5] = Q
+        d_in = _t(acc_bad)
+        eng.eval_batch_device(_t(ct.astype(np.uint32)), d_in, torch.empty_like(d_in), 2)
+        with pytest.raises(mk.MkaccError) as e:
+            eng.sync()
+        assert e.value.code == -5

@@ -26,7 +26,7 @@ def _engine(mk, method, k, n, q, baseG):
 def test_native_library_loaded(mk):
     import mkfhe_amd._lib as L
     lib = L.load()
-    assert lib.mkacc_abi_version() == 1
+    assert lib.mkacc_abi_version() == 2
 
 
 def test_ntt_forward_inverse_parity(mk, oracle):

@@ -1,0 +1,148 @@
+"""The loaders refuse libraries that were not built from this tree (VERDICT r2
+"what's weak" #3: round 2's A/B records came from libraries nothing tied to a
+source state), the seed-0 entropy journal makes fresh keys replayable, and the
+group API's host logic -- all without a GPU."""
+import ctypes
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+FAKE_SRC = r"""
+int mkacc_abi_version(void) { return ABI; }
+const char* mkacc_build_info(void) { return INFO; }
+"""
+
+
+def _fake_lib(tmp_path, name, abi, info):
+    src = tmp_path / f"{name}.c"
+    src.write_text(FAKE_SRC)
+    out = tmp_path / f"{name}.so"
+    subprocess.check_call(["gcc", "-shared", "-fPIC", f"-DABI={abi}", f'-DINFO="{info}"', "-o", str(out), str(src)])
+    return str(out)
+
+
+def test_in_tree_libraries_match_this_tree():
+    from mkfhe_amd import _lib, build, keys
+    L = _lib.load()
+    ids = build.engine_ids()
+    assert L.build_info["header"] == ids["header"] and L.build_info["source"] == ids["source"]
+    assert L.build_info["dg"] == "2,3,4,5"   # every digit count is instantiated
+    K = keys.load()
+    assert K.build_info["header"] == build.keys_ids()["header"]
+    assert K.build_info["source"] == build.keys_ids()["source"]
+
+
+def test_loader_refuses_foreign_header(tmp_path):
+    from mkfhe_amd import _lib, build
+    ids = build.engine_ids()
+    bad = _fake_lib(tmp_path, "hdr", 2, f"abi=2;header=0000000000000000;source={ids['source']};dg=2,3;flags=")
+    with pytest.raises(_lib.LibraryMismatch, match="header id"):
+        _lib.open_checked(bad)
+
+
+def test_loader_refuses_abi_mismatch(tmp_path):
+    from mkfhe_amd import _lib, build
+    ids = build.engine_ids()
+    bad = _fake_lib(tmp_path, "abi", 1, f"abi=1;header={ids['header']};source={ids['source']};dg=3;flags=")
+    with pytest.raises(_lib.LibraryMismatch, match="ABI version"):
+        _lib.open_checked(bad)
+
+
+def test_loader_refuses_library_without_build_info(tmp_path):
+    from mkfhe_amd import _lib
+    src = tmp_path / "old.c"
+    src.write_text("int mkacc_abi_version(void) { return 1; }\n")
+    out = tmp_path / "old.so"
+    subprocess.check_call(["gcc", "-shared", "-fPIC", "-o", str(out), str(src)])
+    with pytest.raises(_lib.LibraryMismatch, match="older than ABI 2"):
+        _lib.open_checked(str(out))
+
+
+def test_loader_refuses_stale_source_only_when_required(tmp_path):
+    from mkfhe_amd import _lib, build
+    ids = build.engine_ids()
+    info = f"abi=2;header={ids['header']};source=ffffffffffffffff;dg=2,3,4,5;flags=-DX=1"
+    stale = _fake_lib(tmp_path, "stale", 2, info)
+    with pytest.raises(_lib.LibraryMismatch, match="stale build"):
+        _lib.verify_build(stale, info, 2, build.ENGINE_HEADER, ids, require_source=True)
+    # an A/B variant (MKFHE_LIB) may differ in sources/flags but not in the ABI or header
+    got = _lib.verify_build(stale, info, 2, build.ENGINE_HEADER, ids, require_source=False)
+    assert got["flags"] == "-DX=1"
+
+
+def test_mkfhe_lib_variant_is_checked(tmp_path):
+    """A process started with MKFHE_LIB pointing at a foreign library fails at load."""
+    bad = _fake_lib(tmp_path, "var", 2, "abi=2;header=1111111111111111;source=x;dg=3;flags=")
+    r = subprocess.run([sys.executable, "-c", "from mkfhe_amd import _lib; _lib.load()"], cwd=ROOT,
+                       env={**os.environ, "MKFHE_LIB": bad}, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "refusing" in r.stderr
+
+
+# ---- seed-0 entropy journal ----------------------------------------------------------------
+
+def _fresh_sk(K, p):
+    return K.mntru_keygen(p, 0).F
+
+
+def test_entropy_journal_replays_seed0_keys():
+    from mkfhe_amd import keys as K
+    p = K.paramset("STD100_MKNTRU", 0)
+    K.entropy_set(None)                      # a fresh master, as a new process would draw
+    master, calls = K.entropy_get()
+    assert calls == 0 and len(master) == 64
+    a1, a2 = _fresh_sk(K, p), _fresh_sk(K, p)
+    assert K.entropy_get() == (master, 2)
+    assert not np.array_equal(a1, a2)        # every seed-0 call draws a new key
+    K.entropy_set(master)                    # replay
+    assert np.array_equal(_fresh_sk(K, p), a1) and np.array_equal(_fresh_sk(K, p), a2)
+    K.entropy_set(master, 1)                 # resume at the second call
+    assert np.array_equal(_fresh_sk(K, p), a2)
+    K.entropy_set(None)
+    assert K.entropy_get()[0] != master
+
+
+def test_entropy_from_environment():
+    code = ("from mkfhe_amd import keys as K; p = K.paramset('STD100_MKNTRU', 0); "
+            "print(K.entropy_get()[0]); print(int(K.mntru_keygen(p, 0).F.sum()))")
+    hexkey = "0123456789abcdef" * 4
+    runs = [subprocess.run([sys.executable, "-c", code], cwd=ROOT, env={**os.environ, "MKFHE_ENTROPY": hexkey},
+                           capture_output=True, text=True, timeout=120) for _ in range(2)]
+    assert all(r.returncode == 0 for r in runs), runs[0].stderr
+    assert runs[0].stdout.split()[0] == hexkey
+    assert runs[0].stdout == runs[1].stdout
+
+
+def test_encrypt_count_limit_is_an_error_not_a_crash():
+    from mkfhe_amd import keys as K
+    p = K.paramset("STD100_MKNTRU", 0)
+    sk = K.mntru_keygen(p, 5)
+    m = np.zeros(1, np.uint32)
+    ct = np.zeros(1, np.uint32)
+    rc = K.load().mkkg_mntru_encrypt(ctypes.byref(p), 0, K._p(np.ascontiguousarray(sk.Finv)), K._p(m), 4, 1 << 24,
+                                     K._p(ct))
+    assert rc == -1 and "2^24" in K.load().mkkg_last_error().decode()
+
+
+# ---- group host logic ------------------------------------------------------------------------
+
+@pytest.mark.parametrize("B,P", [(0, 1), (1, 2), (4096, 8), (65536, 8), (1001, 3), (5, 8)])
+def test_shard_range_matches_python(B, P):
+    from mkfhe_amd.accumulator import shard_range_c
+    from mkfhe_amd.shard import shard_range
+    got = [shard_range_c(B, P, i) for i in range(P)]
+    assert got == [shard_range(B, i, P) for i in range(P)]
+    assert got[0][0] == 0 and got[-1][1] == B
+
+
+def test_group_create_without_gpu_fails_cleanly():
+    from conftest import gpu_available
+    if gpu_available():
+        pytest.skip("needs a host without a GPU")
+    import mkfhe_amd as mk
+    with pytest.raises(mk.MkaccError):
+        mk.MKAccumulatorGroup(mk.paramset("STD100_MKNTRU"), [0, 0])

@@ -1,11 +1,11 @@
 #!/bin/bash
 # usage: tools/build_variant.sh NAME [-DFLAG ...]
-#   a DG=3-only engine build for A/B timing (mkfhe_amd/lib/variants/NAME.so)
+#   an engine build with extra -D switches for A/B timing (mkfhe_amd/lib/variants/NAME.so).
+#   Every digit count is instantiated, so a variant runs every test; its build
+#   identity (mkacc_build_info: header/source ids and these flags) is checked by
+#   mkfhe_amd._lib.load when it is loaded through MKFHE_LIB.
 NAME=$1; shift
-mkdir -p mkfhe_amd/lib/variants
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -fvisibility-inlines-hidden -Wl,-Bsymbolic \
-  -Wno-unused-result -Wno-pass-failed -I include -DMKACC_ONLY_DG=3 "$@" -Rpass-analysis=kernel-resource-usage \
-  -o mkfhe_amd/lib/variants/$NAME.so mkfhe_amd/csrc/mkacc_engine.hip 2> mkfhe_amd/lib/variants/$NAME.res
+python3 -m mkfhe_amd.build --variant "$NAME" "$@" > /dev/null
 rc=$?
 grep -A9 "mk_step_kernelILi3ELi0ELb0E" mkfhe_amd/lib/variants/$NAME.res | grep -E "VGPRs( Spill)?:" | sed 's/.*remark: *//' | tr '\n' ' '
 echo " [$NAME rc=$rc]"

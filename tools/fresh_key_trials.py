@@ -30,6 +30,8 @@ def main():
     want = 1 - (m1 & m2)
     bad_sets = 0
     for t in range(trials):
+        K.entropy_set(None)          # a fresh seed-0 master per trial, printed on failure
+        master = K.entropy_get()[0]
         cc = BinFHEContext()
         cc.GenerateBinFHEContext(ps, 0)
         sk = cc.MNTRU_KeyGen()
@@ -43,6 +45,7 @@ def main():
         line = f"trial {t}: single {list(map(int, d1))} batch {list(map(int, d2))} same={np.array_equal(single, batch)}"
         if not ok:
             bad_sets += 1
+            line += f" | MKFHE_ENTROPY={master}"
             p, bk = cc.params, cc.BTKey
             k, n = p.acc.k, p.acc.n
             orc = oracle.Oracle(oracle.XZW, k, n, N, p.acc.Q, p.acc.q, p.acc.baseG)
