@@ -156,6 +156,15 @@ def open_checked(path: str, require_source: bool | None = None):
     from . import build as _build
     if not os.path.exists(path):
         raise RuntimeError(f"{path} not found: build the HIP engine first (python -m mkfhe_amd.build)")
+    # One HIP runtime per process.  torch ships its own libamdhip64 (soname
+    # libamdhip64.so.7, but NEEDED as "libamdhip64.so"): loaded first, it also
+    # satisfies this library's libamdhip64.so.7 dependency; loaded after
+    # /opt/rocm's copy, it becomes a second runtime that sees no GPU ("No HIP
+    # GPUs are available") and whose tensors this library could not use.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(path)
     for name in ("mkacc_abi_version", "mkacc_build_info"):
         if not hasattr(L, name):

@@ -47,11 +47,11 @@ int fail(int code, const std::string& msg) {
     } while (0)
 
 // 256-thread workgroups, two per CU (2 waves / SIMD, LDS 65.8 KB each).
-// 512-thread workgroups sharing one LDS table image (one per CU) were tried
-// and rejected: waves 4-7 of such a workgroup produced rare, run-to-run
-// varying wrong results on MI355X (tools/dbg/stress.py; root cause not
-// identified -- isolated transposes and LDS fills were clean), while two
-// 4-wave workgroups per CU are deterministic and measured faster.
+// The round-1 wrong results in waves 4-7 of 512-thread workgroups were the
+// co-resident-wave store-data hazard of 16-byte buffer stores (DESIGN.md s2;
+// fixed by bstore4, guarded by tools/isa_audit.py), not the workgroup shape;
+// two 4-wave workgroups per CU stay because they were measured faster than
+// one 8-wave workgroup sharing a single LDS table image.
 constexpr int kWavesPerBlock = 4;
 constexpr int kThreads = 64 * kWavesPerBlock;
 
@@ -301,6 +301,9 @@ struct DigitMac {
 #ifndef MKACC_DSCR_PF
 #define MKACC_DSCR_PF 0
 #endif
+#ifndef MKACC_DSCR_WAIT
+#define MKACC_DSCR_WAIT 0
+#endif
     static constexpr int kPrefetch = DS == 2 ? (MKACC_DSCR_PF ? MKACC_DSCR_PF : (DG <= 3 ? 3 : 2)) : Prefetch<DG>::value;
     static constexpr int kBuf = kPrefetch + 1;
     const StepRes& sr;
@@ -472,6 +475,9 @@ __device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_
         KeyGroup kg[mac.kBuf];
         ntt_fwd(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, s.l, Q, s.m.m1);
         digit_range<DG>(x, Q);
+        // MKACC_DSCR_WAIT=1: the d_i scratch stores of the first pass are waited for
+        // here, just before the first reload, instead of right after that pass
+        if (DS == 2 && MKACC_DSCR_WAIT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
         for (int j = 0; j < mac.kPrefetch; ++j) mac.issue(kg[j], j);
         mac.run(x, uj, sv, kg);
@@ -660,7 +666,7 @@ __device__ __forceinline__ void step_body(const StepCtx& s, uint32_t k, uint32_t
         grow_sv();
         t0 = 2;
         // the scratch stores complete before the later passes read them back
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (!MKACC_DSCR_WAIT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     for (uint32_t t = t0; t < k; ++t) {
         party_pass<DG, METHOD, FIRST, false, DSCR ? 2 : 0>(s, index + t < k ? index + t : index + t - k, sv, w);

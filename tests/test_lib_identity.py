@@ -146,3 +146,15 @@ def test_group_create_without_gpu_fails_cleanly():
     import mkfhe_amd as mk
     with pytest.raises(mk.MkaccError):
         mk.MKAccumulatorGroup(mk.paramset("STD100_MKNTRU"), [0, 0])
+
+
+def test_one_hip_runtime_per_process():
+    """Loading the engine first must not leave two HIP runtimes in the process
+    (torch's bundled libamdhip64 and /opt/rocm's): _lib imports torch before the
+    CDLL so the engine binds to torch's copy (round-3 record: a second runtime
+    reported "No HIP GPUs are available" to torch)."""
+    code = ("import mkfhe_amd._lib as L; L.load(); import torch; "
+            "maps = {l.split()[-1] for l in open('/proc/self/maps') if 'libamdhip64' in l}; print(len(maps), sorted(maps))")
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.startswith("1 "), r.stdout
