@@ -57,8 +57,10 @@ Q50 = 1125899906826241               # config 5 stress modulus (SURVEY.md s0 ite
 REF_CPU_S_PER_EVALACC = {            # reference EvalAcc, 1 core of the survey container
     "STD100_MKNTRU": 0.274, "STD128_MKNTRU": 0.475, "STD100_MKNTRU_LWE": 0.215,
     "STD100_MKNTRU_LWE_2": 0.721, "STD128_MKNTRU_3": 6.750, "STD100_MKNTRU_3": 2.872}
-# oracle / reference single-thread EvalAcc time on the same container type
-ORACLE_OVER_REF = {"STD128_MKNTRU": 2.97, "STD100_MKNTRU": 2.62, "STD100_MKNTRU_LWE_2": 2.77}
+# oracle / reference single-thread EvalAcc time on the same container type (BASELINE.md s3;
+# tools/oracle_calib.py, profiles/r3/oracle_calibration.json: the 32-bit word oracle path)
+ORACLE_OVER_REF = {"STD128_MKNTRU": 0.566, "STD100_MKNTRU": 0.575, "STD100_MKNTRU_LWE_2": 0.460,
+                   "STD100_MKNTRU_3": 0.447, "STD128_MKNTRU_3": 0.432}
 
 
 def algorithmic_counts(k: int, n: int, dg: int, nk: int, N: int = 2048, B: int = 1, word: int = 4):
@@ -425,6 +427,9 @@ def run_rank(args, env: dict, make_engine, make_checker, torch_device: str, back
                 "host": cpu,
                 "reference_1core_s_per_evalacc": ref,
                 "oracle_over_reference_1core": ORACLE_OVER_REF.get(args.paramset) if ref else None,
+                # the reference's throughput on the same cores, scaled by the 1-core time ratio
+                "reference_equivalent_value": (G / dt_c * ORACLE_OVER_REF[args.paramset]
+                                               if ref and args.paramset in ORACLE_OVER_REF else None),
                 "reference_source": "SURVEY.md s6: the reference's own EvalAcc, 1 thread of the survey container",
             }
     if world > 1:
