@@ -23,8 +23,9 @@ import sys
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(_HERE)
-SOURCES = [os.path.join(_HERE, "csrc", "mkacc_engine.hip")]
-HEADERS = [os.path.join(_HERE, "csrc", f) for f in ("mkacc_device.hpp", "mkacc_host_math.hpp", "mkacc_gate.hpp", "mkacc_wide.hpp", "mkacc_widefp.hpp")] + [
+SOURCES = [os.path.join(_HERE, "csrc", f) for f in ("mkacc_engine.hip", "mkacc_steps.hip")]
+HEADERS = [os.path.join(_HERE, "csrc", f) for f in ("mkacc_kernels.hpp", "mkacc_device.hpp", "mkacc_host_math.hpp",
+                                                    "mkacc_gate.hpp", "mkacc_wide.hpp", "mkacc_widefp.hpp")] + [
     os.path.join(ROOT, "include", "mkfhe_amd.h")]
 OUT = os.path.join(_HERE, "lib", "libmkfhe_amd.so")
 KEYS_SOURCES = [os.path.join(_HERE, "csrc", "mkkeys.cpp")]
@@ -83,20 +84,59 @@ def build_keys(force: bool = False, verbose: bool = False) -> str:
     return KEYS_OUT
 
 
+# Translation units of the engine library, compiled in parallel and linked into
+# one .so: the host unit (C ABI, batch / gate / primitive kernels) and the step
+# kernel units of mkacc_steps.hip (one per digit count and kernel kind, and the
+# two 64-bit word paths), which the host unit launches through mkacc_tu.
+UNITS = [("engine", "mkacc_engine.hip", [])] + [
+    (f"step_dg{d}", "mkacc_steps.hip", [f"-DMKACC_TU_DG={d}", "-DMKACC_TU_PART=0"]) for d in (2, 3, 4, 5)] + [
+    (f"lat_dg{d}", "mkacc_steps.hip", [f"-DMKACC_TU_DG={d}", "-DMKACC_TU_PART=1"]) for d in (2, 3, 4)] + [
+    ("wide", "mkacc_steps.hip", ["-DMKACC_TU_WIDE=1"]), ("widefp", "mkacc_steps.hip", ["-DMKACC_TU_WIDE=2"])]
+
+
+def _jobs() -> int:
+    for var in ("MAX_JOBS", "MKFHE_BUILD_JOBS"):
+        if os.environ.get(var, "").isdigit():
+            return max(1, int(os.environ[var]))
+    return max(1, min(len(UNITS), os.cpu_count() or 1))
+
+
 def compile_engine(out: str, flags: list[str], report: str, verbose: bool = False) -> str:
-    """hipcc the engine into `out` with extra `flags` (-D switches of A/B builds)."""
+    """hipcc the engine units into `out` with extra `flags` (-D switches of A/B builds)."""
+    from concurrent.futures import ThreadPoolExecutor
+
     os.makedirs(os.path.dirname(out), exist_ok=True)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-fvisibility-inlines-hidden", "-Wl,-Bsymbolic",
-           "-Wno-unused-result", "-Wno-pass-failed", "-I", os.path.join(ROOT, "include"),
-           *_id_defines("MKACC", engine_ids(), flags), *flags,
-           "-Rpass-analysis=kernel-resource-usage", "-o", out + ".tmp"] + SOURCES
-    if verbose:
-        print(" ".join(cmd))
+    objdir = out[:-3] + ".objs"
+    os.makedirs(objdir, exist_ok=True)
+    common = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
+              "-fvisibility-inlines-hidden", "-Wno-unused-result", "-Wno-pass-failed",
+              "-I", os.path.join(ROOT, "include"), *_id_defines("MKACC", engine_ids(), flags), *flags,
+              "-Rpass-analysis=kernel-resource-usage"]
+
+    def unit(u):
+        name, src, defs = u
+        obj = os.path.join(objdir, name + ".o")
+        cmd = common + defs + ["-c", "-o", obj, os.path.join(_HERE, "csrc", src)]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        return name, obj, r
+
+    with ThreadPoolExecutor(max_workers=_jobs()) as ex:
+        results = list(ex.map(unit, UNITS))
     # per-kernel VGPR / spill / occupancy report next to the library
     with open(report, "w") as rep:
-        subprocess.check_call(cmd, stderr=rep)
+        for name, _, r in results:
+            rep.write(f"### unit {name}\n{r.stderr}")
+    for name, _, r in results:
+        if r.returncode != 0:
+            raise subprocess.CalledProcessError(r.returncode, f"hipcc unit {name}", r.stdout, r.stderr[-4000:])
+    link = [hipcc, f"--offload-arch={ARCH}", "--hip-link", "-shared", "-fPIC", "-Wl,-Bsymbolic", "-o", out + ".tmp"] + [
+        obj for _, obj, _ in results]
+    if verbose:
+        print(" ".join(link), flush=True)
+    subprocess.check_call(link)
     os.replace(out + ".tmp", out)
     return out
 

@@ -46,860 +46,10 @@ int fail(int code, const std::string& msg) {
             return fail(MKACC_E_DEVICE, std::string(#expr) + ": " + hipGetErrorString(_e));    \
     } while (0)
 
-// 256-thread workgroups, two per CU (2 waves / SIMD, LDS 65.8 KB each).
-// The round-1 wrong results in waves 4-7 of 512-thread workgroups were the
-// co-resident-wave store-data hazard of 16-byte buffer stores (DESIGN.md s2;
-// fixed by bstore4, guarded by tools/isa_audit.py), not the workgroup shape;
-// two 4-wave workgroups per CU stay because they were measured faster than
-// one 8-wave workgroup sharing a single LDS table image.
-constexpr int kWavesPerBlock = 4;
-constexpr int kThreads = 64 * kWavesPerBlock;
-
-// Table image (built once per context, HBM), in uint2 pairs:
-//   [0, kTwlPairs)              forward per-lane twiddles (mkacc_device.hpp layout)
-//   [kTwlPairs, +kInvImgPairs)  inverse per-lane twiddles and the psi^-i twist (ntt_inv)
-//   [kPsiOff, + 2N)             psi^e (e in [0, 2N)) with Shoup companion, at psi_pos(e)
-//   [kPsm1Off, + 2N)            psi^e - 1 with Shoup companion, at psi_pos(e)
-// The NTTs read the twiddle runs from HBM/L2 (L1-resident, coalesced); the
-// psi^e - 1 table, gathered at data-dependent slots, is copied into LDS at kernel
-// start, followed by one transpose scratch of kLdsWords per wave.
-constexpr int kPsiPairs = 2 * kN;
-constexpr int kPsiOff = kTwlPairs + kInvImgPairs;
-constexpr int kPsm1Off = kPsiOff + kPsiPairs;
-constexpr int kImgPairs = kPsm1Off + kPsiPairs;
-constexpr int kImgWords = 2 * kImgPairs;
-static_assert(kPsm1Off % 2 == 0 && kTwlC % 2 == 0, "LDS tables are copied with dwordx4");
-// LDS: [forward stage-10 twiddles, 1024 pairs][psi^e - 1 table, 2N pairs][scratch]
-constexpr int kLdsTabWords = 2 * (1024 + kPsiPairs);
-constexpr size_t kStepLdsBytes = (size_t)(kLdsTabWords + kWavesPerBlock * kLdsWords) * 4;
-static_assert(kLdsTabWords % 4 == 0, "LDS tables are copied with dwordx4");
-static_assert(2 * kStepLdsBytes <= 160 * 1024, "two workgroups per CU");
-
-// Bank-spreading position of psi^e in the LDS table.  A wave gathers
-// e = c (2 brv6(lane) + 1) + 128 c brv5(r) mod 2N (Mono): the low 7 bits are
-// the lane's alone, the register part only moves bits 7..11.  Xor-ing bits 5..6
-// into bits 0..1 touches the low 7 bits only, so the gather address stays
-// additive in r (Mono::at: one add and one and), and it spreads the 64 lanes
-// over all 32 bank pairs of a ds_read_b64 when c is odd or 2 mod 4 -- the best
-// any swizzle of the low bits can do.  Exhaustively over all c and r (model:
-// most distinct dwords per bank, 2 = conflict-free) this averages 3.83 LDS
-// cycles per gather against 4.28 for the earlier e ^ ((e >> 5) & 31), which
-// also cost 6 VALU of address arithmetic per gather instead of 2.
-// MKACC_PSI_HI=1 (A/B): the earlier e ^ ((e >> 5) & 31), gathered with 4 VALU
-#ifndef MKACC_PSI_HI
-#define MKACC_PSI_HI 0
-#endif
-__host__ __device__ __forceinline__ uint32_t psi_pos(uint32_t e) {
-    return MKACC_PSI_HI ? e ^ ((e >> 5) & 31u) : e ^ ((e >> 5) & 3u);
-}
-
-enum { XZW = 0, XZW_B = 1 };
-
-// Device key words (upload_keys_impl / key_layout_kernel): every evk / pkey word
-// is stored times N^-1 * 2^32 mod Q -- N^-1 because the accumulator lives scaled by
-// N^-1 (the inverse NTT then needs no N^-1), 2^32 so that one Montgomery reduction
-// (redc) of a lazy sum of key products returns the plain sum.  For MKNTRU the
-// ev1 block of every step i < n holds ev1 + ev2 (both the d- and f-halves), so
-// ev1 - ev2 X^-c = (ev1 + ev2) + ev2 (X^(N-c) - 1) is one product with a
-// psi^e - 1 table entry (key_eff).
-struct StepArgs {
-    const uint32_t* acc_in;    // [B][k][N] C4, scaled by N^-1, residues in [0, 2Q)
-    uint32_t* acc_out;         // [B][k][N]
-    const uint32_t* cvals;     // [B] monomial exponents c of this step, in [0, 2N)
-    const uint32_t* key1;      // ev1 (+ ev2 for MKNTRU) of step (u, i) : [dg][2][N] C4
-    const uint32_t* key2;      // ev2 = (*ek)[u][1][i] (XZW)
-    const uint32_t* keys;      // evs = (*ek)[0][0][n] (first step)
-    const uint32_t* pkey;      // [k][dg][N]
-    const uint32_t* img;       // table image [kImgWords]
-    const uint2* tw_fwd;       // [N] reference forward table (pass A, scalar reads)
-    const uint2* tw_inv;       // [32] inverse pass-1 table (ntt_inv)
-    uint32_t* dscr;            // [B][dg][N] C4 scratch of the step's d_i (mk_step_kernel DSCR) or null
-    uint32_t B, k, index;
-    Mod m;
-    SddConsts sd;
-};
-
-// Copy the forward stage-10 twiddles (the largest per-lane run, used by 3/4
-// of the NTTs) and the psi^e - 1 table of the image into this workgroup's LDS.
-__device__ __forceinline__ void load_image(uint32_t* smem, const uint32_t* img) {
-    const uint4* src = reinterpret_cast<const uint4*>(img);
-    uint4* dst = reinterpret_cast<uint4*>(smem);
-    for (int i = threadIdx.x; i < 512; i += blockDim.x) dst[i] = src[kTwlC / 2 + i];
-    for (int i = threadIdx.x; i < kN; i += blockDim.x) dst[512 + i] = src[kPsm1Off / 2 + i];
-    __syncthreads();
-}
-
-struct Tables {
-    const uint2* twf;    // HBM image: forward per-lane twiddles
-    const uint2* twi;    // HBM image: inverse per-lane twiddles + twist
-    const uint2* twfc;   // LDS: forward stage-10 twiddles
-    const uint2* psi;    // LDS: psi^e - 1
-};
-__device__ __forceinline__ Tables tables(uint32_t* smem, const uint32_t* img) {
-    const uint2* g = reinterpret_cast<const uint2*>(img);
-    const uint2* t = reinterpret_cast<const uint2*>(smem);
-    return Tables{g, g + kTwlPairs, t, t + 1024};
-}
-
-// Monomial X^e at EVAL slot j = (lane << 5) | r: the reference stores
-// a(psi^(2 brv(j) + 1)) at position j (transformnat-impl.h:705-760), so
-// X^c -> psi^(c (2 brv(j) + 1)), with 2 brv(j) + 1 = 128 brv5(r) + (2 brv6(lane) + 1).
-// co = c * (2 brv6(lane) + 1) per lane; the r part 128 c brv5(r) is
-// wave-uniform and moves only bits 7..11 of e, which psi_pos leaves in place, so
-// the byte offset of psi_pos(e) is (w + 1024 c brv5(r)) & 0x7fff with the per-lane
-// w = psi_pos(co mod 2N) * 8.  at() returns the LDS pair of psi^e - 1, i.e. the
-// EVAL slot of X^c - 1.
-struct Mono {
-    uint32_t w;         // per lane: 8 psi_pos(c (2 brv6(l) + 1) mod 2N)
-    uint32_t c;         // wave-uniform exponent
-    __device__ __forceinline__ uint2 at(const uint2* psi, int r) const {
-        constexpr uint32_t kBr5[32] = {0, 16, 8, 24, 4, 20, 12, 28, 2, 18, 10, 26, 6, 22, 14, 30,
-                                       1, 17, 9, 25, 5, 21, 13, 29, 3, 19, 11, 27, 7, 23, 15, 31};
-        // the wave-uniform part is recomputed per use (one s_mul) rather than
-        // kept as 32 hoisted SGPR constants per monomial; the add is volatile asm
-        // so the 32 per-slot addresses are not hoisted out of the party / digit
-        // loops (they would stay live in VGPRs across the NTTs)
-        uint32_t cs = c;
-        asm volatile("" : "+s"(cs));
-        uint32_t a;
-        asm volatile("v_add_u32 %0, %1, %2" : "=v"(a) : "s"(cs * (1024u * kBr5[r])), "v"(w));
-        a &= 0x7fffu;
-        if (MKACC_PSI_HI) a ^= (a >> 5) & 0xf8u;   // 8 psi_pos(e) from 8 e
-        return *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(psi) + a);
-    }
-};
-__device__ __forceinline__ Mono make_mono(uint32_t c, uint32_t l) {
-    const uint32_t o = ((__brev(l) >> 26) << 1) | 1u;   // 2 brv6(l) + 1
-    const uint32_t co = __umul24(c, o) & (2u * kN - 1u);
-    return Mono{(MKACC_PSI_HI ? co : psi_pos(co)) << 3, c};
-}
-
-// Lazy Shoup product x*w in [0, 2Q) (x < 2^32)
-__device__ __forceinline__ uint32_t mul_shoup_lazy(uint32_t x, uint2 w, uint32_t Q) {
-    const uint32_t q = __umulhi(x, w.y);
-    return (uint32_t)mad64_pin<true>(q, 0u - Q, mul64_pin<false>(x, w.x));   // x*w - q*Q in [0, 2Q)
-}
-
-// Ranges of the lazy Montgomery sums, in units of Q (values) and Q^2 (sums).
-// redc needs a sum below Q * 2^32 > 32 Q^2.  Digit-NTT outputs are < kG Q
-// (digit_range), effective key words from key_eff < kD Q, and the previous
-// accumulator joins the party sum as acc * (2^32 mod Q) < 2 Q^2 when it fits
-// (kAccInSum), otherwise it is added after the reduction.
-template <int DG, int METHOD, bool FIRST>
-struct Bounds {
-    static constexpr int kG = DG > 4 ? 2 : 4;
-    static constexpr int kD = DG * kG * 3 + 2 <= 32 ? 3 : (DG * kG * 2 <= 32 ? 2 : 1);
-    // the d-words the party sums actually see: XZW_B steps after the first use ev1 itself
-    static constexpr int kDSum = (METHOD == XZW_B && !FIRST) ? 1 : kD;
-    static constexpr bool kAccInSum = !FIRST && DG * kG * kDSum + 2 <= 32;
-    static_assert(DG * kG * kDSum + (kAccInSum ? 2 : 0) <= 32, "party sum bound");
-    // sumV gains DG * kG per party (pkey canonical); fold64 leaves < 2
-    static constexpr int kSvParty = DG * kG;
-    // f-part: the index party's folded sum (< 2, < 4 with the accumulator added
-    // there) plus DG products with canonical f-words (split form) or, in the
-    // first step, with f-words reduced to canonical
-    static_assert(4 + DG * kG <= 32, "f-part bound");
-};
-
-// [0, 3Q) -> [0, KD Q)
-template <int KD>
-__device__ __forceinline__ uint32_t from3q(uint32_t d, uint32_t Q) {
-    if (KD <= 2) d = min(d, d - 2u * Q);
-    if (KD <= 1) d = min(d, d - Q);
-    return d;
-}
-
-// Effective key word d_i / f_i of mk-acc-xzw(_B).cpp AddToAccXZW{,0}, below KD Q.
-// k1 is the stored ev1 word (ev1 + ev2 for MKNTRU, StepArgs), k2 = ev2, ks = evs.
-template <int METHOD, bool FIRST, int KD>
-__device__ __forceinline__ uint32_t key_eff(uint32_t k1, uint32_t k2, uint32_t ks, const uint2* psi,
-                                            const Mono& mp, const Mono& mn, int r, uint32_t Q) {
-    if (METHOD == XZW) {
-        if (FIRST) {
-            // evs + ev1*(X^c-1) + ev2*(X^-c-1)          (xzw.cpp:375-378)
-            const uint32_t e1 = k1 + Q - k2;                         // ev1, (0, 2Q)
-            uint32_t d = ks + mul_shoup_lazy(e1, mp.at(psi, r), Q) + mul_shoup_lazy(k2, mn.at(psi, r), Q);
-            d = min(d, d - 2u * Q);                                  // [0, 5Q) -> [0, 3Q)
-            return from3q<KD>(d, Q);
-        }
-        // ev1 - ev2*(X^-c - 1) - ev2  ==  ev1 - ev2*X^-c  ==  (ev1 + ev2) + ev2*(X^(N-c) - 1)
-        // (xzw.cpp:322-325); mn is the monomial X^(N-c) = -X^-c here
-        return from3q<KD>(k1 + mul_shoup_lazy(k2, mn.at(psi, r), Q), Q);
-    } else {
-        if (FIRST) {
-            // evs + ev1*(X^c-1)                            (xzw_B.cpp:368-371)
-            return from3q<KD>(ks + mul_shoup_lazy(k1, mp.at(psi, r), Q), Q);
-        }
-        return k1;                                        // (xzw_B.cpp:311-314)
-    }
-}
-
-// digit NTT outputs: [0, 4Q) for DG <= 4, brought to [0, 2Q) at DG = 5 (Bounds::kG)
-template <int DG>
-__device__ __forceinline__ void digit_range(uint32_t (&x)[kRegs], uint32_t Q) {
-    if (DG > 4) {
-#pragma unroll
-        for (int r = 0; r < kRegs; ++r) x[r] = min(x[r], x[r] - 2u * Q);
-    }
-}
-
-// Key words of one 4-register group of a MAC: software-pipelined kPrefetch
-// groups ahead so the L2 latency of the step's key block overlaps the arithmetic.
-template <int DG>
-#ifndef MKACC_PF3
-#define MKACC_PF3 1
-#endif
-struct Prefetch { static constexpr int value = DG <= 3 ? MKACC_PF3 : 0; };
-// accumulator loads: each gate's own rows, written by the previous step launch
-__device__ __forceinline__ u32x4 aload4(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-    return __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
-}
-// key-block loads (shared by every gate of the launch, streamed from L2)
-__device__ __forceinline__ u32x4 kload4(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-    // default cache policy: the 8 waves of a CU share the key lines through L1
-    // (non-temporal loads measured 11% slower, profiles/r2/ab_series1.txt)
-    return __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
-}
-struct KeyGroup {
-    u32x4 k1, k2, ks, pk, acc;
-    uint2 mono[4];   // X^(N-c) - 1 at the group's slots (XZW after the first step)
-};
-// per-wave resources of the MAC helpers
-struct StepRes {
-    __amdgpu_buffer_rsrc_t rin, rk1, rk2, rks, rpk, rds;
-    const uint2* psi;
-    Mono mp, mn;
-    Mod m;
-    uint32_t vo;
-};
-
-// uj_u += g * d_i ; sv += g * P[u][i]          (xzw.cpp:263-269)
-// START (digit 0): uj_u starts from acc_u * 2^32 (AddToAccXZW's acc + acctemp,
-// xzw.cpp:342-344; in Montgomery form, redc divides by 2^32) when the bound
-// allows, streamed in with the keys; 0 in the FIRST step, where AddToAccXZW0
-// overwrites acc (xzw.cpp:380).
-// The caller issues the first kPrefetch key groups (issue()), run() streams
-// the rest kPrefetch groups ahead.  (Issuing the first group before the digit
-// NTT spilled 23 VGPRs and measured 4% slower, profiles/r2/ab_series1.txt.)
-// DS (XZW after the first step, mk_step_kernel DSCR): d_i is the same for every
-// party of the step, so the first party pass computes it and stores it to the
-// gate's HBM scratch (DS = 1) and the later passes load it (DS = 2) instead of
-// the ev1'/ev2 words and the psi^e - 1 gathers; DS = 0 computes it per party.
-template <int DG, int METHOD, bool FIRST, bool START, int DS = 0>
-struct DigitMac {
-    using Bd = Bounds<DG, METHOD, FIRST>;
-    static_assert(DS == 0 || (METHOD == XZW && !FIRST), "d_i scratch: XZW steps after the first");
-    static constexpr bool kAcc = START && Bd::kAccInSum;
-    // MKACC_MONO_PF=0 (A/B): gather X^(N-c) - 1 at use instead of with the key group
-#ifndef MKACC_MONO_PF
-#define MKACC_MONO_PF 1
-#endif
-    static constexpr bool kMonoPf = MKACC_MONO_PF && METHOD == XZW && !FIRST && DS != 2;
-    // a d_i reload comes from HBM and frees the k2 / psi registers: prefetched
-    // 3 groups ahead at DG <= 3, 2 at DG >= 4 (3 spill 10 VGPRs there); 1 group measured
-    // 1-4% slower (profiles/r2/ab_dscr.txt)
-#ifndef MKACC_DSCR_PF
-#define MKACC_DSCR_PF 0
-#endif
-#ifndef MKACC_DSCR_WAIT
-#define MKACC_DSCR_WAIT 0
-#endif
-    static constexpr int kPrefetch = DS == 2 ? (MKACC_DSCR_PF ? MKACC_DSCR_PF : (DG <= 3 ? 3 : 2)) : Prefetch<DG>::value;
-    static constexpr int kBuf = kPrefetch + 1;
-    const StepRes& sr;
-    uint32_t koff, poff, aoff, doff;
-    __device__ __forceinline__ DigitMac(const StepRes& r, int i, uint32_t u)
-        : sr(r), koff((uint32_t)(2 * i) * (kN * 4u)), poff((u * DG + (uint32_t)i) * (kN * 4u)), aoff(u * (kN * 4u)),
-          doff((uint32_t)i * (kN * 4u)) {}
-    __device__ __forceinline__ void issue(KeyGroup& t, int gq) const {
-        const uint32_t go = gq * 1024u;
-        if (DS == 2)
-            t.k1 = aload4(sr.rds, sr.vo, doff + go);   // d_i of the first party pass
-        else
-            t.k1 = kload4(sr.rk1, sr.vo, koff + go);
-        t.pk = kload4(sr.rpk, sr.vo, poff + go);
-        if (METHOD == XZW && DS != 2) t.k2 = kload4(sr.rk2, sr.vo, koff + go);
-        if (FIRST) t.ks = kload4(sr.rks, sr.vo, koff + go);
-        if (kAcc) t.acc = aload4(sr.rin, sr.vo, aoff + go);
-        if (kMonoPf) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) t.mono[e] = sr.mn.at(sr.psi, 4 * gq + e);
-        }
-    }
-    __device__ __forceinline__ void run(const uint32_t (&g)[kRegs], uint64_t (&uj)[kRegs], uint64_t (&sv)[kRegs],
-                                        KeyGroup (&kg)[kBuf]) const {
-        const uint32_t Q = sr.m.Q;
-#pragma unroll
-        for (int gq = 0; gq < 8; ++gq) {
-            if (gq + kPrefetch < 8) issue(kg[(gq + kPrefetch) % kBuf], gq + kPrefetch);
-            const KeyGroup& t = kg[gq % kBuf];
-            u32x4 dv;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int r = 4 * gq + e;
-                const uint32_t deff =
-                    DS == 2 ? t.k1[e]
-                    : kMonoPf ? from3q<Bd::kD>(t.k1[e] + mul_shoup_lazy(t.k2[e], t.mono[e], Q), Q)   // = key_eff
-                              : key_eff<METHOD, FIRST, Bd::kD>(t.k1[e], t.k2[e], t.ks[e], sr.psi, sr.mp, sr.mn, r, Q);
-                dv[e] = deff;
-                const uint64_t base = kAcc ? mad64(t.acc[e], sr.m.r32, 0) : (START ? 0ull : uj[r]);
-                uj[r] = mad64(g[r], deff, base);
-                sv[r] = mad64(g[r], t.pk[e], sv[r]);
-            }
-            if (DS == 1) bstore4(dv, sr.rds, sr.vo, doff + gq * 1024u);
-            sched_fence();
-        }
-    }
-};
-
-// w += h * f_i                                  (xzw.cpp:281-288)
-// (first step, and XZW_B: f-words reduced to canonical, Bounds' f-part bound)
-template <int DG, int METHOD, bool FIRST>
-__device__ __forceinline__ void mac_index(const uint32_t (&h)[kRegs], int i, uint64_t (&w)[kRegs],
-                                          __amdgpu_buffer_rsrc_t rk1, __amdgpu_buffer_rsrc_t rk2,
-                                          __amdgpu_buffer_rsrc_t rks, const uint2* psi, const Mono& mp,
-                                          const Mono& mn, uint32_t vo, uint32_t Q) {
-    const uint32_t polyB = kN * 4u;
-    const uint32_t koff = (uint32_t)(2 * i + 1) * polyB;
-    constexpr int kPrefetch = Prefetch<DG>::value;
-    KeyGroup kg[kPrefetch + 1];
-    auto issue = [&](KeyGroup& t, int gq) {
-        const uint32_t go = gq * 1024u;
-        t.k1 = kload4(rk1, vo, koff + go);
-        if (METHOD == XZW) t.k2 = kload4(rk2, vo, koff + go);
-        if (FIRST) t.ks = kload4(rks, vo, koff + go);
-    };
-#pragma unroll
-    for (int j = 0; j < kPrefetch; ++j) issue(kg[j], j);
-#pragma unroll
-    for (int gq = 0; gq < 8; ++gq) {
-        if (gq + kPrefetch < 8) issue(kg[(gq + kPrefetch) % (kPrefetch + 1)], gq + kPrefetch);
-        const KeyGroup& t = kg[gq % (kPrefetch + 1)];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const int r = 4 * gq + e;
-            const uint32_t feff = key_eff<METHOD, FIRST, 1>(t.k1[e], t.k2[e], t.ks[e], psi, mp, mn, r, Q);
-            w[r] = mad64(h[r], feff, w[r]);
-        }
-        sched_fence();
-    }
-}
-
-// XZW steps after the first: f_i = ev1'_i - ev2'_i X^-c (xzw.cpp:322-325) is
-// linear in the keys, so with the stored ev1 + ev2:
-//   sum_i h_i f_i = sum_i h_i (ev1 + ev2)'_i + (X^(N-c) - 1) sum_i h_i ev2'_i
-// two lazy sums per slot here and ONE monomial product per slot after the last
-// digit (step_body) instead of one per slot and digit.
-template <int DG>
-struct SplitMac {
-    static constexpr int kPrefetch = Prefetch<DG>::value;
-    static constexpr int kBuf = kPrefetch + 1;
-    const StepRes& sr;
-    uint32_t koff;
-    __device__ __forceinline__ SplitMac(const StepRes& r, int i) : sr(r), koff((uint32_t)(2 * i + 1) * (kN * 4u)) {}
-    __device__ __forceinline__ void issue(KeyGroup& t, int gq) const {
-        const uint32_t go = gq * 1024u;
-        t.k1 = kload4(sr.rk1, sr.vo, koff + go);
-        t.k2 = kload4(sr.rk2, sr.vo, koff + go);
-    }
-    __device__ __forceinline__ void run(const uint32_t (&h)[kRegs], uint64_t (&w)[kRegs], uint64_t (&w2)[kRegs],
-                                        KeyGroup (&kg)[kBuf]) const {
-#pragma unroll
-        for (int gq = 0; gq < 8; ++gq) {
-            if (gq + kPrefetch < 8) issue(kg[(gq + kPrefetch) % kBuf], gq + kPrefetch);
-            const KeyGroup& t = kg[gq % kBuf];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int r = 4 * gq + e;
-                w[r] = mad64(h[r], t.k1[e], w[r]);
-                w2[r] = mad64(h[r], t.k2[e], w2[r]);
-            }
-            sched_fence();
-        }
-    }
-};
-
-// Per-wave state shared by the passes of one step.
-struct StepCtx {
-    const Tables tb;
-    uint32_t* lds;
-    const uint2* tw_fwd;
-    const uint2* tw_inv;
-    Mod m;
-    SddConsts sd;
-    Mono mp, mn;
-    uint32_t l, vo;
-    __amdgpu_buffer_rsrc_t rin, rout, rk1, rk2, rks, rpk, rds;
-    __device__ __forceinline__ StepRes res() const { return StepRes{rin, rk1, rk2, rks, rpk, rds, tb.psi, mp, mn, m, vo}; }
-};
-
-// One party u of HbProd (mk-acc-xzw.cpp:245-270) fused with AddToAccXZW's
-// rotation and final add (xzw.cpp:336-344):
-//   uj_u = (FIRST ? 0 : acc_u) + sum_i NTT(g_i) * d_i,   g = SDD(iNTT(acc_u * (X^c - 1)))
-//   sv  += sum_i NTT(g_i) * P[u][i]
-// Party `index` is processed last (LAST): its lazy sum stays in registers
-// (`uj`, folded) and receives the f-part of HbProd before the single store.
-template <int DG, int METHOD, bool FIRST, bool LAST, int DS = 0>
-__device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_t (&sv)[kRegs],
-                                           uint64_t (&uj)[kRegs]) {
-    using Bd = Bounds<DG, METHOD, FIRST>;
-    const uint32_t Q = s.m.Q, polyB = kN * 4u;
-    uint32_t x[kRegs];
-#pragma unroll
-    for (int gq = 0; gq < 8; ++gq) {
-        const u32x4 t = aload4(s.rin, s.vo, u * polyB + gq * 1024u);
-        x[4 * gq] = t.x; x[4 * gq + 1] = t.y; x[4 * gq + 2] = t.z; x[4 * gq + 3] = t.w;
-    }
-    if (!FIRST) {
-        // acctemp = acc * (X^c - 1)                     (xzw.cpp:336-338)
-        // one Shoup product with the psi^e - 1 table entry: [0, 2Q) for any x;
-        // the 32 table reads are issued while the accumulator loads are in flight
-        uint2 mw[kRegs];
-#pragma unroll
-        for (int r = 0; r < kRegs; ++r) mw[r] = s.mp.at(s.tb.psi, r);
-        sched_fence();
-#pragma unroll
-        for (int r = 0; r < kRegs; ++r) x[r] = mul_shoup_lazy(x[r], mw[r], Q);
-    }
-    ntt_inv(x, s.lds, s.tw_inv, s.tb.twi, s.l, Q);
-    // SignedDigitDecompose (mk-acc.cpp:54-80): digit 1 -> x, digits 2.. packed
-    PackedDigits<DG> pd;
-#pragma unroll
-    for (int r = 0; r < kRegs; ++r) {
-        x[r] = pd.put(r, sdd_offset(x[r], s.sd), s.sd);
-        if ((r & 7) == 7) sched_fence();
-    }
-    const StepRes sr = s.res();
-    {
-        const DigitMac<DG, METHOD, FIRST, true, DS> mac(sr, 0, u);
-        KeyGroup kg[mac.kBuf];
-        ntt_fwd(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, s.l, Q, s.m.m1);
-        digit_range<DG>(x, Q);
-        // MKACC_DSCR_WAIT=1: the d_i scratch stores of the first pass are waited for
-        // here, just before the first reload, instead of right after that pass
-        if (DS == 2 && MKACC_DSCR_WAIT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-        for (int j = 0; j < mac.kPrefetch; ++j) mac.issue(kg[j], j);
-        mac.run(x, uj, sv, kg);
-    }
-#pragma unroll 1
-    for (int i = 1; i < DG; ++i) {
-#pragma unroll
-        for (int r = 0; r < kRegs; ++r) x[r] = pd.get(r, i + 1, s.sd);
-        const DigitMac<DG, METHOD, FIRST, false, DS> mac(sr, i, u);
-        KeyGroup kg[mac.kBuf];
-        ntt_fwd(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, s.l, Q, s.m.m1);
-        digit_range<DG>(x, Q);
-#pragma unroll
-        for (int j = 0; j < mac.kPrefetch; ++j) mac.issue(kg[j], j);
-        mac.run(x, uj, sv, kg);
-    }
-    if (LAST) {
-        // the index party's sum continues into the f-part (step_body)
-#pragma unroll
-        for (int r = 0; r < kRegs; ++r) uj[r] = fold64(uj[r], s.m.r32);
-        return;
-    }
-    // acc_u <- redc(uj_u) (+ acc_u when it is not in the sum), in [0, 2Q)
-#pragma unroll
-    for (int gq = 0; gq < 8; ++gq) {
-        u32x4 t;
-        if constexpr (!Bd::kAccInSum && !FIRST) t = aload4(s.rin, s.vo, u * polyB + gq * 1024u);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const int r = 4 * gq + e;
-            uint32_t v = redc(uj[r], Q, s.m.qinv);
-            if constexpr (!Bd::kAccInSum && !FIRST) {
-                v += t[e];
-                v = min(v, v - 2u * Q);
-            }
-            t[e] = v;
-        }
-        bstore4(t, s.rout, s.vo, u * polyB + gq * 1024u);
-    }
-}
-
-template <int DG, int METHOD, bool FIRST, bool DSCR>
-__device__ __forceinline__ void step_body(const StepCtx& s, uint32_t k, uint32_t index);
-template <int DG, int METHOD, bool FIRST>
-__device__ __forceinline__ void f_part(const StepCtx& s, uint32_t index, uint64_t (&w)[kRegs], uint32_t (&x)[kRegs]);
-
-// DSCR: d_i computed once per step and gate (first party pass) and reloaded from
-// a.dscr by the other k - 1 passes (DigitMac DS); the host picks it by k.
-template <int DG, int METHOD, bool FIRST, bool DSCR = false>
-__global__ __launch_bounds__(kThreads, 2) void mk_step_kernel(StepArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    load_image(smem, a.img);
-    const uint32_t l = threadIdx.x & 63u;
-    // wave-uniform (SGPR) gate index: the per-gate buffer descriptors must be
-    // scalar, otherwise every load through them becomes a waterfall loop
-    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t gate = blockIdx.x * kWavesPerBlock + wv;
-    if (gate >= a.B) return;
-    const uint32_t c = __builtin_amdgcn_readfirstlane(a.cvals[gate]);
-    const uint32_t cneg = (2u * kN - c) & (2u * kN - 1u);
-    const uint32_t k = a.k;
-    const uint32_t polyB = kN * 4u;
-    const StepCtx s{tables(smem, a.img),
-                    smem + kLdsTabWords + wv * kLdsWords,
-                    a.tw_fwd,
-                    a.tw_inv,
-                    a.m,
-                    a.sd,
-                    make_mono(c, l),
-                    // X^-c in the first step; X^(N-c) = -X^-c in the later XZW steps (key_eff)
-                    make_mono(FIRST || METHOD != XZW ? cneg : (cneg + kN) & (2u * kN - 1u), l),
-                    l,
-                    l * 16u,
-                    make_rsrc(a.acc_in + (size_t)gate * k * kN, k * polyB),
-                    make_rsrc(a.acc_out + (size_t)gate * k * kN, k * polyB),
-                    make_rsrc(a.key1, DG * 2 * polyB),
-                    make_rsrc(a.key2, DG * 2 * polyB),
-                    make_rsrc(a.keys, DG * 2 * polyB),
-                    make_rsrc(a.pkey, k * DG * polyB),
-                    make_rsrc(DSCR ? a.dscr + (size_t)gate * DG * kN : a.acc_in, DSCR ? DG * polyB : 0u)};
-    step_body<DG, METHOD, FIRST, DSCR>(s, k, a.index);
-}
-
-// Small batches (host: use_lat): one workgroup per gate and one wave per party,
-// so the k party passes of a step run concurrently and only the f-part is
-// serial -- 2 (dg + 1) transforms on a step's critical path instead of
-// (k + 1)(dg + 1).  The same party_pass / f_part code as mk_step_kernel: each
-// wave's sumV covers its own party; it is reduced to [0, 2Q), summed through
-// LDS by the wave of party `index`, which then runs the f-part alone (the
-// sums are exact mod Q, so the grouping is bit-exact).
-constexpr uint32_t kLatMaxK = 8;
-constexpr size_t lat_lds_bytes(uint32_t k) { return (size_t)(kLdsTabWords + k * kLdsWords) * 4; }
-template <int DG, int METHOD, bool FIRST>
-__global__ __launch_bounds__(64 * kLatMaxK, 1) void mk_lat_kernel(StepArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    load_image(smem, a.img);
-    const uint32_t l = threadIdx.x & 63u;
-    const uint32_t u = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // this wave's party
-    const uint32_t gate = blockIdx.x;
-    const uint32_t c = __builtin_amdgcn_readfirstlane(a.cvals[gate]);
-    const uint32_t cneg = (2u * kN - c) & (2u * kN - 1u);
-    const uint32_t k = a.k, index = a.index;
-    const uint32_t polyB = kN * 4u;
-    uint32_t* scratch = smem + kLdsTabWords + u * kLdsWords;
-    const StepCtx s{tables(smem, a.img),
-                    scratch,
-                    a.tw_fwd,
-                    a.tw_inv,
-                    a.m,
-                    a.sd,
-                    make_mono(c, l),
-                    make_mono(FIRST || METHOD != XZW ? cneg : (cneg + kN) & (2u * kN - 1u), l),
-                    l,
-                    l * 16u,
-                    make_rsrc(a.acc_in + (size_t)gate * k * kN, k * polyB),
-                    make_rsrc(a.acc_out + (size_t)gate * k * kN, k * polyB),
-                    make_rsrc(a.key1, DG * 2 * polyB),
-                    make_rsrc(a.key2, DG * 2 * polyB),
-                    make_rsrc(a.keys, DG * 2 * polyB),
-                    make_rsrc(a.pkey, k * DG * polyB),
-                    make_rsrc(a.acc_in, 0u)};
-    const uint32_t Q = s.m.Q;
-    uint64_t sv[kRegs], w[kRegs];
-#pragma unroll
-    for (int r = 0; r < kRegs; ++r) sv[r] = 0;
-    if (u == index)
-        party_pass<DG, METHOD, FIRST, true>(s, u, sv, w);
-    else
-        party_pass<DG, METHOD, FIRST, false>(s, u, sv, w);
-    // this party's sumV share, [0, 2Q), into the wave's own (now idle) scratch
-#pragma unroll
-    for (int r = 0; r < kRegs; ++r) scratch[r * 64 + l] = redc(sv[r], Q, s.m.qinv);
-    // redc's multiply-add is inline asm that writes its carry-out to VCC; hipcc
-    // does not count it as a VALU write of VCC and computed the branch below with
-    // an SALU write of VCC on the very next instruction.  The late VALU write
-    // could land after it, zero VCC and send every wave down the index-party path
-    // (intermittent wrong acc[index]; tools/isa_audit.py checks the distance).
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_nop 7" ::: "vcc");
-    __builtin_amdgcn_sched_barrier(0);
-    __syncthreads();
-    if (u != index) return;
-    uint32_t x[kRegs];
-#pragma unroll
-    for (int r = 0; r < kRegs; ++r) {
-        uint32_t v = 0;
-        for (uint32_t p = 0; p < k; ++p) v += smem[kLdsTabWords + p * kLdsWords + r * 64 + l];   // < 16 Q
-        v = min(v, v - 8u * Q);
-        v = min(v, v - 4u * Q);
-        x[r] = min(v, v - 2u * Q);                                                               // [0, 2Q)
-    }
-    f_part<DG, METHOD, FIRST>(s, index, w, x);
-}
-
-// One accumulator step for one gate per wavefront.
-//   FIRST:  AddToAccXZW0 (mk-acc-xzw.cpp:347-381 / xzw_B.cpp:333-381): acc <- HbProd(acc)
-//   else:   AddToAccXZW  (mk-acc-xzw.cpp:292-345 / xzw_B.cpp:281-330):
-//           acc <- acc + HbProd(acc * (X^c - 1))
-// HbProd is mk-acc-xzw.cpp:231-290, register resident: the per-slot sums
-// uj_u = sum_i g_i d_i, sumV = sum_u sum_i g_i P[u][i] and w = sum_i h_i f_i are
-// lazy 64-bit accumulators (v_mad_u64_u32) reduced once (Montgomery); all sums
-// are exact mod Q, so the reordering (parties in the order index+1, ..., index)
-// is bit-exact.
-template <int DG, int METHOD, bool FIRST, bool DSCR>
-__device__ __forceinline__ void step_body(const StepCtx& s, uint32_t k, uint32_t index) {
-    using Bd = Bounds<DG, METHOD, FIRST>;
-    const uint32_t Q = s.m.Q;
-    uint64_t sv[kRegs];
-#pragma unroll
-    for (int r = 0; r < kRegs; ++r) sv[r] = 0;
-    uint64_t w[kRegs];
-    // sumV grows by kSvParty (units of Q^2) per party; fold it before it could
-    // pass 32 (fold64 leaves < 2)
-    int svb = 0;
-    auto grow_sv = [&]() {
-        svb += Bd::kSvParty;
-        if (svb + Bd::kSvParty > 32) {
-#pragma unroll
-            for (int r = 0; r < kRegs; ++r) sv[r] = fold64(sv[r], s.m.r32);
-            svb = 2;
-        }
-    };
-    uint32_t t0 = 1;
-    if constexpr (DSCR) {   // k >= 2 (host: use_dscr)
-        party_pass<DG, METHOD, FIRST, false, 1>(s, index + 1 < k ? index + 1 : 0, sv, w);
-        grow_sv();
-        t0 = 2;
-        // the scratch stores complete before the later passes read them back
-        if (!MKACC_DSCR_WAIT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    for (uint32_t t = t0; t < k; ++t) {
-        party_pass<DG, METHOD, FIRST, false, DSCR ? 2 : 0>(s, index + t < k ? index + t : index + t - k, sv, w);
-        grow_sv();
-    }
-    party_pass<DG, METHOD, FIRST, true, DSCR ? 2 : 0>(s, index, sv, w);
-    uint32_t x[kRegs];
-#pragma unroll
-    for (int r = 0; r < kRegs; ++r) x[r] = redc(sv[r], Q, s.m.qinv);
-    f_part<DG, METHOD, FIRST>(s, index, w, x);
-}
-
-// Second half of HbProd for party `index` (mk-acc-xzw.cpp:272-289) and the
-// final store of acc[index]: w = its folded party sum (party_pass LAST),
-// x = sumV in [0, 2Q).  iNTT(sumV) -> SDD -> NTT -> acc[index] += <., f>.
-template <int DG, int METHOD, bool FIRST>
-__device__ __forceinline__ void f_part(const StepCtx& s, uint32_t index, uint64_t (&w)[kRegs], uint32_t (&x)[kRegs]) {
-    using Bd = Bounds<DG, METHOD, FIRST>;
-    const uint32_t Q = s.m.Q;
-    const uint32_t l = s.l;
-    const uint32_t polyB = kN * 4u;
-    if constexpr (!Bd::kAccInSum && !FIRST) {
-        // acc[index] joins the f-part sum (Bounds: < 4 Q^2 with the folded party sum)
-#pragma unroll
-        for (int gq = 0; gq < 8; ++gq) {
-            const u32x4 t = aload4(s.rin, s.vo, index * polyB + gq * 1024u);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) w[4 * gq + e] = mad64(t[e], s.m.r32, w[4 * gq + e]);
-        }
-    }
-
-    const StepRes sr = s.res();
-    ntt_inv(x, s.lds, s.tw_inv, s.tb.twi, l, Q);
-    PackedDigits<DG> pd;
-#pragma unroll
-    for (int r = 0; r < kRegs; ++r) {
-        x[r] = pd.put(r, sdd_offset(x[r], s.sd), s.sd);
-        if ((r & 7) == 7) sched_fence();
-    }
-    constexpr bool kSplit = METHOD == XZW && !FIRST;
-    uint64_t w2[kSplit ? kRegs : 1];
-    if constexpr (kSplit) {
-#pragma unroll
-        for (int r = 0; r < kRegs; ++r) w2[r] = 0;
-    }
-#pragma unroll 1
-    for (int i = 0; i < DG; ++i) {
-        if (i > 0) {
-#pragma unroll
-            for (int r = 0; r < kRegs; ++r) x[r] = pd.get(r, i + 1, s.sd);
-        }
-        if constexpr (kSplit) {
-            const SplitMac<DG> mac(sr, i);
-            KeyGroup kg[mac.kBuf];
-            ntt_fwd(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, l, Q, s.m.m1);
-            digit_range<DG>(x, Q);
-#pragma unroll
-            for (int j = 0; j < mac.kPrefetch; ++j) mac.issue(kg[j], j);
-            mac.run(x, w, w2, kg);
-        } else {
-            ntt_fwd(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, l, Q, s.m.m1);
-            digit_range<DG>(x, Q);
-            mac_index<DG, METHOD, FIRST>(x, i, w, s.rk1, s.rk2, s.rks, s.tb.psi, s.mp, s.mn, s.vo, Q);
-        }
-    }
-    const uint32_t ioff = index * polyB;
-    uint2 mw[kSplit ? kRegs : 1];
-    if constexpr (kSplit) {
-#pragma unroll
-        for (int r = 0; r < kRegs; ++r) mw[r] = s.mn.at(s.tb.psi, r);
-    }
-#pragma unroll
-    for (int gq = 0; gq < 8; ++gq) {
-        u32x4 t;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const int r = 4 * gq + e;
-            uint32_t v = redc(w[r], Q, s.m.qinv);                                   // [0, 2Q)
-            if constexpr (kSplit) {
-                // + (X^(N-c) - 1) * sum_i h_i ev2'_i
-                v += mul_shoup_lazy(redc(w2[r], Q, s.m.qinv), mw[r], Q);             // [0, 4Q)
-                v = min(v, v - 2u * Q);
-            }
-            t[e] = v;
-        }
-        bstore4(t, s.rout, s.vo, ioff + gq * 1024u);
-    }
-}
-
-// ---- batch prologue / epilogue kernels --------------------------------------
-
-// c = floor(ct * 2N / q) (mk-acc-xzw.cpp:110,125) or c = ct (mk-acc-xzw_B.cpp:119,124),
-// with c == 2N mapped to 0 (xzw.cpp:301).  Output layout [k*n][B].
-// Device entry points validate their inputs where a kernel reads them anyway:
-// a word outside its range raises the context's `bad` flag (reported by
-// mkacc_sync as MKACC_E_RANGE); the monomial exponent stays masked to [0, 2N).
-__global__ void prep_c_kernel(const uint32_t* __restrict__ ct, uint32_t* __restrict__ cvals, uint32_t B,
-                              uint32_t kn, uint32_t method, uint32_t q, uint32_t* __restrict__ bad) {
-    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= (size_t)B * kn) return;
-    const uint32_t s = (uint32_t)(idx / B), b = (uint32_t)(idx % B);
-    const uint32_t raw = ct[(size_t)b * kn + s];
-    if (raw >= (method == XZW ? q : 2u * kN + 1u)) *bad = 1u;   // XZW_B: c <= 2N (2N -> 0)
-    uint32_t c = method == XZW ? (uint32_t)(((uint64_t)raw * (2u * kN)) / q) : raw;
-    if (c >= 2u * kN) c -= 2u * kN;
-    cvals[idx] = c;
-}
-
-// reference EVAL order -> C4, multiplied by a constant (N^-1 on the way in, N on the way out)
-__global__ void eval_to_c4_kernel(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, size_t npoly,
-                                  uint32_t s, uint32_t sp, uint32_t Q, uint32_t* __restrict__ bad) {
-    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= npoly * kN) return;
-    const size_t p = idx / kN;
-    const uint32_t j = (uint32_t)(idx % kN);
-    const uint32_t x = in[idx];
-    if (bad && x >= Q) *bad = 1u;
-    out[p * kN + c4_index(j)] = mul_shoup(x, s, sp, Q);
-}
-
-// Key upload from device memory: reference layout [k][nk][n+1][dg][2][N] (EVAL,
-// u32 or u64 words) -> device layout [k][n+1][nk][dg][2][N] in C4 order, times
-// N^-1 2^32 (s, sp; StepArgs).  MKNTRU (nk = 2): the ev1 words of the steps i < n
-// become ev1 + ev2.  pkey [k][dg][N] is the same map with nk = n1 = 1.
-template <typename W>
-__global__ void key_layout_kernel(const W* __restrict__ src, uint32_t* __restrict__ dst, size_t npolys, uint32_t nk,
-                                  uint32_t n1, uint32_t dg2, uint32_t Q, uint32_t s, uint32_t sp,
-                                  uint32_t* __restrict__ bad) {
-    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= npolys * kN) return;
-    size_t p = idx / kN;
-    const uint32_t j = (uint32_t)(idx % kN);
-    const uint32_t dp = (uint32_t)(p % dg2); p /= dg2;
-    const uint32_t i = (uint32_t)(p % n1); p /= n1;
-    const uint32_t jj = (uint32_t)(p % nk);
-    const size_t u = p / nk;
-    const size_t dpoly = ((u * n1 + i) * nk + jj) * dg2 + dp;
-    const uint64_t x = (uint64_t)src[idx];
-    if (x >= Q) *bad = 1u;
-    uint32_t v = (uint32_t)x;
-    if (nk == 2 && jj == 0 && i + 1 < n1) {
-        // ev1 + ev2 (the ev2 word is range-checked by its own thread)
-        const uint64_t y = (uint64_t)src[idx + (size_t)n1 * dg2 * kN];
-        v = (uint32_t)((x + (y < Q ? y : 0)) % Q);
-    }
-    dst[dpoly * kN + c4_index(j)] = mul_shoup(v, s, sp, Q);
-}
-__global__ void c4_to_eval_kernel(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, size_t npoly,
-                                  uint32_t s, uint32_t sp, uint32_t Q) {
-    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= npoly * kN) return;
-    const size_t p = idx / kN;
-    const uint32_t j = (uint32_t)(idx % kN);
-    out[idx] = mul_shoup(in[p * kN + c4_index(j)], s, sp, Q);
-}
-
-// ---- primitive kernels (parity tests of the NTT / SDD building blocks) -------
-
-__global__ __launch_bounds__(kThreads) void ntt_fwd_kernel(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
-                                                            uint32_t count, const uint32_t* img, const uint2* twf,
-                                                            uint32_t Q, uint32_t m1) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    load_image(smem, img);
-    const Tables tb = tables(smem, img);
-    const uint32_t l = threadIdx.x & 63u, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t p = blockIdx.x * kWavesPerBlock + wv;
-    if (p >= count) return;
-    const uint32_t* src = in + (size_t)p * kN;
-    uint32_t x[kRegs];
-#pragma unroll
-    for (int r = 0; r < kRegs; ++r) x[r] = src[jA(l, r)];
-    ntt_fwd(x, smem + kLdsTabWords + wv * kLdsWords, twf, tb.twf, tb.twfc, l, Q, m1);
-    uint32_t* dst = out + (size_t)p * kN;
-#pragma unroll
-    for (int r = 0; r < kRegs; ++r) dst[jC(l, r)] = canon4(x[r], Q);
-}
-
-__global__ __launch_bounds__(kThreads) void ntt_inv_kernel(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
-                                                            uint32_t count, const uint32_t* img, const uint2* twi,
-                                                            uint32_t Q, uint32_t ninv, uint32_t ninvp) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    load_image(smem, img);
-    const Tables tb = tables(smem, img);
-    const uint32_t l = threadIdx.x & 63u, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t p = blockIdx.x * kWavesPerBlock + wv;
-    if (p >= count) return;
-    const uint32_t* src = in + (size_t)p * kN;
-    uint32_t x[kRegs];
-#pragma unroll
-    for (int r = 0; r < kRegs; ++r) x[r] = src[jC(l, r)];
-    ntt_inv(x, smem + kLdsTabWords + wv * kLdsWords, twi, tb.twi, l, Q);
-    uint32_t* dst = out + (size_t)p * kN;
-#pragma unroll
-    for (int r = 0; r < kRegs; ++r) dst[jA(l, r)] = mul_shoup(x[r], ninv, ninvp, Q);
-}
-
-// SignedDigitDecompose through the same offset-word digits the step kernel
-// feeds its NTTs, reduced to the reference's canonical residues.
-__global__ void sdd_kernel(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint32_t count, uint32_t dg,
-                           uint32_t Q, SddConsts sd) {
-    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= (size_t)count * kN) return;
-    const size_t p = idx / kN, j = idx % kN;
-    const uint32_t D = sdd_offset(in[idx], sd);
-    for (uint32_t i = 0; i < dg; ++i) {
-        const uint32_t v = sdd_digit(D, i + 1, sd);
-        out[(p * dg + i) * kN + j] = v >= Q ? v - Q : v;
-    }
-}
-
-// ---- kernel table -------------------------------------------------------------
-
-using StepFn = void (*)(StepArgs);
-
-template <int DG>
-StepFn pick_step(int method, bool first, bool dscr) {
-    if (method == XZW) {
-        if (first) return mk_step_kernel<DG, XZW, true>;
-        return dscr ? mk_step_kernel<DG, XZW, false, true> : mk_step_kernel<DG, XZW, false>;
-    }
-    return first ? mk_step_kernel<DG, XZW_B, true> : mk_step_kernel<DG, XZW_B, false>;
-}
-
-StepFn step_fn(int dg, int method, bool first, bool dscr);
-
-template <int DG>
-StepFn pick_lat(int method, bool first) {
-    if (method == XZW) return first ? mk_lat_kernel<DG, XZW, true> : mk_lat_kernel<DG, XZW, false>;
-    return first ? mk_lat_kernel<DG, XZW_B, true> : mk_lat_kernel<DG, XZW_B, false>;
-}
-StepFn lat_fn(int dg, int method, bool first);
-
 }  // namespace
+
+#include "mkacc_kernels.hpp"
+
 
 #include "mkacc_gate.hpp"
 #include "mkacc_wide.hpp"
@@ -937,22 +87,30 @@ __global__ void wide_key_layout_kernel(const W* __restrict__ src, uint64_t* __re
 // returned null here for other digit counts and the launch of a null kernel
 // produced the segfault / all-wrong records of ab_l1, lat_l1 and ab_d1,
 // DESIGN.md s2; a null kernel is now refused at mkacc_create and launch.)
-StepFn step_fn(int dg, int method, bool first, bool dscr) {
+const void* step_fn(int dg, int method, bool first, bool dscr) {
     switch (dg) {
-        case 2: return pick_step<2>(method, first, dscr);
-        case 3: return pick_step<3>(method, first, dscr);
-        case 4: return pick_step<4>(method, first, dscr);
-        case 5: return pick_step<5>(method, first, dscr);
+        case 2: return mkacc_tu::step_dg2(method, first, dscr);
+        case 3: return mkacc_tu::step_dg3(method, first, dscr);
+        case 4: return mkacc_tu::step_dg4(method, first, dscr);
+        case 5: return mkacc_tu::step_dg5(method, first, dscr);
         default: return nullptr;
     }
 }
-StepFn lat_fn(int dg, int method, bool first) {
+const void* lat_fn(int dg, int method, bool first) {
     switch (dg) {
-        case 2: return pick_lat<2>(method, first);
-        case 3: return pick_lat<3>(method, first);
-        case 4: return pick_lat<4>(method, first);
+        case 2: return mkacc_tu::lat_dg2(method, first);
+        case 3: return mkacc_tu::lat_dg3(method, first);
+        case 4: return mkacc_tu::lat_dg4(method, first);
         default: return nullptr;
     }
+}
+
+// launch of a kernel reached through the mkacc_tu table (one by-value argument);
+// a launch error is left for the caller's hipGetLastError
+template <class A>
+void launch_ptr(const void* fn, dim3 grid, dim3 block, size_t lds, hipStream_t s, A a) {
+    void* args[] = {&a};
+    (void)hipLaunchKernel(fn, grid, block, args, lds, s);
 }
 
 // Key-switching keys from device memory (mkacc_upload_ksk_*_device): the host
@@ -1162,13 +320,13 @@ uint32_t* launch_steps(mkacc_ctx* c, size_t B) {
             a.dscr = c->d_dscr;
             // a null kernel must never reach hipLaunchKernelGGL (mkacc_create checks the set)
             if (lat) {
-                const StepFn fn = lat_fn((int)c->dg, c->method_class, first);
+                const void* fn = lat_fn((int)c->dg, c->method_class, first);
                 if (!fn) return nullptr;
-                hipLaunchKernelGGL(fn, dim3((unsigned)B), dim3(64 * k), lat_lds_bytes(k), c->stream, a);
+                launch_ptr(fn, dim3((unsigned)B), dim3(64 * k), lat_lds_bytes(k), c->stream, a);
             } else {
-                const StepFn fn = step_fn((int)c->dg, c->method_class, first, !first && c->d_dscr != nullptr);
+                const void* fn = step_fn((int)c->dg, c->method_class, first, !first && c->d_dscr != nullptr);
                 if (!fn) return nullptr;
-                hipLaunchKernelGGL(fn, grid, block, lds, c->stream, a);
+                launch_ptr(fn, grid, block, lds, c->stream, a);
             }
             std::swap(cur, nxt);
         }
@@ -1611,10 +769,8 @@ int wide_launch_batch(mkacc_ctx* c, const uint32_t* d_ct, const uint64_t* d_in, 
                 a.C = c->wfC;
                 a.m = c->wfm;
                 a.sd = c->wsd;
-                void (*fn)(widefp::StepArgs);
-                if (c->method_class == XZW) fn = first ? widefp::step_kernel<XZW, true> : widefp::step_kernel<XZW, false>;
-                else fn = first ? widefp::step_kernel<XZW_B, true> : widefp::step_kernel<XZW_B, false>;
-                hipLaunchKernelGGL(fn, dim3((unsigned)B), dim3(widefp::kThreads), 0, c->stream, a);
+                launch_ptr(mkacc_tu::widefp_step(c->method_class, first), dim3((unsigned)B), dim3(widefp::kThreads), 0,
+                           c->stream, a);
                 std::swap(cur, nxt);
             }
         hipLaunchKernelGGL(widefp::to_canonical_kernel, g, dim3(256), 0, c->stream, cur, d_out, words, c->wfm);
@@ -1649,10 +805,8 @@ int wide_launch_batch(mkacc_ctx* c, const uint32_t* d_ct, const uint64_t* d_in, 
             a.ninvp = c->wninvp;
             a.m = c->wm;
             a.sd = c->wsd;
-            void (*fn)(wide::StepArgs);
-            if (c->method_class == XZW) fn = first ? wide::step_kernel<XZW, true> : wide::step_kernel<XZW, false>;
-            else fn = first ? wide::step_kernel<XZW_B, true> : wide::step_kernel<XZW_B, false>;
-            hipLaunchKernelGGL(fn, dim3((unsigned)B), dim3(wide::kThreads), 0, c->stream, a);
+            launch_ptr(mkacc_tu::wide_step(c->method_class, first), dim3((unsigned)B), dim3(wide::kThreads), 0, c->stream,
+                       a);
             std::swap(cur, nxt);
         }
     HIP_TRY(hipMemcpyAsync(d_out, cur, accb, hipMemcpyDeviceToDevice, c->stream));

@@ -1,0 +1,44 @@
+// mkacc_steps.hip -- kernel translation units of the engine library.  The
+// build (mkfhe_amd/build.py) compiles this file once per unit, in parallel:
+//   -DMKACC_TU_DG=d -DMKACC_TU_PART=0   mk_step_kernel instantiations of digit count d
+//   -DMKACC_TU_DG=d -DMKACC_TU_PART=1   mk_lat_kernel instantiations of digit count d
+//   -DMKACC_TU_WIDE=1 / 2              64-bit word step kernels (integer / FP64)
+// and the host unit (mkacc_engine.hip) launches them through mkacc_tu.
+#include "mkacc_kernels.hpp"
+
+#if defined(MKACC_TU_WIDE)
+#include "mkacc_wide.hpp"
+#include "mkacc_widefp.hpp"
+namespace mkacc_tu {
+#if MKACC_TU_WIDE == 1
+KernelPtr wide_step(int method, bool first) {
+    if (method == XZW) return first ? (KernelPtr)wide::step_kernel<XZW, true> : (KernelPtr)wide::step_kernel<XZW, false>;
+    return first ? (KernelPtr)wide::step_kernel<XZW_B, true> : (KernelPtr)wide::step_kernel<XZW_B, false>;
+}
+#else
+KernelPtr widefp_step(int method, bool first) {
+    if (method == XZW)
+        return first ? (KernelPtr)widefp::step_kernel<XZW, true> : (KernelPtr)widefp::step_kernel<XZW, false>;
+    return first ? (KernelPtr)widefp::step_kernel<XZW_B, true> : (KernelPtr)widefp::step_kernel<XZW_B, false>;
+}
+#endif
+}  // namespace mkacc_tu
+
+#elif defined(MKACC_TU_DG)
+#define MKACC_CAT2(a, b) a##b
+#define MKACC_CAT(a, b) MKACC_CAT2(a, b)
+namespace mkacc_tu {
+#if MKACC_TU_PART == 0
+KernelPtr MKACC_CAT(step_dg, MKACC_TU_DG)(int method, bool first, bool dscr) {
+    return (KernelPtr)pick_step<MKACC_TU_DG>(method, first, dscr);
+}
+#else
+KernelPtr MKACC_CAT(lat_dg, MKACC_TU_DG)(int method, bool first) {
+    return (KernelPtr)pick_lat<MKACC_TU_DG>(method, first);
+}
+#endif
+}  // namespace mkacc_tu
+
+#else
+#error "mkacc_steps.hip is compiled with MKACC_TU_DG or MKACC_TU_WIDE (mkfhe_amd/build.py)"
+#endif

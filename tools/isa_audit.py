@@ -32,12 +32,30 @@ _VRANGE = re.compile(r"v\[(\d+):(\d+)\]|v(\d+)\b")
 
 
 def disassemble(lib: str) -> str:
+    """Disassembly of every gfx950 code object in the library: a library linked
+    from several translation units holds one offload bundle per unit,
+    concatenated in .hip_fatbin (each starts with the bundle magic)."""
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    out = []
     with tempfile.TemporaryDirectory() as d:
-        fat, obj = os.path.join(d, "fat.bin"), os.path.join(d, "code.o")
+        fat = os.path.join(d, "fat.bin")
         subprocess.check_call([f"{LLVM}/llvm-objcopy", "-O", "binary", "--only-section=.hip_fatbin", lib, fat])
-        subprocess.check_call([f"{LLVM}/clang-offload-bundler", "--type=o", "--unbundle", f"--input={fat}",
-                               f"--output={obj}", "--targets=hipv4-amdgcn-amd-amdhsa--gfx950"])
-        return subprocess.check_output([f"{LLVM}/llvm-objdump", "-d", "--no-show-raw-insn", obj], text=True)
+        blob = open(fat, "rb").read()
+        starts, i = [], blob.find(magic)
+        while i >= 0:
+            starts.append(i)
+            i = blob.find(magic, i + 1)
+        if not starts:
+            raise RuntimeError(f"{lib}: no offload bundle in .hip_fatbin")
+        for n, s in enumerate(starts):
+            e = starts[n + 1] if n + 1 < len(starts) else len(blob)
+            part, obj = os.path.join(d, f"b{n}.bin"), os.path.join(d, f"b{n}.o")
+            with open(part, "wb") as f:
+                f.write(blob[s:e])
+            subprocess.check_call([f"{LLVM}/clang-offload-bundler", "--type=o", "--unbundle", f"--input={part}",
+                                   f"--output={obj}", "--targets=hipv4-amdgcn-amd-amdhsa--gfx950"])
+            out.append(subprocess.check_output([f"{LLVM}/llvm-objdump", "-d", "--no-show-raw-insn", obj], text=True))
+    return "\n".join(out)
 
 
 def vregs(operand: str) -> set[int]:
