@@ -24,7 +24,7 @@ import sys
 _HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(_HERE)
 SOURCES = [os.path.join(_HERE, "csrc", f) for f in ("mkacc_engine.hip", "mkacc_steps.hip")]
-HEADERS = [os.path.join(_HERE, "csrc", f) for f in ("mkacc_kernels.hpp", "mkacc_device.hpp", "mkacc_host_math.hpp",
+HEADERS = [os.path.join(_HERE, "csrc", f) for f in ("mkacc_kernels.hpp", "mkacc_step2.hpp", "mkacc_device.hpp", "mkacc_host_math.hpp",
                                                     "mkacc_gate.hpp", "mkacc_wide.hpp", "mkacc_widefp.hpp")] + [
     os.path.join(ROOT, "include", "mkfhe_amd.h")]
 OUT = os.path.join(_HERE, "lib", "libmkfhe_amd.so")
@@ -91,6 +91,7 @@ def build_keys(force: bool = False, verbose: bool = False) -> str:
 UNITS = [("engine", "mkacc_engine.hip", [])] + [
     (f"step_dg{d}", "mkacc_steps.hip", [f"-DMKACC_TU_DG={d}", "-DMKACC_TU_PART=0"]) for d in (2, 3, 4, 5)] + [
     (f"lat_dg{d}", "mkacc_steps.hip", [f"-DMKACC_TU_DG={d}", "-DMKACC_TU_PART=1"]) for d in (2, 3, 4)] + [
+    (f"step2_dg{d}", "mkacc_steps.hip", [f"-DMKACC_TU_DG={d}", "-DMKACC_TU_PART=2"]) for d in (2, 3, 4)] + [
     ("wide", "mkacc_steps.hip", ["-DMKACC_TU_WIDE=1"]), ("widefp", "mkacc_steps.hip", ["-DMKACC_TU_WIDE=2"])]
 
 
@@ -101,8 +102,10 @@ def _jobs() -> int:
     return max(1, min(len(UNITS), os.cpu_count() or 1))
 
 
-def compile_engine(out: str, flags: list[str], report: str, verbose: bool = False) -> str:
-    """hipcc the engine units into `out` with extra `flags` (-D switches of A/B builds)."""
+def compile_engine(out: str, flags: list[str], report: str, verbose: bool = False, only=None) -> str:
+    """hipcc the engine units into `out` with extra `flags` (-D switches of A/B builds).
+    only: names of the units to compile with the flags; the others are linked from
+    the default build's objects (an A/B variant of one kernel family)."""
     from concurrent.futures import ThreadPoolExecutor
 
     os.makedirs(os.path.dirname(out), exist_ok=True)
@@ -123,8 +126,13 @@ def compile_engine(out: str, flags: list[str], report: str, verbose: bool = Fals
         r = subprocess.run(cmd, capture_output=True, text=True)
         return name, obj, r
 
+    units = UNITS if only is None else [u for u in UNITS if u[0] in only]
     with ThreadPoolExecutor(max_workers=_jobs()) as ex:
-        results = list(ex.map(unit, UNITS))
+        results = list(ex.map(unit, units))
+    if only is not None:
+        base = OUT[:-3] + ".objs"
+        results += [(u[0], os.path.join(base, u[0] + ".o"), subprocess.CompletedProcess([], 0, "", ""))
+                    for u in UNITS if u[0] not in only]
     # per-kernel VGPR / spill / occupancy report next to the library
     with open(report, "w") as rep:
         for name, _, r in results:
@@ -148,15 +156,24 @@ def build(force: bool = False, verbose: bool = False) -> str:
     return compile_engine(OUT, [], os.path.join(os.path.dirname(OUT), "resource_usage.txt"), verbose)
 
 
-def build_variant(name: str, flags: list[str], verbose: bool = False) -> str:
-    """An A/B build of the engine with extra -D switches: lib/variants/NAME.so."""
+def build_variant(name: str, flags: list[str], verbose: bool = False, only=None) -> str:
+    """An A/B build of the engine with extra -D switches: lib/variants/NAME.so
+    (only: recompile just these units, the rest from the default build)."""
+    if only is not None:
+        build()
     out = os.path.join(_HERE, "lib", "variants", name + ".so")
-    return compile_engine(out, flags, out[:-3] + ".res", verbose)
+    return compile_engine(out, flags, out[:-3] + ".res", verbose, only)
 
 
 if __name__ == "__main__":
     if "--variant" in sys.argv:
-        i = sys.argv.index("--variant")
-        print(build_variant(sys.argv[i + 1], sys.argv[i + 2:], verbose=True))
+        args = list(sys.argv[1:])
+        only = None
+        if "--units" in args:
+            j = args.index("--units")
+            only = args[j + 1].split(",")
+            del args[j:j + 2]
+        i = args.index("--variant")
+        print(build_variant(args[i + 1], args[i + 2:], verbose=True, only=only))
     else:
         print(build(force="--force" in sys.argv, verbose=True))

@@ -105,10 +105,17 @@ __device__ __forceinline__ uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {
 // is used the compiler narrows C++ to v_mul_lo_u32 + v_add_u32; the 64-bit
 // form does both in one issue slot (tools/ubench_isa.hip: all three cost about
 // the same).  SB: b is wave-uniform (SGPR operand).  Carry-out goes to VCC.
+// gfx950 needs a wait state between a VALU that writes an SGPR (this carry-out)
+// and a VALU that reads any SGPR: with a wave-uniform b in an SGPR, hipcc puts an
+// s_nop 0 between back-to-back multiply-adds.  MKACC_PIN_VB=1 takes b from a VGPR
+// (the compiler keeps a VGPR copy of the loop-invariant constant).
+#ifndef MKACC_PIN_VB
+#define MKACC_PIN_VB 0
+#endif
 template <bool SB>
 __device__ __forceinline__ uint64_t mad64_pin(uint32_t a, uint32_t b, uint64_t c) {
     uint64_t r;
-    if constexpr (SB)
+    if constexpr (SB && !MKACC_PIN_VB)
         asm("v_mad_u64_u32 %0, vcc, %1, %2, %3" : "=v"(r) : "v"(a), "s"(b), "v"(c) : "vcc");
     else
         asm("v_mad_u64_u32 %0, vcc, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c) : "vcc");
@@ -117,7 +124,7 @@ __device__ __forceinline__ uint64_t mad64_pin(uint32_t a, uint32_t b, uint64_t c
 template <bool SB>
 __device__ __forceinline__ uint64_t mul64_pin(uint32_t a, uint32_t b) {
     uint64_t r;
-    if constexpr (SB)
+    if constexpr (SB && !MKACC_PIN_VB)
         asm("v_mad_u64_u32 %0, vcc, %1, %2, 0" : "=v"(r) : "v"(a), "s"(b) : "vcc");
     else
         asm("v_mad_u64_u32 %0, vcc, %1, %2, 0" : "=v"(r) : "v"(a), "v"(b) : "vcc");

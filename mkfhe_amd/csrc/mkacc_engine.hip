@@ -87,7 +87,29 @@ __global__ void wide_key_layout_kernel(const W* __restrict__ src, uint64_t* __re
 // returned null here for other digit counts and the launch of a null kernel
 // produced the segfault / all-wrong records of ab_l1, lat_l1 and ab_d1,
 // DESIGN.md s2; a null kernel is now refused at mkacc_create and launch.)
-const void* step_fn(int dg, int method, bool first, bool dscr) {
+// Batch step kernel generation: 2 = mk_step2_kernel (mkacc_step2.hpp, digit NTTs
+// first, one key stream per pass; built for dg <= 4), 1 = mk_step_kernel (every
+// digit count).  Default 2 for dg <= 3 (STD128_MKNTRU 163.8 -> 159.6 us per
+// launch, STD100_MKNTRU 132.6 -> 126.2, STD100_MKNTRU_LWE_2 187.4 -> 183.7),
+// 1 above (dg = 4, STD128_MKNTRU_3: 1191 against 1799 us for the spilling
+// step2 kernel).  MKACC_STEP=1/2 overrides where built; read once per context
+// (mkacc_ctx::step_ver), which sizes its workspace for that kernel.
+int step_version(int dg) {
+    if (dg > 4) return 1;
+    const char* e = std::getenv("MKACC_STEP");
+    if (e && (e[0] == '1' || e[0] == '2')) return e[0] - '0';
+    return dg <= 3 ? 2 : 1;
+}
+
+const void* step_fn(int dg, int method, bool first, bool dscr, int ver) {
+    if (ver == 2) {
+        switch (dg) {
+            case 2: return mkacc_tu::step2_dg2(method, first);
+            case 3: return mkacc_tu::step2_dg3(method, first);
+            case 4: return mkacc_tu::step2_dg4(method, first);
+            default: return nullptr;
+        }
+    }
     switch (dg) {
         case 2: return mkacc_tu::step_dg2(method, first, dscr);
         case 3: return mkacc_tu::step_dg3(method, first, dscr);
@@ -169,6 +191,7 @@ struct mkacc_ctx {
     int device = 0;
     int cus = 256;                // compute units of the device (mk_lat_kernel residency)
     int method_class = XZW;   // XZW or XZW_B
+    int step_ver = 1;         // batch step kernel generation (step_version)
     uint32_t dg = 0, nk = 0;
     Mod mod{};
     SddConsts sd{};
@@ -186,7 +209,7 @@ struct mkacc_ctx {
     uint32_t* d_acc0 = nullptr;
     uint32_t* d_acc1 = nullptr;
     uint32_t* d_cvals = nullptr;
-    uint32_t* d_dscr = nullptr;   // [B][dg][N] d_i scratch (use_dscr), sized with the workspace
+    uint32_t* d_dscr = nullptr;   // per-gate step scratch, sized with the workspace (step_scratch_words)
     // host-pointer API staging
     size_t io_B = 0;
     uint32_t* d_ct = nullptr;
@@ -248,7 +271,7 @@ const uint32_t* key_step(const mkacc_ctx* c, uint32_t u, uint32_t i, uint32_t j)
 // MKACC_DSCR=0/1 overrides.
 constexpr uint32_t kDscrMinK = 4;
 bool use_dscr(const mkacc_ctx* c) {
-    if (c->method_class != XZW || c->p.k < 2) return false;
+    if (c->method_class != XZW || c->p.k < 2 || c->step_ver != 1) return false;
     const char* e = std::getenv("MKACC_DSCR");
     if (e && *e) return e[0] != '0';
     return c->p.k >= kDscrMinK;
@@ -268,6 +291,15 @@ bool use_lat(const mkacc_ctx* c, size_t B) {
     return B <= (size_t)c->cus * (kLdsPerCu / lat_lds_bytes(c->p.k));
 }
 
+// Per-gate scratch words of the batch step kernel: mk_step_kernel DSCR keeps the
+// step's d_i ([dg][N]); mk_step2_kernel keeps sumV between the party passes ([N],
+// Step2Cfg::kSvMem).
+size_t step_scratch_words(const mkacc_ctx* c) {
+    if (use_dscr(c)) return (size_t)c->dg * kN;
+    if (c->step_ver == 2) return kN;
+    return 0;
+}
+
 int ensure_ws(mkacc_ctx* c, size_t B) {
     if (B <= c->ws_B) return MKACC_OK;
     if (c->d_acc0) HIP_TRY(hipFree(c->d_acc0));
@@ -280,7 +312,7 @@ int ensure_ws(mkacc_ctx* c, size_t B) {
     HIP_TRY(hipMalloc(&c->d_acc0, accw * 4));
     HIP_TRY(hipMalloc(&c->d_acc1, accw * 4));
     HIP_TRY(hipMalloc(&c->d_cvals, B * c->p.k * (size_t)c->p.n * 4));
-    if (use_dscr(c)) HIP_TRY(hipMalloc(&c->d_dscr, B * c->dg * (size_t)kN * 4));
+    if (const size_t sw = step_scratch_words(c)) HIP_TRY(hipMalloc(&c->d_dscr, B * sw * 4));
     c->ws_B = B;
     return MKACC_OK;
 }
@@ -324,7 +356,7 @@ uint32_t* launch_steps(mkacc_ctx* c, size_t B) {
                 if (!fn) return nullptr;
                 launch_ptr(fn, dim3((unsigned)B), dim3(64 * k), lat_lds_bytes(k), c->stream, a);
             } else {
-                const void* fn = step_fn((int)c->dg, c->method_class, first, !first && c->d_dscr != nullptr);
+                const void* fn = step_fn((int)c->dg, c->method_class, first, !first && use_dscr(c), c->step_ver);
                 if (!fn) return nullptr;
                 launch_ptr(fn, grid, block, lds, c->stream, a);
             }
@@ -919,7 +951,7 @@ const char* mkacc_build_info(void) {
     static const std::string info = [] {
         std::string dgs;
         for (int dg = 2; dg <= 5; ++dg)
-            if (step_fn(dg, XZW, true, false) && step_fn(dg, XZW_B, false, false))
+            if (step_fn(dg, XZW, true, false, step_version(dg)) && step_fn(dg, XZW_B, false, false, step_version(dg)))
                 dgs += (dgs.empty() ? "" : ",") + std::to_string(dg);
         return "abi=" + std::to_string(MKACC_ABI_VERSION) + ";header=" MKACC_HEADER_ID ";source=" MKACC_SOURCE_ID
                ";dg=" + dgs + ";flags=" MKACC_BUILD_FLAGS;
@@ -992,9 +1024,10 @@ int mkacc_create(const mkacc_params* pin, int device, mkacc_ctx** out) {
     }
     c->method_class = p.method == MKACC_METHOD_MKNTRU ? XZW : XZW_B;
     c->dg = dg;
+    c->step_ver = step_version((int)dg);
     c->nk = c->method_class == XZW ? 2 : 1;
     c->wide = wide;
-    if (!wide && !step_fn((int)dg, c->method_class, true, false))
+    if (!wide && !step_fn((int)dg, c->method_class, true, false, c->step_ver))
         return fail(MKACC_E_UNSUPPORTED, "this build has no step kernel for dg = " + std::to_string(dg));
     if (wide) {
         HIP_TRY(hipSetDevice(device));

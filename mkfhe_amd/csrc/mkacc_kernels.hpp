@@ -863,6 +863,14 @@ StepFn pick_step(int method, bool first, bool dscr) {
 }
 
 
+#include "mkacc_step2.hpp"
+
+template <int DG>
+StepFn pick_step2(int method, bool first) {
+    if (method == XZW) return first ? mk_step2_kernel<DG, XZW, true> : mk_step2_kernel<DG, XZW, false>;
+    return first ? mk_step2_kernel<DG, XZW_B, true> : mk_step2_kernel<DG, XZW_B, false>;
+}
+
 template <int DG>
 StepFn pick_lat(int method, bool first) {
     if (method == XZW) return first ? mk_lat_kernel<DG, XZW, true> : mk_lat_kernel<DG, XZW, false>;
@@ -881,6 +889,9 @@ MKACC_TU_API KernelPtr step_dg2(int method, bool first, bool dscr);
 MKACC_TU_API KernelPtr step_dg3(int method, bool first, bool dscr);
 MKACC_TU_API KernelPtr step_dg4(int method, bool first, bool dscr);
 MKACC_TU_API KernelPtr step_dg5(int method, bool first, bool dscr);
+MKACC_TU_API KernelPtr step2_dg2(int method, bool first);   // mk_step2_kernel (mkacc_step2.hpp)
+MKACC_TU_API KernelPtr step2_dg3(int method, bool first);
+MKACC_TU_API KernelPtr step2_dg4(int method, bool first);
 MKACC_TU_API KernelPtr lat_dg2(int method, bool first);
 MKACC_TU_API KernelPtr lat_dg3(int method, bool first);
 MKACC_TU_API KernelPtr lat_dg4(int method, bool first);

@@ -1,0 +1,297 @@
+// mkacc_step2.hpp -- the batch step kernel, round-3 form (mk_step2_kernel).
+// Included inside mkacc_kernels.hpp's anonymous namespace.
+//
+// Same algebra as mk_step_kernel (HbProd, mk-acc-xzw.cpp:231-290, fused with
+// AddToAccXZW{,0}, xzw.cpp:292-381; every sum exact mod Q, so bit-exact), but
+// each of the k + 1 passes of a step runs its dg digit NTTs FIRST and keeps
+// their outputs G_i in registers, then makes ONE streaming pass over the key
+// words in which every slot's sums are short-lived temporaries:
+//
+//   party u:  G = NTT(SDD(iNTT(acc_u (X^c - 1))))
+//             acc'_u = acc_u + sum_i G_i ev1'_i + (X^(N-c) - 1) sum_i G_i ev2_i
+//             sv     = sv + sum_i G_i P[u][i]                 (32-bit between parties)
+//   f-part:   G = NTT(SDD(iNTT(sv)))
+//             acc'_index += sum_i G_i f1'_i + (X^(N-c) - 1) sum_i G_i f2_i
+//
+// Against mk_step_kernel this
+//   * drops the 64-bit per-slot sums that lived across the digit NTTs
+//     (uj and sumV: 128 VGPRs) for dg x 32 G registers, so the kernel runs
+//     without spills and with deeper key prefetch;
+//   * never forms d_i = ev1' + ev2 (X^(N-c) - 1) per slot and digit: the
+//     monomial product is applied once per slot to the reduced ev2 sum (the
+//     f-part's split form, now also for the parties): (dg - 1) fewer psi
+//     gathers and Shoup products per slot and party, and no per-gate d_i
+//     scratch at large k (mk_step_kernel DSCR);
+//   * runs the parties and the f-part through ONE copy of the transform code
+//     (k + 1 iterations of a rolled loop; the index party's output goes to
+//     acc_out and the f-part reads it back), (dg + 1) NTTs of code instead of
+//     2 (dg + 1) + 1.
+// The first (KDM) step and XZW_B form the per-slot effective key inline
+// (key_eff, one sum), as mk_step_kernel does.
+#pragma once
+
+template <int GS>
+struct VecLd;
+// cache policy of the accumulator stores (aux; 16 = sc1: the line leaves the XCD's L2,
+// MI355X_MICROARCH.md, so the streamed outputs do not evict the inputs that the
+// MAC reads a second time)
+#ifndef MKACC_S2_STAUX
+#define MKACC_S2_STAUX 0
+#endif
+template <>
+struct VecLd<4> {
+    using T = u32x4;
+    __device__ __forceinline__ static T ld(__amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so) { return bload4(r, vo, so); }
+    __device__ __forceinline__ static void st(T v, __amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so) {
+        __builtin_amdgcn_raw_buffer_store_b128(v, r, vo, so, MKACC_S2_STAUX);
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_nop 1");   // store-data hazard (bstore4)
+        __builtin_amdgcn_sched_barrier(0);
+    }
+};
+template <>
+struct VecLd<2> {
+    using T = u32x2;
+    __device__ __forceinline__ static T ld(__amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so) { return bload2(r, vo, so); }
+    // 8-byte stores carry no store-data hazard (bstore4)
+    __device__ __forceinline__ static void st(T v, __amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so) {
+        __builtin_amdgcn_raw_buffer_store_b64(v, r, vo, so, MKACC_S2_STAUX);
+    }
+};
+
+// Key-stream shape of one pass.  kGS slots per load group (C4 layout: slot r of
+// lane l at byte (r >> 2) * 1024 + l * 16 + (r & 3) * 4), kPf groups in flight.
+template <int DG, int METHOD, bool FIRST>
+struct Step2Cfg {
+    static constexpr bool kSplit = METHOD == XZW && !FIRST;   // two sums + one monomial product per slot
+    static constexpr bool kK2 = METHOD == XZW;                // ev2 words needed
+#ifndef MKACC_S2_GS
+#define MKACC_S2_GS 0
+#endif
+    static constexpr int kGS = MKACC_S2_GS ? MKACC_S2_GS : (DG <= 3 ? 4 : 2);
+    // load groups in flight ahead of the one being summed: 1 at dg <= 3; at dg = 4
+    // the 4 x 32 G registers leave room for none without spills
+#ifndef MKACC_S2_PF
+#define MKACC_S2_PF -1
+#endif
+    static constexpr int kPf = MKACC_S2_PF >= 0 ? MKACC_S2_PF : (DG <= 3 ? 1 : 0);
+    // X^(N-c) - 1 gathered with the group's key loads (1) or at use (0)
+#ifndef MKACC_S2_MONO
+#define MKACC_S2_MONO 0
+#endif
+    static constexpr bool kMonoPf = kSplit && MKACC_S2_MONO;
+    // sumV between the party passes: in the gate's HBM scratch (StepArgs::dscr),
+    // streamed in with the keys, instead of 32 VGPRs live across every transform
+#ifndef MKACC_S2_SVMEM
+#define MKACC_S2_SVMEM 0
+#endif
+    static constexpr bool kSvMem = MKACC_S2_SVMEM;
+
+    static constexpr int kGroups = kRegs / kGS;
+    static constexpr int kBuf = kPf + 1;
+    __device__ __forceinline__ static constexpr uint32_t soff(int g) {
+        return (uint32_t)(((g * kGS) >> 2) * 1024 + ((g * kGS) & 3) * 4);
+    }
+    // redc bound (units of Q^2, below 32): digit-NTT outputs < kG Q, canonical keys,
+    // plus a 32-bit start value in [0, 2Q) times 2^32 mod Q (< 2 Q^2)
+    static constexpr int kG = DG > 4 ? 2 : 4;
+    static_assert(2 + DG * kG <= 32, "step2 sum bound");
+};
+
+// One load group: the key words of kGS slots for every digit, the start value
+// (previous accumulator / index party output) and the slots' X^(N-c) - 1.
+template <int DG, int METHOD, bool FIRST>
+struct Grp2 {
+    using C = Step2Cfg<DG, METHOD, FIRST>;
+    using V = typename VecLd<C::kGS>::T;
+    V k1[DG];
+    V k2[C::kK2 ? DG : 1];
+    V ks[FIRST ? DG : 1];
+    V pk[DG];
+    V st;
+    V sv;   // kSvMem: sumV of the earlier parties
+    uint2 mono[C::kMonoPf ? C::kGS : 1];
+};
+
+// Streaming MAC of one pass over the step's key block.
+//   F = false (party u): keys d-half of ev1'/ev2 (2i), P[u][i]; start = acc_in[u];
+//                        out -> acc_out[u]; sv <- redc(sv r32 + sum G P)
+//                        (kSvMem: the earlier parties' sv is read from the gate's
+//                        scratch, scaled by svf = 0 for the first party, r32 after;
+//                        sv is returned in registers and also stored)
+//   F = true  (f-part):  keys f-half (2i + 1); start = acc_out[index] (the index
+//                        party's output); out -> acc_out[index]
+template <int DG, int METHOD, bool FIRST, bool F>
+__device__ __forceinline__ void mac2(const StepCtx& s, uint32_t u, const uint32_t (&G)[DG][kRegs],
+                                     uint32_t (&sv)[kRegs], uint32_t svf = 0) {
+    using C = Step2Cfg<DG, METHOD, FIRST>;
+    using L = VecLd<C::kGS>;
+    using Grp = Grp2<DG, METHOD, FIRST>;
+    const uint32_t Q = s.m.Q, polyB = kN * 4u, vo = s.vo;
+    const uint32_t half = F ? polyB : 0u;           // f-half of each digit's key pair
+    const uint32_t uoff = u * polyB;
+    const uint32_t poff = u * DG * polyB;
+    auto issue = [&](Grp& t, int g) {
+        const uint32_t so = C::soff(g);
+#pragma unroll
+        for (int i = 0; i < DG; ++i) {
+            const uint32_t ko = (uint32_t)(2 * i) * polyB + half + so;
+            t.k1[i] = L::ld(s.rk1, vo, ko);
+            if (C::kK2) t.k2[i] = L::ld(s.rk2, vo, ko);
+            if (FIRST) t.ks[i] = L::ld(s.rks, vo, ko);
+            if (!F) t.pk[i] = L::ld(s.rpk, vo, poff + (uint32_t)i * polyB + so);
+        }
+        // party: acc_u (not in the first step, which overwrites acc); f-part: the
+        // index party's output, written by this wave earlier in the step
+        if (F) t.st = L::ld(s.rout, vo, uoff + so);
+        else if (!FIRST) t.st = L::ld(s.rin, vo, uoff + so);
+        if (!F && C::kSvMem) t.sv = L::ld(s.rds, vo, so);
+        if (C::kMonoPf) {
+#pragma unroll
+            for (int e = 0; e < C::kGS; ++e) t.mono[e] = s.mn.at(s.tb.psi, g * C::kGS + e);
+        }
+    };
+    Grp kg[C::kBuf];
+#pragma unroll
+    for (int j = 0; j < C::kPf; ++j) issue(kg[j], j);
+#pragma unroll
+    for (int g = 0; g < C::kGroups; ++g) {
+        if (g + C::kPf < C::kGroups) issue(kg[(g + C::kPf) % C::kBuf], g + C::kPf);
+        const Grp& t = kg[g % C::kBuf];
+        typename L::T ov;
+#pragma unroll
+        for (int e = 0; e < C::kGS; ++e) {
+            const int r = g * C::kGS + e;
+            uint64_t a1 = (F || !FIRST) ? mad64(t.st[e], s.m.r32, 0) : 0ull;
+            uint64_t a2 = 0, sa = F ? 0ull : mad64(C::kSvMem ? t.sv[e] : sv[r], C::kSvMem ? svf : s.m.r32, 0);
+#pragma unroll
+            for (int i = 0; i < DG; ++i) {
+                if constexpr (C::kSplit) {
+                    a1 = mad64(G[i][r], t.k1[i][e], a1);
+                    a2 = mad64(G[i][r], t.k2[i][e], a2);
+                } else {
+                    const uint32_t ke = key_eff<METHOD, FIRST, 1>(t.k1[i][e], C::kK2 ? t.k2[i][e] : 0u,
+                                                                 FIRST ? t.ks[i][e] : 0u, s.tb.psi, s.mp, s.mn, r, Q);
+                    a1 = mad64(G[i][r], ke, a1);
+                }
+                if (!F) sa = mad64(G[i][r], t.pk[i][e], sa);
+            }
+            uint32_t v = redc(a1, Q, s.m.qinv);                                       // [0, 2Q)
+            if constexpr (C::kSplit) {
+                const uint2 mo = C::kMonoPf ? t.mono[e] : s.mn.at(s.tb.psi, r);
+                v += mul_shoup_lazy(redc(a2, Q, s.m.qinv), mo, Q);                  // [0, 4Q)
+                v = min(v, v - 2u * Q);
+            }
+            ov[e] = v;
+            if (!F) sv[r] = redc(sa, Q, s.m.qinv);
+        }
+        L::st(ov, s.rout, vo, uoff + C::soff(g));
+        if (!F && C::kSvMem) {   // (also after the last party: no branch in the stream)
+            typename L::T sw;
+#pragma unroll
+            for (int e = 0; e < C::kGS; ++e) sw[e] = sv[g * C::kGS + e];
+            L::st(sw, s.rds, vo, C::soff(g));
+        }
+#ifndef MKACC_S2_FENCE
+#define MKACC_S2_FENCE 1
+#endif
+        if (MKACC_S2_FENCE) sched_fence();
+    }
+}
+
+// iNTT -> SDD -> dg forward NTTs: x (layout C, [0, 2Q)) -> G[i] = NTT(digit i + 1)
+template <int DG>
+__device__ __forceinline__ void digit_ntts(const StepCtx& s, uint32_t (&x)[kRegs], uint32_t (&G)[DG][kRegs]) {
+    const uint32_t Q = s.m.Q;
+    ntt_inv(x, s.lds, s.tw_inv, s.tb.twi, s.l, Q);
+    // SignedDigitDecompose (mk-acc.cpp:54-80): digit 1 -> G[0], digits 2.. packed
+    PackedDigits<DG> pd;
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) {
+        G[0][r] = pd.put(r, sdd_offset(x[r], s.sd), s.sd);
+        if ((r & 7) == 7) sched_fence();
+    }
+    ntt_fwd(G[0], s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, s.l, Q, s.m.m1);
+    digit_range<DG>(G[0], Q);
+#pragma unroll
+    for (int i = 1; i < DG; ++i) {
+#pragma unroll
+        for (int r = 0; r < kRegs; ++r) G[i][r] = pd.get(r, i + 1, s.sd);
+        ntt_fwd(G[i], s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, s.l, Q, s.m.m1);
+        digit_range<DG>(G[i], Q);
+    }
+}
+
+template <int DG, int METHOD, bool FIRST>
+__global__ __launch_bounds__(kThreads, 2) void mk_step2_kernel(StepArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    load_image(smem, a.img);
+    const uint32_t l = threadIdx.x & 63u;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t gate = blockIdx.x * kWavesPerBlock + wv;
+    if (gate >= a.B) return;
+    const uint32_t c = __builtin_amdgcn_readfirstlane(a.cvals[gate]);
+    const uint32_t cneg = (2u * kN - c) & (2u * kN - 1u);
+    const uint32_t k = a.k, index = a.index;
+    const uint32_t polyB = kN * 4u;
+    const StepCtx s{tables(smem, a.img),
+                    smem + kLdsTabWords + wv * kLdsWords,
+                    a.tw_fwd,
+                    a.tw_inv,
+                    a.m,
+                    a.sd,
+                    make_mono(c, l),
+                    // X^-c in the first step; X^(N-c) = -X^-c in the later XZW steps (key_eff)
+                    make_mono(FIRST || METHOD != XZW ? cneg : (cneg + kN) & (2u * kN - 1u), l),
+                    l,
+                    l * 16u,
+                    make_rsrc(a.acc_in + (size_t)gate * k * kN, k * polyB),
+                    make_rsrc(a.acc_out + (size_t)gate * k * kN, k * polyB),
+                    make_rsrc(a.key1, DG * 2 * polyB),
+                    make_rsrc(a.key2, DG * 2 * polyB),
+                    make_rsrc(a.keys, DG * 2 * polyB),
+                    make_rsrc(a.pkey, k * DG * polyB),
+                    make_rsrc(Step2Cfg<DG, METHOD, FIRST>::kSvMem ? a.dscr + (size_t)gate * kN : a.acc_in,
+                              Step2Cfg<DG, METHOD, FIRST>::kSvMem ? polyB : 0u)};
+    const uint32_t Q = s.m.Q;
+    uint32_t sv[kRegs];
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) sv[r] = 0;
+    // passes t = 0 .. k-1: party t; t = k: the f-part of party `index`
+    // (prefetching the next party's accumulator in the previous pass's stream kept
+    // 32 more VGPRs live: 53 spills, 206 us per launch against 168)
+#pragma unroll 1
+    for (uint32_t t = 0; t <= k; ++t) {
+        const bool fpart = __builtin_amdgcn_readfirstlane(t) == k;
+        uint32_t x[kRegs];
+        if (!fpart) {
+#pragma unroll
+            for (int gq = 0; gq < 8; ++gq) {
+                const u32x4 v = aload4(s.rin, s.vo, t * polyB + gq * 1024u);
+                x[4 * gq] = v.x; x[4 * gq + 1] = v.y; x[4 * gq + 2] = v.z; x[4 * gq + 3] = v.w;
+            }
+            if (!FIRST) {
+                // acctemp = acc * (X^c - 1)                 (xzw.cpp:336-338)
+                uint2 mw[kRegs];
+#pragma unroll
+                for (int r = 0; r < kRegs; ++r) mw[r] = s.mp.at(s.tb.psi, r);
+                sched_fence();
+#pragma unroll
+                for (int r = 0; r < kRegs; ++r) x[r] = mul_shoup_lazy(x[r], mw[r], Q);
+            }
+        } else {
+            // sumV of every party, [0, 2Q)
+#pragma unroll
+            for (int r = 0; r < kRegs; ++r) x[r] = sv[r];
+            // the index party's output (acc_out[index], this wave's own stores) is
+            // read back by the f-part's MAC
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        uint32_t G[DG][kRegs];
+        digit_ntts<DG>(s, x, G);
+        if (!fpart)
+            mac2<DG, METHOD, FIRST, false>(s, t, G, sv, t == 0 ? 0u : s.m.r32);
+        else
+            mac2<DG, METHOD, FIRST, true>(s, index, G, sv);
+    }
+}

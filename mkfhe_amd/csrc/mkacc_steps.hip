@@ -2,6 +2,7 @@
 // build (mkfhe_amd/build.py) compiles this file once per unit, in parallel:
 //   -DMKACC_TU_DG=d -DMKACC_TU_PART=0   mk_step_kernel instantiations of digit count d
 //   -DMKACC_TU_DG=d -DMKACC_TU_PART=1   mk_lat_kernel instantiations of digit count d
+//   -DMKACC_TU_DG=d -DMKACC_TU_PART=2   mk_step2_kernel instantiations of digit count d
 //   -DMKACC_TU_WIDE=1 / 2              64-bit word step kernels (integer / FP64)
 // and the host unit (mkacc_engine.hip) launches them through mkacc_tu.
 #include "mkacc_kernels.hpp"
@@ -32,9 +33,13 @@ namespace mkacc_tu {
 KernelPtr MKACC_CAT(step_dg, MKACC_TU_DG)(int method, bool first, bool dscr) {
     return (KernelPtr)pick_step<MKACC_TU_DG>(method, first, dscr);
 }
-#else
+#elif MKACC_TU_PART == 1
 KernelPtr MKACC_CAT(lat_dg, MKACC_TU_DG)(int method, bool first) {
     return (KernelPtr)pick_lat<MKACC_TU_DG>(method, first);
+}
+#else
+KernelPtr MKACC_CAT(step2_dg, MKACC_TU_DG)(int method, bool first) {
+    return (KernelPtr)pick_step2<MKACC_TU_DG>(method, first);
 }
 #endif
 }  // namespace mkacc_tu
