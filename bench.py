@@ -81,14 +81,18 @@ def algorithmic_counts(k: int, n: int, dg: int, nk: int, N: int = 2048, B: int =
     return mulmods, bytes_
 
 
-def measured_traffic(paramset: str):
+def measured_traffic(paramset: str, kernel: str):
     """Per-launch HBM bytes of the step kernel from the committed PMC record
     (profiles/traffic_<paramset>.json, written by tools/pmc_summary.py from
-    separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes), or None."""
+    separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes), or None -- also
+    when the record was taken of another step kernel than the one benched."""
     f = os.path.join(ROOT, "profiles", f"traffic_{paramset}.json")
     if not os.path.exists(f):
         return None
-    return json.load(open(f))["traffic_bytes"]
+    rec = json.load(open(f))
+    if rec.get("kernel", "mk_step_kernel") != kernel:
+        return None
+    return rec["traffic_bytes"]
 
 
 def parse(argv=None):
@@ -375,6 +379,7 @@ def run_rank(args, env: dict, make_engine, make_checker, torch_device: str, back
                      f"{'KeySwitch' if lwe else 'KeySwitch2'}") if stage == "gate" else "EvalAcc (blind rotation) only"
         pl = per_launch_s or float("nan")
         wide_fp = wide and getattr(eng, "wide_fp", False)
+        kname = eng.step_kernel_name(B) if hasattr(eng, "step_kernel_name") else "mk_step_kernel"
         peak_mm, peak_src = ((PEAK_FP64_MULMOD_TPS, "exact FP64 product, profiles/r2/ubench_wide.txt") if wide_fp else
                              (PEAK_INT64_MULMOD_TPS, "64-bit Shoup product, profiles/r2/ubench_wide.txt") if wide else
                              (PEAK_SHOUP_MULMOD_TPS, "27-bit Shoup product, profiles/round1_ubench_intops.txt"))
@@ -405,8 +410,8 @@ def run_rank(args, env: dict, make_engine, make_checker, torch_device: str, back
                        "reference's KATs, the EvalAcc composition is 'parity unpinned' beyond them (DESIGN.md s3)"),
             "roofline": {"bound": "hbm", "achieved": by / pl / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": by / pl / 1e9 / PEAK_HBM_GBS,
-                         "traffic": measured_traffic(args.paramset) if not (args.n_override or wide) else None,
-                         "kernel": ("widefp::step_kernel" if wide_fp else "wide::step_kernel") if wide else "mk_step_kernel",
+                         "traffic": measured_traffic(args.paramset, kname) if not (args.n_override or wide) else None,
+                         "kernel": kname,
                          "per_launch_us": pl * 1e6,
                          "bytes_per_launch": by},
             # VALU view: algorithmic mod-muls per launch against the measured rate of the

@@ -112,6 +112,10 @@ int mkacc_eval_batch_u64(mkacc_ctx* ctx, const uint32_t* ct, const uint64_t* acc
  * then mkacc_eval_batch_device takes uint64_t accumulators and the gate calls are
  * unsupported.  1: integer kernels; 2: the FP64 kernels (mkacc_widefp.hpp, Q < 2^50). */
 int mkacc_is_wide(const mkacc_ctx* ctx);
+/* Name of the batch step kernel a context launches for B gates (diagnostics:
+ * bench.py's roofline record and kernel-trace matching), e.g. "mk_step2_kernel";
+ * a static string, "" for a null context. */
+const char* mkacc_step_kernel_name(const mkacc_ctx* ctx, size_t B);
 
 /* Same with DEVICE pointers on the context's device; enqueued on the context
  * stream and returns without waiting (use mkacc_sync).  Used by bench.py so

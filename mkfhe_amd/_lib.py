@@ -68,6 +68,7 @@ SIGNATURES = {
     "mkacc_eval_batch": (ctypes.c_int, [ctypes.c_void_p, _u32p, _u32p, _u32p, ctypes.c_size_t]),
     "mkacc_eval_batch_u64": (ctypes.c_int, [ctypes.c_void_p, _u32p, _u64p, _u64p, ctypes.c_size_t]),
     "mkacc_is_wide": (ctypes.c_int, [ctypes.c_void_p]),
+    "mkacc_step_kernel_name": (ctypes.c_char_p, [ctypes.c_void_p, ctypes.c_size_t]),
     "mkacc_ntt_forward_u64": (ctypes.c_int, [ctypes.c_void_p, _u64p, _u64p, ctypes.c_size_t]),
     "mkacc_ntt_inverse_u64": (ctypes.c_int, [ctypes.c_void_p, _u64p, _u64p, ctypes.c_size_t]),
     "mkacc_sdd_u64": (ctypes.c_int, [ctypes.c_void_p, _u64p, _u64p, ctypes.c_size_t]),

@@ -153,6 +153,10 @@ class MKAccumulatorEngine:
         """True if the 64-bit word path runs its FP64 kernels (Q < 2^50, mkacc_widefp.hpp)."""
         return _lib.load().mkacc_is_wide(self._h) == 2
 
+    def step_kernel_name(self, B: int) -> str:
+        """The batch step kernel this context launches for B gates."""
+        return _lib.load().mkacc_step_kernel_name(self._h, int(B)).decode()
+
     def eval_batch(self, ct: np.ndarray, acc: np.ndarray) -> np.ndarray:
         """EvalAcc on B gates: ct [B][k][n], acc [B][k][N] EVAL -> new acc.
         uint64 accumulators (or Q >= 2^32) go through mkacc_eval_batch_u64."""

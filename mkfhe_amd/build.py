@@ -91,7 +91,7 @@ def build_keys(force: bool = False, verbose: bool = False) -> str:
 UNITS = [("engine", "mkacc_engine.hip", [])] + [
     (f"step_dg{d}", "mkacc_steps.hip", [f"-DMKACC_TU_DG={d}", "-DMKACC_TU_PART=0"]) for d in (2, 3, 4, 5)] + [
     (f"lat_dg{d}", "mkacc_steps.hip", [f"-DMKACC_TU_DG={d}", "-DMKACC_TU_PART=1"]) for d in (2, 3, 4)] + [
-    (f"step2_dg{d}", "mkacc_steps.hip", [f"-DMKACC_TU_DG={d}", "-DMKACC_TU_PART=2"]) for d in (2, 3, 4)] + [
+    (f"step2_dg{d}", "mkacc_steps.hip", [f"-DMKACC_TU_DG={d}", "-DMKACC_TU_PART=2"]) for d in (2, 3)] + [
     ("wide", "mkacc_steps.hip", ["-DMKACC_TU_WIDE=1"]), ("widefp", "mkacc_steps.hip", ["-DMKACC_TU_WIDE=2"])]
 
 

@@ -131,6 +131,17 @@ __device__ __forceinline__ uint64_t mul64_pin(uint32_t a, uint32_t b) {
     return r;
 }
 
+// The pinned multiply-adds write their carry-out to VCC from an asm body, which
+// hipcc does not count as a VALU write of VCC: an SALU write/read of VCC (a
+// wave-uniform branch) right after them can see the late VALU write (DESIGN.md
+// s2, the mk_lat_kernel defect).  Put this between such multiply-adds and the
+// next wave-uniform branch; tools/isa_audit.py checks every build.
+__device__ __forceinline__ void vcc_fence() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 7" ::: "vcc");
+    __builtin_amdgcn_sched_barrier(0);
+}
+
 // Montgomery reduction (R = 2^32) of a lazy 64-bit sum x < Q * 2^32:
 // m = x * (-Q^-1) mod 2^32 makes x + m Q divisible by 2^32, and
 // (x + m Q) / 2^32 < 2Q is congruent to x * 2^-32 mod Q.  Two instructions

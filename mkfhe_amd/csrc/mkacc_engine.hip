@@ -88,17 +88,20 @@ __global__ void wide_key_layout_kernel(const W* __restrict__ src, uint64_t* __re
 // produced the segfault / all-wrong records of ab_l1, lat_l1 and ab_d1,
 // DESIGN.md s2; a null kernel is now refused at mkacc_create and launch.)
 // Batch step kernel generation: 2 = mk_step2_kernel (mkacc_step2.hpp, digit NTTs
-// first, one key stream per pass; built for dg <= 4), 1 = mk_step_kernel (every
-// digit count).  Default 2 for dg <= 3 (STD128_MKNTRU 163.8 -> 159.6 us per
-// launch, STD100_MKNTRU 132.6 -> 126.2, STD100_MKNTRU_LWE_2 187.4 -> 183.7),
-// 1 above (dg = 4, STD128_MKNTRU_3: 1191 against 1799 us for the spilling
-// step2 kernel).  MKACC_STEP=1/2 overrides where built; read once per context
-// (mkacc_ctx::step_ver), which sizes its workspace for that kernel.
+// first, one key stream per pass; built for dg <= 3), 1 = mk_step_kernel (every
+// digit count).  Default 2 where built (STD128_MKNTRU 163.8 -> 158.5 us per
+// launch, STD100_MKNTRU 132.6 -> 126.2, STD100_MKNTRU_LWE_2 187.4 -> 183.7).  At
+// dg = 4 the 4 x 32 digit-NTT registers leave no room for the key prefetch
+// (STD128_MKNTRU_3: 1,704 us with 4-slot groups and no prefetch, 2,593 us with
+// 1-slot groups, against 1,194 us for mk_step_kernel with its d_i scratch;
+// DESIGN.md s2), so it is not built there.  MKACC_STEP=1 selects
+// mk_step_kernel; read once per context (mkacc_ctx::step_ver), which sizes its
+// workspace for that kernel.
 int step_version(int dg) {
-    if (dg > 4) return 1;
+    if (dg > 3) return 1;
     const char* e = std::getenv("MKACC_STEP");
-    if (e && (e[0] == '1' || e[0] == '2')) return e[0] - '0';
-    return dg <= 3 ? 2 : 1;
+    if (e && e[0] == '1') return 1;
+    return 2;
 }
 
 const void* step_fn(int dg, int method, bool first, bool dscr, int ver) {
@@ -106,7 +109,6 @@ const void* step_fn(int dg, int method, bool first, bool dscr, int ver) {
         switch (dg) {
             case 2: return mkacc_tu::step2_dg2(method, first);
             case 3: return mkacc_tu::step2_dg3(method, first);
-            case 4: return mkacc_tu::step2_dg4(method, first);
             default: return nullptr;
         }
     }
@@ -358,7 +360,11 @@ uint32_t* launch_steps(mkacc_ctx* c, size_t B) {
             } else {
                 const void* fn = step_fn((int)c->dg, c->method_class, first, !first && use_dscr(c), c->step_ver);
                 if (!fn) return nullptr;
-                launch_ptr(fn, grid, block, lds, c->stream, a);
+                if (c->step_ver == 2)
+                    launch_ptr(fn, dim3((unsigned)((B + kS2Waves - 1) / kS2Waves)), dim3(64 * kS2Waves),
+                               kStep2LdsBytes + (lds - kStepLdsBytes), c->stream, a);
+                else
+                    launch_ptr(fn, grid, block, lds, c->stream, a);
             }
             std::swap(cur, nxt);
         }
@@ -1184,6 +1190,12 @@ int mkacc_upload_keys_device(mkacc_ctx* c, const void* d_evk, const void* d_pkey
     return upload_keys_device_impl(c, (const uint64_t*)d_evk, (const uint64_t*)d_pkey);
 }
 
+const char* mkacc_step_kernel_name(const mkacc_ctx* c, size_t B) {
+    if (!c) return "";
+    if (c->wide) return c->wfp ? "widefp::step_kernel" : "wide::step_kernel";
+    if (use_lat(c, B)) return "mk_lat_kernel";
+    return c->step_ver == 2 ? "mk_step2_kernel" : "mk_step_kernel";
+}
 int mkacc_is_wide(const mkacc_ctx* c) { return c && c->wide ? (c->wfp ? 2 : 1) : 0; }
 
 int mkacc_eval_batch_u64(mkacc_ctx* c, const uint32_t* ct, const uint64_t* acc_in, uint64_t* acc_out, size_t B) {

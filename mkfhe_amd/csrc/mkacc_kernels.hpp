@@ -46,6 +46,14 @@ constexpr int kLdsTabWords = 2 * (1024 + kPsiPairs);
 constexpr size_t kStepLdsBytes = (size_t)(kLdsTabWords + kWavesPerBlock * kLdsWords) * 4;
 static_assert(kLdsTabWords % 4 == 0, "LDS tables are copied with dwordx4");
 static_assert(2 * kStepLdsBytes <= 160 * 1024, "two workgroups per CU");
+// mk_step2_kernel workgroup: kS2Waves gates sharing one LDS table image (4: two
+// workgroups per CU; 8: one, the table copied once per CU)
+#ifndef MKACC_S2_WAVES
+#define MKACC_S2_WAVES 4
+#endif
+constexpr int kS2Waves = MKACC_S2_WAVES;
+constexpr size_t kStep2LdsBytes = (size_t)(kLdsTabWords + kS2Waves * kLdsWords) * 4;
+static_assert((8 / kS2Waves) * kStep2LdsBytes <= 160 * 1024, "8 waves per CU");
 
 // Bank-spreading position of psi^e in the LDS table.  A wave gathers
 // e = c (2 brv6(lane) + 1) + 128 c brv5(r) mod 2N (Mono): the low 7 bits are
@@ -891,7 +899,6 @@ MKACC_TU_API KernelPtr step_dg4(int method, bool first, bool dscr);
 MKACC_TU_API KernelPtr step_dg5(int method, bool first, bool dscr);
 MKACC_TU_API KernelPtr step2_dg2(int method, bool first);   // mk_step2_kernel (mkacc_step2.hpp)
 MKACC_TU_API KernelPtr step2_dg3(int method, bool first);
-MKACC_TU_API KernelPtr step2_dg4(int method, bool first);
 MKACC_TU_API KernelPtr lat_dg2(int method, bool first);
 MKACC_TU_API KernelPtr lat_dg3(int method, bool first);
 MKACC_TU_API KernelPtr lat_dg4(int method, bool first);

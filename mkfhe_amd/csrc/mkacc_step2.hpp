@@ -59,6 +59,22 @@ struct VecLd<2> {
     }
 };
 
+struct u32x1 {
+    uint32_t v;
+    __device__ __forceinline__ uint32_t operator[](int) const { return v; }
+    __device__ __forceinline__ uint32_t& operator[](int) { return v; }
+};
+template <>
+struct VecLd<1> {
+    using T = u32x1;
+    __device__ __forceinline__ static T ld(__amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so) {
+        return T{__builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0)};
+    }
+    __device__ __forceinline__ static void st(T v, __amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so) {
+        __builtin_amdgcn_raw_buffer_store_b32(v.v, r, vo, so, MKACC_S2_STAUX);
+    }
+};
+
 // Key-stream shape of one pass.  kGS slots per load group (C4 layout: slot r of
 // lane l at byte (r >> 2) * 1024 + l * 16 + (r & 3) * 4), kPf groups in flight.
 template <int DG, int METHOD, bool FIRST>
@@ -69,8 +85,8 @@ struct Step2Cfg {
 #define MKACC_S2_GS 0
 #endif
     static constexpr int kGS = MKACC_S2_GS ? MKACC_S2_GS : (DG <= 3 ? 4 : 2);
-    // load groups in flight ahead of the one being summed: 1 at dg <= 3; at dg = 4
-    // the 4 x 32 G registers leave room for none without spills
+    // load groups in flight ahead of the one being summed: 1 at dg <= 3 (at dg = 4,
+    // not built, the 4 x 32 G registers leave room for none without spills)
 #ifndef MKACC_S2_PF
 #define MKACC_S2_PF -1
 #endif
@@ -197,6 +213,7 @@ __device__ __forceinline__ void mac2(const StepCtx& s, uint32_t u, const uint32_
 #endif
         if (MKACC_S2_FENCE) sched_fence();
     }
+    vcc_fence();   // the caller's branches follow the last reductions
 }
 
 // iNTT -> SDD -> dg forward NTTs: x (layout C, [0, 2Q)) -> G[i] = NTT(digit i + 1)
@@ -223,12 +240,12 @@ __device__ __forceinline__ void digit_ntts(const StepCtx& s, uint32_t (&x)[kRegs
 }
 
 template <int DG, int METHOD, bool FIRST>
-__global__ __launch_bounds__(kThreads, 2) void mk_step2_kernel(StepArgs a) {
+__global__ __launch_bounds__(64 * kS2Waves, 8 / kS2Waves) void mk_step2_kernel(StepArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     load_image(smem, a.img);
     const uint32_t l = threadIdx.x & 63u;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t gate = blockIdx.x * kWavesPerBlock + wv;
+    const uint32_t gate = blockIdx.x * kS2Waves + wv;
     if (gate >= a.B) return;
     const uint32_t c = __builtin_amdgcn_readfirstlane(a.cvals[gate]);
     const uint32_t cneg = (2u * kN - c) & (2u * kN - 1u);
@@ -278,6 +295,7 @@ __global__ __launch_bounds__(kThreads, 2) void mk_step2_kernel(StepArgs a) {
                 sched_fence();
 #pragma unroll
                 for (int r = 0; r < kRegs; ++r) x[r] = mul_shoup_lazy(x[r], mw[r], Q);
+                vcc_fence();   // the jump over the f-part branch follows the rotation
             }
         } else {
             // sumV of every party, [0, 2Q)
@@ -287,8 +305,10 @@ __global__ __launch_bounds__(kThreads, 2) void mk_step2_kernel(StepArgs a) {
             // read back by the f-part's MAC
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
+        vcc_fence();   // the branch above follows the rotation's multiply-adds
         uint32_t G[DG][kRegs];
         digit_ntts<DG>(s, x, G);
+        vcc_fence();   // the MAC branch follows the last butterflies
         if (!fpart)
             mac2<DG, METHOD, FIRST, false>(s, t, G, sv, t == 0 ? 0u : s.m.r32);
         else
