@@ -277,14 +277,20 @@ __global__ __launch_bounds__(64 * kS2Waves, 8 / kS2Waves) void mk_step2_kernel(S
     // passes t = 0 .. k-1: party t; t = k: the f-part of party `index`
     // (prefetching the next party's accumulator in the previous pass's stream kept
     // 32 more VGPRs live: 53 spills, 206 us per launch against 168)
+    // Parties in the order index + 1, ..., index (MKACC_S2_ORDER=1): the index
+    // party's output, read back by the f-part, is written last (shortest time in L2)
+#ifndef MKACC_S2_ORDER
+#define MKACC_S2_ORDER 1
+#endif
 #pragma unroll 1
     for (uint32_t t = 0; t <= k; ++t) {
         const bool fpart = __builtin_amdgcn_readfirstlane(t) == k;
+        const uint32_t u = MKACC_S2_ORDER ? (index + 1 + t < k ? index + 1 + t : index + 1 + t - k) : t;
         uint32_t x[kRegs];
         if (!fpart) {
 #pragma unroll
             for (int gq = 0; gq < 8; ++gq) {
-                const u32x4 v = aload4(s.rin, s.vo, t * polyB + gq * 1024u);
+                const u32x4 v = aload4(s.rin, s.vo, u * polyB + gq * 1024u);
                 x[4 * gq] = v.x; x[4 * gq + 1] = v.y; x[4 * gq + 2] = v.z; x[4 * gq + 3] = v.w;
             }
             if (!FIRST) {
@@ -310,7 +316,7 @@ __global__ __launch_bounds__(64 * kS2Waves, 8 / kS2Waves) void mk_step2_kernel(S
         digit_ntts<DG>(s, x, G);
         vcc_fence();   // the MAC branch follows the last butterflies
         if (!fpart)
-            mac2<DG, METHOD, FIRST, false>(s, t, G, sv, t == 0 ? 0u : s.m.r32);
+            mac2<DG, METHOD, FIRST, false>(s, u, G, sv, t == 0 ? 0u : s.m.r32);
         else
             mac2<DG, METHOD, FIRST, true>(s, index, G, sv);
     }
