@@ -34,9 +34,10 @@ template <int GS>
 struct VecLd;
 // cache policy of the accumulator stores (aux; 16 = sc1: the line leaves the XCD's L2,
 // MI355X_MICROARCH.md, so the streamed outputs do not evict the inputs that the
-// MAC reads a second time)
+// MAC reads a second time): HBM traffic 243 -> 223 MB per STD128_MKNTRU launch
+// at unchanged time (profiles/r3/pmc_sc1.txt, ab_step2.txt)
 #ifndef MKACC_S2_STAUX
-#define MKACC_S2_STAUX 0
+#define MKACC_S2_STAUX 16
 #endif
 template <>
 struct VecLd<4> {
