@@ -5,8 +5,8 @@
 #   identity (mkacc_build_info: header/source ids and these flags) is checked by
 #   mkfhe_amd._lib.load when it is loaded through MKFHE_LIB.
 NAME=$1; shift
-python3 -m mkfhe_amd.build --variant "$NAME" "$@" > /dev/null
+python3 -m mkfhe_amd.build --variant "$NAME" "$@" > /dev/null   # add --units a,b to recompile only those units
 rc=$?
-grep -A9 "mk_step_kernelILi3ELi0ELb0E" mkfhe_amd/lib/variants/$NAME.res | grep -E "VGPRs( Spill)?:" | sed 's/.*remark: *//' | tr '\n' ' '
+grep -A9 "mk_step2_kernelILi3ELi0ELb0E" mkfhe_amd/lib/variants/$NAME.res | grep -E "VGPRs( Spill)?:" | sed 's/.*remark: *//' | tr '\n' ' '
 echo " [$NAME rc=$rc]"
 exit $rc
