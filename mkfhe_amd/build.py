@@ -84,6 +84,12 @@ def build_keys(force: bool = False, verbose: bool = False) -> str:
     return KEYS_OUT
 
 
+# Machine-scheduler strategy of the step2 unit at dg = 3 (the headline kernel):
+# max-memory-clause schedules it at 256 VGPRs with no spills (the default
+# strategy spills 6) and ran 154.6-155.3 us per STD128_MKNTRU launch against
+# 159.0-159.9 (profiles/r3/ab_sched.txt); the ISA audit stays clean with it.
+STEP2_SCHED = {3: ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"]}
+
 # Translation units of the engine library, compiled in parallel and linked into
 # one .so: the host unit (C ABI, batch / gate / primitive kernels) and the step
 # kernel units of mkacc_steps.hip (one per digit count and kernel kind, and the
@@ -91,7 +97,8 @@ def build_keys(force: bool = False, verbose: bool = False) -> str:
 UNITS = [("engine", "mkacc_engine.hip", [])] + [
     (f"step_dg{d}", "mkacc_steps.hip", [f"-DMKACC_TU_DG={d}", "-DMKACC_TU_PART=0"]) for d in (2, 3, 4, 5)] + [
     (f"lat_dg{d}", "mkacc_steps.hip", [f"-DMKACC_TU_DG={d}", "-DMKACC_TU_PART=1"]) for d in (2, 3, 4)] + [
-    (f"step2_dg{d}", "mkacc_steps.hip", [f"-DMKACC_TU_DG={d}", "-DMKACC_TU_PART=2"]) for d in (2, 3)] + [
+    (f"step2_dg{d}", "mkacc_steps.hip", [f"-DMKACC_TU_DG={d}", "-DMKACC_TU_PART=2"] + STEP2_SCHED.get(d, []))
+    for d in (2, 3)] + [
     ("wide", "mkacc_steps.hip", ["-DMKACC_TU_WIDE=1"]), ("widefp", "mkacc_steps.hip", ["-DMKACC_TU_WIDE=2"])]
 
 
@@ -151,7 +158,8 @@ def compile_engine(out: str, flags: list[str], report: str, verbose: bool = Fals
 
 def build(force: bool = False, verbose: bool = False) -> str:
     build_keys(force, verbose)
-    if not force and not _stale(OUT, SOURCES + HEADERS):
+    # this file holds the per-unit compile flags, so a change here rebuilds too
+    if not force and not _stale(OUT, SOURCES + HEADERS + [os.path.abspath(__file__)]):
         return OUT
     return compile_engine(OUT, [], os.path.join(os.path.dirname(OUT), "resource_usage.txt"), verbose)
 
