@@ -5,7 +5,9 @@
 //
 //   g++ -std=c++17 -O2 -Iinclude examples/boolean-mklwe.cpp -Lmkfhe_amd/lib
 //       -lmkfhe_amd -lmkfhe_keys -Wl,-rpath,$PWD/mkfhe_amd/lib -o boolean-mklwe
-//   ./boolean-mklwe [STD100_MKNTRU_LWE|...]
+//   ./boolean-mklwe [STD100_MKNTRU_LWE|...] [--replay]
+//   --replay: record the seed-0 entropy master so a run with a wrong gate can be
+//   replayed (prints it on failure; whoever holds it holds every key of the run)
 #include <cstdio>
 #include <cstring>
 #include <ctime>
@@ -23,9 +25,19 @@ static BINFHE_PARAMSET parse(const char* s) {
 }
 
 int main(int argc, char** argv) {
+    const char* set = nullptr;
+    bool replay = false;
+    for (int i = 1; i < argc; ++i) {
+        if (!strcmp(argv[i], "--replay"))
+            replay = true;
+        else
+            set = argv[i];
+    }
+    if (replay) BinFHEContext::EnableEntropyReplay();   // opt-in: the master is secret material
+
     // Sample Program: Step 1: Set CryptoContext
     auto cc = BinFHEContext();
-    cc.GenerateBinFHEContext(argc > 1 ? parse(argv[1]) : STD100_MKNTRU_LWE, MKNTRU_LWE);
+    cc.GenerateBinFHEContext(set ? parse(set) : STD100_MKNTRU_LWE, MKNTRU_LWE);
     cout << "Generating sk" << endl;
     auto sk = cc.MKLWE_KeyGen();
 
@@ -52,12 +64,16 @@ int main(int argc, char** argv) {
             bad += result != !(m0 & m1);
         }
     if (bad) {
-        // seed material of every key and ciphertext above (seed-0 entropy journal):
-        // MKFHE_ENTROPY=<master> replays this run; tools/replay_entropy.py recomputes
-        // its gates on the CPU oracle
-        uint64_t calls = 0;
-        const std::string master = BinFHEContext::GetEntropy(&calls);
-        std::cout << "replay: MKFHE_ENTROPY=" << master << " (" << calls << " seed-0 calls)" << std::endl;
+        if (replay) {
+            // seed material of every key and ciphertext above (seed-0 entropy journal):
+            // MKFHE_ENTROPY=<master> with --replay replays this run, and
+            // tools/fresh_key_rate.py --replay <master> recomputes its gates on the CPU oracle
+            uint64_t calls = 0;
+            const std::string master = BinFHEContext::GetEntropy(&calls);
+            std::cout << "replay: MKFHE_ENTROPY=" << master << " (" << calls << " seed-0 calls)" << std::endl;
+        } else {
+            std::cout << "run with --replay to record the key material of a failing run" << std::endl;
+        }
         return 1;
     }
     return 0;

@@ -625,10 +625,16 @@ public:
     }
     // Extension: seed of the key/encryption sampler (0 = random, the reference's behaviour).
     void SetSeed(uint64_t seed) { m_seed = seed; }
-    // Extension: the seed-0 entropy journal of this process (mkfhe_keys.h): the
-    // 64-hex-digit master key and the number of seed-0 calls made under it.  A
-    // run started with MKFHE_ENTROPY=<master> repeats every seed-0 key and
-    // encryption of a run that made the same calls (tools/replay_entropy.py).
+    // Extension: the seed-0 entropy journal of this process (mkfhe_keys.h).
+    // Whoever holds the master holds every seed-0 key of the process, so it is
+    // exported only after EnableEntropyReplay(), which also takes the master
+    // from MKFHE_ENTROPY when that is set (config_error if it is malformed).  A
+    // run that enabled replay with MKFHE_ENTROPY=<master> repeats every seed-0
+    // key and encryption of a run that made the same calls
+    // (tools/fresh_key_rate.py --replay recomputes its gates on the CPU oracle).
+    static void EnableEntropyReplay(bool enable = true) { check(mkkg_entropy_replay(enable ? 1 : 0)); }
+    // The 64-hex-digit master and the number of seed-0 calls made under it;
+    // config_error unless EnableEntropyReplay() ran first.
     static std::string GetEntropy(uint64_t* calls = nullptr) {
         uint32_t m[8];
         check(mkkg_entropy_get(m, calls));

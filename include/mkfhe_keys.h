@@ -42,10 +42,11 @@
  *              SplitMix64(seed) -- NOT a CSPRNG;
  *   seed == 0  fresh keys, the reference's behaviour: ChaCha20 streams under a
  *              256-bit call key derived from the process's entropy journal
- *              (a master key from std::random_device, or MKFHE_ENTROPY = 64
- *              hex digits, and a counter of seed-0 calls).  mkkg_entropy_get
- *              reports the master, so a run with a wrong gate can be replayed
- *              exactly (tools/replay_entropy.py).
+ *              (a master key from std::random_device and a counter of seed-0
+ *              calls).  After an explicit mkkg_entropy_replay(1) the master
+ *              can be exported (mkkg_entropy_get) or taken from MKFHE_ENTROPY,
+ *              so a run with a wrong gate can be replayed exactly
+ *              (tools/fresh_key_rate.py --replay).
  * Outputs are independent of the thread count.
  *
  * Layouts (row-major, canonical residues):
@@ -71,7 +72,7 @@
 extern "C" {
 #endif
 
-#define MKKG_ABI_VERSION 2
+#define MKKG_ABI_VERSION 3
 
 /* SecretKeyDist values used by the MK parameter sets (binfhe-constants.h) */
 #define MKKG_DIST_TERNARY  0  /* UNIFORM_TERNARY */
@@ -177,11 +178,21 @@ int mkkg_ntt_forward(const mkkg_params* p, const uint32_t* in, uint32_t* out, si
 int mkkg_ntt_inverse(const mkkg_params* p, const uint32_t* in, uint32_t* out, size_t count);
 
 /* ---- seed-0 entropy journal --------------------------------------------------
- * master: 8 words = the 64 hex digits of MKFHE_ENTROPY, word 0 first.
+ * WHOEVER HOLDS THE MASTER HOLDS EVERY SEED-0 KEY AND CIPHERTEXT OF THE PROCESS.
+ * Exporting or importing it is therefore an explicit opt-in; by default the
+ * master is drawn from std::random_device, MKFHE_ENTROPY is not read and
+ * mkkg_entropy_get fails.
+ * master: 8 words = 64 hex digits, word 0 first.
+ * mkkg_entropy_replay(1): opt in.  If MKFHE_ENTROPY is set, the journal
+ *   restarts at that master (MKACC_E_ARG, and no opt-in, if it is not 64 hex
+ *   digits); otherwise the current master stays.  mkkg_entropy_replay(0)
+ *   opts out again (the master stays, it is just no longer exported).
  * mkkg_entropy_get: the master (drawn now if no seed-0 call has drawn it yet)
- *   and the number of seed-0 calls made since it was set.
- * mkkg_entropy_set: restart the journal at (master, calls); master NULL draws
- *   a fresh master from std::random_device. */
+ *   and the number of seed-0 calls made since it was set; MKACC_E_ARG unless
+ *   the journal was opted in.
+ * mkkg_entropy_set: restart the journal at (master, calls) and opt in; master
+ *   NULL draws a fresh master from std::random_device. */
+int mkkg_entropy_replay(int enable);
 int mkkg_entropy_get(uint32_t master[8], uint64_t* calls);
 int mkkg_entropy_set(const uint32_t master[8], uint64_t calls);
 

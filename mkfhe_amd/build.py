@@ -47,7 +47,9 @@ def file_id(paths) -> str:
 
 
 def engine_ids() -> dict:
-    return {"header": file_id([ENGINE_HEADER]), "source": file_id(SOURCES + HEADERS)}
+    # this file holds the per-unit compile flags (STEP2_SCHED, UNITS), so it is
+    # part of the source identity: a library built with other flags is stale
+    return {"header": file_id([ENGINE_HEADER]), "source": file_id(SOURCES + HEADERS + [os.path.abspath(__file__)])}
 
 
 def keys_ids() -> dict:
@@ -133,6 +135,10 @@ def compile_engine(out: str, flags: list[str], report: str, verbose: bool = Fals
         r = subprocess.run(cmd, capture_output=True, text=True)
         return name, obj, r
 
+    # a variant always recompiles the host unit too: it carries the build
+    # identity (mkacc_build_info's flags) and the host-side A/B switches
+    if only is not None:
+        only = set(only) | {"engine"}
     units = UNITS if only is None else [u for u in UNITS if u[0] in only]
     with ThreadPoolExecutor(max_workers=_jobs()) as ex:
         results = list(ex.map(unit, units))

@@ -225,6 +225,7 @@ struct mkacc_ctx {
     uint16_t* d_lweB = nullptr;    // MK-LWE: [k][N][Bks][dks]
     uint32_t* d_tv = nullptr;      // test vector NTT(Rx) * N^-1, C4 [N]
     size_t gate_B = 0;
+    uint32_t gate_dks = 0;         // dks d_digits was sized for
     uint8_t* d_digits = nullptr;   // [B][k][dks][N]
     uint32_t* d_bh = nullptr;      // [B] MK-LWE rotation b
     uint32_t* d_gin = nullptr;     // host API staging of gate inputs (grow-only)
@@ -298,7 +299,9 @@ bool use_lat(const mkacc_ctx* c, size_t B) {
 // Step2Cfg::kSvMem).
 size_t step_scratch_words(const mkacc_ctx* c) {
     if (use_dscr(c)) return (size_t)c->dg * kN;
-    if (c->step_ver == 2) return kN;
+#if defined(MKACC_S2_SVMEM) && MKACC_S2_SVMEM
+    if (c->step_ver == 2) return kN;   // A/B build only: the default kernel keeps sumV in registers
+#endif
     return 0;
 }
 
@@ -408,7 +411,9 @@ int launch_batch(mkacc_ctx* c, const uint32_t* d_ct, const uint32_t* d_in, uint3
 int ensure_gate_ws(mkacc_ctx* c, size_t B) {
     int rc = ensure_ws(c, B);
     if (rc) return rc;
-    if (B <= c->gate_B) return MKACC_OK;
+    // d_digits is sized for the key-switching digit count it was allocated with;
+    // a re-upload (or share_ksk) with a different dks must reallocate it
+    if (B <= c->gate_B && c->dks == c->gate_dks) return MKACC_OK;
     if (c->d_digits) HIP_TRY(hipFree(c->d_digits));
     if (c->d_bh) HIP_TRY(hipFree(c->d_bh));
     c->d_digits = nullptr;
@@ -417,6 +422,7 @@ int ensure_gate_ws(mkacc_ctx* c, size_t B) {
     HIP_TRY(hipMalloc(&c->d_digits, B * c->p.k * (size_t)c->dks * kN));
     HIP_TRY(hipMalloc(&c->d_bh, B * c->p.k * 4));   // MK-LWE head rotation b [B], then partial b sums [B][k]
     c->gate_B = B;
+    c->gate_dks = c->dks;
     return MKACC_OK;
 }
 
@@ -562,6 +568,9 @@ int upload_keys_impl(mkacc_ctx* c, const W* evk, const W* pkey) {
             hp[p * kN + c4_index(s)] = (uint32_t)((x * ks) % Q);
         }
     HIP_TRY(hipSetDevice(c->device));
+    // an earlier device batch may still read the old keys on the context stream
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->have_keys = false;
     if (!c->d_keys) HIP_TRY(hipMalloc(&c->d_keys, host.size() * 4));
     if (!c->d_pkey) HIP_TRY(hipMalloc(&c->d_pkey, hp.size() * 4));
     HIP_TRY(hipMemcpy(c->d_keys, host.data(), host.size() * 4, hipMemcpyHostToDevice));
@@ -741,6 +750,8 @@ int wide_upload_keys(mkacc_ctx* c, const W* evk, const W* pkey) {
         hp[s] = mont((uint64_t)pkey[s]);
     }
     HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->have_keys = false;
     if (!c->d_wkeys) HIP_TRY(hipMalloc(&c->d_wkeys, host.size() * 8));
     if (!c->d_wpkey) HIP_TRY(hipMalloc(&c->d_wpkey, pw * 8));
     HIP_TRY(hipMemcpy(c->d_wkeys, host.data(), host.size() * 8, hipMemcpyHostToDevice));
@@ -1273,15 +1284,29 @@ uint32_t mkacc_ks_digits(const mkacc_ks_params* ks) {
 }
 
 namespace {
-int check_ks(mkacc_ctx* c, const mkacc_ks_params* ks) {
+// Key-switching shape of an upload.  Validated first and committed to the
+// context (ks_commit) only once the new key is on the device, so a failed
+// upload never leaves have_ksk set with a key of another shape.
+struct KsPlan {
+    mkacc_ks_params ks;
+    uint32_t dks, n_pad;
+};
+int check_ks(const mkacc_ks_params* ks, KsPlan& plan) {
     if (!ks) return fail(MKACC_E_ARG, "null key-switching parameters");
     if (ks->qKS < 2 || ks->qKS > 65535) return fail(MKACC_E_UNSUPPORTED, "engine supports qKS < 2^16");
     if (ks->baseKS < 2 || ks->baseKS > 256) return fail(MKACC_E_UNSUPPORTED, "engine supports baseKS <= 256");
     if (ks->n_out == 0 || ks->n_out > 4096) return fail(MKACC_E_ARG, "bad output dimension");
-    c->ks = *ks;
-    c->dks = ks_digit_count(ks->qKS, ks->baseKS);
-    c->n_pad = (ks->n_out + kKsTile - 1) / kKsTile * kKsTile;
+    plan.ks = *ks;
+    plan.dks = ks_digit_count(ks->qKS, ks->baseKS);
+    plan.n_pad = (ks->n_out + kKsTile - 1) / kKsTile * kKsTile;
     return MKACC_OK;
+}
+// the old key is gone from here on: no gate may run until ks_commit
+void ks_drop(mkacc_ctx* c) { c->have_ksk = false; }
+void ks_commit(mkacc_ctx* c, const KsPlan& plan) {
+    c->ks = plan.ks;
+    c->dks = plan.dks;
+    c->n_pad = plan.n_pad;
 }
 }  // namespace
 
@@ -1290,9 +1315,10 @@ int mkacc_upload_ksk_mntru(mkacc_ctx* c, const mkacc_ks_params* ks, const uint32
     std::lock_guard<std::mutex> g(c->mu);
     if (c->wide) return fail(MKACC_E_UNSUPPORTED, "the 64-bit word path covers EvalAcc only; NAND gates need Q < 2^27");
     if (c->method_class != XZW) return fail(MKACC_E_ARG, "KeySwitch2 keys belong to the MKNTRU method");
-    int rc = check_ks(c, ks);
+    KsPlan plan;
+    int rc = check_ks(ks, plan);
     if (rc) return rc;
-    const uint32_t k = c->p.k, dks = c->dks, n = ks->n_out, npad = c->n_pad;
+    const uint32_t k = c->p.k, dks = plan.dks, n = ks->n_out, npad = plan.n_pad;
     const size_t L = (size_t)dks * kN;
     // reference row l = j*dks + t  ->  device row t*N + j, columns padded to n_pad
     std::vector<uint16_t> h((size_t)k * L * npad, 0);
@@ -1307,10 +1333,12 @@ int mkacc_upload_ksk_mntru(mkacc_ctx* c, const mkacc_ks_params* ks, const uint32
                 }
             }
     HIP_TRY(hipSetDevice(c->device));
+    ks_drop(c);
     if (c->d_ksk) HIP_TRY(hipFree(c->d_ksk));
     c->d_ksk = nullptr;
     HIP_TRY(hipMalloc(&c->d_ksk, h.size() * 2));
     HIP_TRY(hipMemcpy(c->d_ksk, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+    ks_commit(c, plan);
     c->have_ksk = true;
     return MKACC_OK;
 }
@@ -1321,9 +1349,10 @@ int mkacc_upload_ksk_mklwe(mkacc_ctx* c, const mkacc_ks_params* ks, const uint32
     if (c->wide) return fail(MKACC_E_UNSUPPORTED, "the 64-bit word path covers EvalAcc only; NAND gates need Q < 2^27");
     if (c->method_class != XZW_B) return fail(MKACC_E_ARG, "MK-LWE KeySwitch keys belong to the MKNTRU_LWE method");
     if (int rc = reject_mkntru_b(c)) return rc;
-    int rc = check_ks(c, ks);
+    KsPlan plan;
+    int rc = check_ks(ks, plan);
     if (rc) return rc;
-    const size_t rows = (size_t)c->p.k * kN * ks->baseKS * c->dks;
+    const size_t rows = (size_t)c->p.k * kN * ks->baseKS * plan.dks;
     std::vector<uint16_t> ha(rows * ks->n_out), hb(rows);
     for (size_t i = 0; i < ha.size(); ++i) {
         if (A[i] >= ks->qKS) return fail(MKACC_E_RANGE, "A word not a canonical residue mod qKS");
@@ -1334,6 +1363,7 @@ int mkacc_upload_ksk_mklwe(mkacc_ctx* c, const mkacc_ks_params* ks, const uint32
         hb[i] = (uint16_t)B[i];
     }
     HIP_TRY(hipSetDevice(c->device));
+    ks_drop(c);
     if (c->d_lweA) HIP_TRY(hipFree(c->d_lweA));
     if (c->d_lweB) HIP_TRY(hipFree(c->d_lweB));
     c->d_lweA = nullptr;
@@ -1342,6 +1372,7 @@ int mkacc_upload_ksk_mklwe(mkacc_ctx* c, const mkacc_ks_params* ks, const uint32
     HIP_TRY(hipMalloc(&c->d_lweB, hb.size() * 2));
     HIP_TRY(hipMemcpy(c->d_lweA, ha.data(), ha.size() * 2, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->d_lweB, hb.data(), hb.size() * 2, hipMemcpyHostToDevice));
+    ks_commit(c, plan);
     c->have_ksk = true;
     return MKACC_OK;
 }
@@ -1352,10 +1383,9 @@ namespace {
 // the device key-switching uploads: layout kernel(s) on the context stream, then
 // the range flag (d_bad[1]) read back; no keys are kept if a word is out of range
 template <class L>
-int ksk_device_finish(mkacc_ctx* c, L&& launch) {
+int ksk_device_finish(mkacc_ctx* c, const KsPlan& plan, L&& launch) {
     uint32_t* kbad = c->d_bad + 1;
     HIP_TRY(hipMemsetAsync(kbad, 0, 4, c->stream));
-    c->have_ksk = false;
     int rc = launch(kbad);
     if (rc) return rc;
     HIP_TRY(hipGetLastError());
@@ -1363,6 +1393,7 @@ int ksk_device_finish(mkacc_ctx* c, L&& launch) {
     HIP_TRY(hipMemcpyAsync(&bad, kbad, 4, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     if (bad) return fail(MKACC_E_RANGE, "key-switching key word not a canonical residue mod qKS");
+    ks_commit(c, plan);
     c->have_ksk = true;
     return MKACC_OK;
 }
@@ -1375,17 +1406,19 @@ int mkacc_upload_ksk_mntru_device(mkacc_ctx* c, const mkacc_ks_params* ks, const
     std::lock_guard<std::mutex> g(c->mu);
     if (c->wide) return fail(MKACC_E_UNSUPPORTED, "the 64-bit word path covers EvalAcc only; NAND gates need Q < 2^27");
     if (c->method_class != XZW) return fail(MKACC_E_ARG, "KeySwitch2 keys belong to the MKNTRU method");
-    int rc = check_ks(c, ks);
+    KsPlan plan;
+    int rc = check_ks(ks, plan);
     if (rc) return rc;
     HIP_TRY(hipSetDevice(c->device));
-    const size_t w = (size_t)c->p.k * c->dks * kN * c->n_pad;
+    const size_t w = (size_t)c->p.k * plan.dks * kN * plan.n_pad;
+    ks_drop(c);
     if (c->d_ksk) HIP_TRY(hipFree(c->d_ksk));
     c->d_ksk = nullptr;
     HIP_TRY(hipMalloc(&c->d_ksk, w * 2));
-    return ksk_device_finish(c, [&](uint32_t* kbad) {
+    return ksk_device_finish(c, plan, [&](uint32_t* kbad) {
         hipLaunchKernelGGL(ksk_mntru_layout_kernel, dim3((unsigned)((w + 255) / 256)), dim3(256), 0, c->stream,
-                           (const uint32_t*)d_ksk, c->d_ksk, c->p.k, c->dks, c->ks.n_out, c->n_pad,
-                           (uint32_t)c->ks.qKS, kbad);
+                           (const uint32_t*)d_ksk, c->d_ksk, c->p.k, plan.dks, plan.ks.n_out, plan.n_pad,
+                           (uint32_t)plan.ks.qKS, kbad);
         return MKACC_OK;
     });
 }
@@ -1396,16 +1429,18 @@ int mkacc_upload_ksk_mklwe_device(mkacc_ctx* c, const mkacc_ks_params* ks, const
     if (c->wide) return fail(MKACC_E_UNSUPPORTED, "the 64-bit word path covers EvalAcc only; NAND gates need Q < 2^27");
     if (c->method_class != XZW_B) return fail(MKACC_E_ARG, "MK-LWE KeySwitch keys belong to the MKNTRU_LWE method");
     if (int rc = reject_mkntru_b(c)) return rc;
-    int rc = check_ks(c, ks);
+    KsPlan plan;
+    int rc = check_ks(ks, plan);
     if (rc) return rc;
     HIP_TRY(hipSetDevice(c->device));
-    const size_t rows = (size_t)c->p.k * kN * ks->baseKS * c->dks, wa = rows * ks->n_out;
+    const size_t rows = (size_t)c->p.k * kN * ks->baseKS * plan.dks, wa = rows * ks->n_out;
+    ks_drop(c);
     if (c->d_lweA) HIP_TRY(hipFree(c->d_lweA));
     if (c->d_lweB) HIP_TRY(hipFree(c->d_lweB));
     c->d_lweA = c->d_lweB = nullptr;
     HIP_TRY(hipMalloc(&c->d_lweA, wa * 2));
     HIP_TRY(hipMalloc(&c->d_lweB, rows * 2));
-    return ksk_device_finish(c, [&](uint32_t* kbad) {
+    return ksk_device_finish(c, plan, [&](uint32_t* kbad) {
         hipLaunchKernelGGL(ksk_narrow_kernel, dim3((unsigned)((wa + 255) / 256)), dim3(256), 0, c->stream,
                            (const uint32_t*)d_A, c->d_lweA, wa, (uint32_t)ks->qKS, kbad);
         hipLaunchKernelGGL(ksk_narrow_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, c->stream,
@@ -1635,10 +1670,16 @@ int ensure_like(mkacc_ctx* dst, T*& d, size_t words) {
     return MKACC_OK;
 }
 
-// member i > 0 takes member 0's converted keys (device layout) by device copy
-int share_keys(mkacc_ctx* dst, const mkacc_ctx* src) {
+// Member i > 0 takes member 0's converted keys (device layout) by device copy.
+// Two phases so the copies to all members run concurrently (one xGMI link per
+// peer on a fully connected node): *_enqueue allocates and enqueues the copy on
+// the member's stream, *_finish waits for it and marks the keys present.
+int share_keys_enqueue(mkacc_ctx* dst, const mkacc_ctx* src) {
     const size_t kw = (size_t)src->p.k * (src->p.n + 1) * key_block_words(src), pw = (size_t)src->p.k * src->dg * kN;
     int rc;
+    HIP_TRY(hipSetDevice(dst->device));
+    HIP_TRY(hipStreamSynchronize(dst->stream));   // no batch of this member still reads the old keys
+    dst->have_keys = false;
     if (src->wide) {
         if ((rc = ensure_like(dst, dst->d_wkeys, kw)) || (rc = ensure_like(dst, dst->d_wpkey, pw))) return rc;
         if ((rc = dev_copy(dst, dst->d_wkeys, src, src->d_wkeys, kw * 8)) ||
@@ -1650,15 +1691,19 @@ int share_keys(mkacc_ctx* dst, const mkacc_ctx* src) {
             (rc = dev_copy(dst, dst->d_pkey, src, src->d_pkey, pw * 4)))
             return rc;
     }
+    return MKACC_OK;
+}
+int share_keys_finish(mkacc_ctx* dst, const mkacc_ctx*) {
+    HIP_TRY(hipSetDevice(dst->device));
     HIP_TRY(hipStreamSynchronize(dst->stream));
     dst->have_keys = true;
     return MKACC_OK;
 }
 
-int share_ksk(mkacc_ctx* dst, const mkacc_ctx* src) {
-    dst->ks = src->ks;
-    dst->dks = src->dks;
-    dst->n_pad = src->n_pad;
+int share_ksk_enqueue(mkacc_ctx* dst, const mkacc_ctx* src) {
+    HIP_TRY(hipSetDevice(dst->device));
+    HIP_TRY(hipStreamSynchronize(dst->stream));
+    ks_drop(dst);
     const size_t L = (size_t)src->dks * kN;
     int rc;
     if (src->method_class == XZW) {
@@ -1677,21 +1722,48 @@ int share_ksk(mkacc_ctx* dst, const mkacc_ctx* src) {
             (rc = dev_copy(dst, dst->d_lweB, src, src->d_lweB, rows * 2)))
             return rc;
     }
+    return MKACC_OK;
+}
+int share_ksk_finish(mkacc_ctx* dst, const mkacc_ctx* src) {
+    HIP_TRY(hipSetDevice(dst->device));
     HIP_TRY(hipStreamSynchronize(dst->stream));
+    ks_commit(dst, KsPlan{src->ks, src->dks, src->n_pad});
     dst->have_ksk = true;
     return MKACC_OK;
 }
 
-// upload through member 0 (its host-side conversion and checks), then share
-template <class F, class S>
-int group_upload(mkacc_group* g, F&& upload0, S&& share) {
+// Upload through member 0 (its host-side conversion and checks), wait for
+// member 0's stream (the layout conversion may run there), then copy to every
+// other member concurrently: all copies are enqueued before the first wait.
+template <class F, class E, class W>
+int group_upload(mkacc_group* g, F&& upload0, E&& enqueue, W&& finish) {
     if (!g || g->m.empty()) return fail(MKACC_E_ARG, "null group");
     int rc = upload0(g->m[0]);
     if (rc) return rc;
-    for (size_t i = 1; i < g->m.size(); ++i) {
-        std::lock_guard<std::mutex> lk(g->m[i]->mu);
-        if ((rc = share(g->m[i], g->m[0]))) return rc;
+    mkacc_ctx* src = g->m[0];
+    {
+        std::lock_guard<std::mutex> lk(src->mu);
+        HIP_TRY(hipSetDevice(src->device));
+        HIP_TRY(hipStreamSynchronize(src->stream));
     }
+    std::vector<std::unique_lock<std::mutex>> locks;
+    for (size_t i = 1; i < g->m.size(); ++i) locks.emplace_back(g->m[i]->mu);
+    int first = MKACC_OK;
+    std::string msg;
+    size_t started = 1;
+    for (; started < g->m.size(); ++started)
+        if ((rc = enqueue(g->m[started], src))) {
+            first = rc;
+            msg = mkacc_last_error();
+            break;
+        }
+    // wait for every copy that was enqueued, even after a failure
+    for (size_t i = 1; i < started; ++i)
+        if ((rc = finish(g->m[i], src)) && !first) {
+            first = rc;
+            msg = mkacc_last_error();
+        }
+    if (first) return fail(first, msg);
     return MKACC_OK;
 }
 
@@ -1762,16 +1834,20 @@ uint32_t mkacc_group_size(const mkacc_group* g) { return g ? (uint32_t)g->m.size
 mkacc_ctx* mkacc_group_member(mkacc_group* g, uint32_t i) { return g && i < g->m.size() ? g->m[i] : nullptr; }
 
 int mkacc_group_upload_keys(mkacc_group* g, const uint32_t* evk, const uint32_t* pkey) {
-    return group_upload(g, [&](mkacc_ctx* c) { return mkacc_upload_keys(c, evk, pkey); }, share_keys);
+    return group_upload(g, [&](mkacc_ctx* c) { return mkacc_upload_keys(c, evk, pkey); }, share_keys_enqueue,
+                        share_keys_finish);
 }
 int mkacc_group_upload_keys_u64(mkacc_group* g, const uint64_t* evk, const uint64_t* pkey) {
-    return group_upload(g, [&](mkacc_ctx* c) { return mkacc_upload_keys_u64(c, evk, pkey); }, share_keys);
+    return group_upload(g, [&](mkacc_ctx* c) { return mkacc_upload_keys_u64(c, evk, pkey); }, share_keys_enqueue,
+                        share_keys_finish);
 }
 int mkacc_group_upload_ksk_mntru(mkacc_group* g, const mkacc_ks_params* ks, const uint32_t* ksk) {
-    return group_upload(g, [&](mkacc_ctx* c) { return mkacc_upload_ksk_mntru(c, ks, ksk); }, share_ksk);
+    return group_upload(g, [&](mkacc_ctx* c) { return mkacc_upload_ksk_mntru(c, ks, ksk); }, share_ksk_enqueue,
+                        share_ksk_finish);
 }
 int mkacc_group_upload_ksk_mklwe(mkacc_group* g, const mkacc_ks_params* ks, const uint32_t* A, const uint32_t* B) {
-    return group_upload(g, [&](mkacc_ctx* c) { return mkacc_upload_ksk_mklwe(c, ks, A, B); }, share_ksk);
+    return group_upload(g, [&](mkacc_ctx* c) { return mkacc_upload_ksk_mklwe(c, ks, A, B); }, share_ksk_enqueue,
+                        share_ksk_finish);
 }
 
 int mkacc_group_eval_batch(mkacc_group* g, const uint32_t* ct, const uint32_t* acc_in, uint32_t* acc_out, size_t B) {

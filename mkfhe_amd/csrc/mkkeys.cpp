@@ -44,11 +44,13 @@ int fail(int code, const std::string& msg) {
 // reference's behaviour: fresh keys every call): ChaCha20 with a 256-bit call
 // key, one stream per (a, b, c) id in the nonce, so no secret is a function of
 // a short seed.  The call keys come from the process's entropy journal: a
-// 256-bit master key (MKFHE_ENTROPY, 64 hex digits, or std::random_device when
-// first needed) and a counter of seed-0 calls; call key = ChaCha20 block of the
-// master at nonce = counter.  mkkg_entropy_get reports the master, so a run
-// whose gates decrypt wrong can be replayed exactly (mkkg_entropy_set or
-// MKFHE_ENTROPY) -- the reference's clock-seeded keys (binfhe-base-scheme.cpp:111,
+// 256-bit master key (std::random_device when first needed) and a counter of
+// seed-0 calls; call key = ChaCha20 block of the master at nonce = counter.
+// Whoever holds the master holds every seed-0 key of the process, so exporting
+// it is an explicit opt-in: mkkg_entropy_replay(1) (which is also the only
+// place MKFHE_ENTROPY is read; a malformed value is an error) or
+// mkkg_entropy_set.  With it, a run whose gates decrypt wrong can be replayed
+// exactly -- the reference's clock-seeded keys (binfhe-base-scheme.cpp:111,
 // mntru-pke.cpp:27) cannot be.
 // ---------------------------------------------------------------------------
 inline uint64_t splitmix(uint64_t& x) {
@@ -70,6 +72,7 @@ void chacha_block(const uint32_t key[8], uint32_t n0, uint32_t n1, uint32_t out[
 struct Entropy {
     std::mutex mu;
     bool init = false;
+    bool replay = false;   // master exportable (mkkg_entropy_replay / mkkg_entropy_set)
     uint32_t master[8] = {};
     uint64_t calls = 0;
 };
@@ -95,10 +98,8 @@ bool parse_hex256(const char* h, uint32_t out[8]) {
 // caller holds e.mu
 void entropy_init_locked(Entropy& e) {
     if (e.init) return;
-    if (!parse_hex256(std::getenv("MKFHE_ENTROPY"), e.master)) {
-        std::random_device rd;
-        for (auto& w : e.master) w = rd();
-    }
+    std::random_device rd;
+    for (auto& w : e.master) w = rd();
     e.calls = 0;
     e.init = true;
 }
@@ -506,10 +507,36 @@ const char* mkkg_build_info(void) {
     return info.c_str();
 }
 
+int mkkg_entropy_replay(int enable) try {
+    Entropy& e = entropy();
+    std::lock_guard<std::mutex> lk(e.mu);
+    if (!enable) {
+        e.replay = false;
+        return MKACC_OK;
+    }
+    if (const char* env = std::getenv("MKFHE_ENTROPY")) {
+        uint32_t m[8];
+        if (!parse_hex256(env, m))
+            return fail(MKACC_E_ARG, "MKFHE_ENTROPY must be 64 hex digits; the replay journal was not enabled");
+        std::memcpy(e.master, m, sizeof m);
+        e.calls = 0;
+        e.init = true;
+    } else {
+        entropy_init_locked(e);
+    }
+    e.replay = true;
+    return MKACC_OK;
+} catch (const std::exception& e) {
+    return fail(MKACC_E_ARG, std::string("mkkg_entropy_replay: ") + e.what());
+}
+
 int mkkg_entropy_get(uint32_t master[8], uint64_t* calls) try {
     if (!master) return fail(MKACC_E_ARG, "null argument");
     Entropy& e = entropy();
     std::lock_guard<std::mutex> lk(e.mu);
+    if (!e.replay)
+        return fail(MKACC_E_ARG, "the entropy master is not exportable: call mkkg_entropy_replay(1) first "
+                                 "(whoever holds the master holds every seed-0 key of the process)");
     entropy_init_locked(e);
     std::memcpy(master, e.master, sizeof e.master);
     if (calls) *calls = e.calls;
@@ -529,6 +556,7 @@ int mkkg_entropy_set(const uint32_t master[8], uint64_t calls) try {
     }
     e.calls = calls;
     e.init = true;
+    e.replay = true;
     return MKACC_OK;
 } catch (const std::exception& e) {
     return fail(MKACC_E_ARG, std::string("mkkg_entropy_set: ") + e.what());

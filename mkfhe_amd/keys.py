@@ -70,6 +70,7 @@ SIGNATURES = {
     "mkkg_file_read_section": (_int, [ctypes.c_char_p, ctypes.c_char_p, _u32p, _u64]),
     "mkkg_ntt_forward": (_int, [_pp, _u32p, _u32p, _sz]),
     "mkkg_ntt_inverse": (_int, [_pp, _u32p, _u32p, _sz]),
+    "mkkg_entropy_replay": (_int, [_int]),
     "mkkg_entropy_get": (_int, [_u32p, ctypes.POINTER(_u64)]),
     "mkkg_entropy_set": (_int, [_u32p, _u64]),
     "mkkg_last_error": (ctypes.c_char_p, []),
@@ -105,8 +106,16 @@ def load():
 
 # ---- seed-0 entropy journal (mkkg_entropy_get / _set) -------------------------------------
 
+def entropy_replay(enable: bool = True):
+    """Opt in to (or out of) exporting the seed-0 master; opting in reads MKFHE_ENTROPY
+    if set (an error if it is not 64 hex digits).  Whoever holds the master holds
+    every seed-0 key of the process (include/mkfhe_keys.h)."""
+    _check(load().mkkg_entropy_replay(1 if enable else 0))
+
+
 def entropy_get() -> tuple[str, int]:
-    """(master key as 64 hex digits = MKFHE_ENTROPY, seed-0 calls since it was set)"""
+    """(master key as 64 hex digits = MKFHE_ENTROPY, seed-0 calls since it was set);
+    needs a prior entropy_replay() or entropy_set()"""
     m = np.zeros(8, np.uint32)
     calls = _u64()
     _check(load().mkkg_entropy_get(_p(m), ctypes.byref(calls)))

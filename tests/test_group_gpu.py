@@ -84,3 +84,85 @@ def test_group_nand_gates_match_single_context(ps, method):
         assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
     else:
         assert np.array_equal(outs[0], outs[1])
+
+
+def _device_count():
+    try:
+        import torch
+        return torch.cuda.device_count()
+    except Exception:
+        return 0
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(_device_count() < 2, reason="needs two GPUs (the peer-copy path between distinct devices)")
+def test_group_on_distinct_devices_matches_single_context(oracle):
+    """Members on two distinct GPUs take the hipMemcpyPeerAsync path of the key
+    sharing (ordered after member 0's stream).  Skipped on a one-GPU box: until an
+    8-GPU node runs it, outputs of groups spanning devices are parity unpinned."""
+    import mkfhe_amd as mk
+    k, n, q, baseG, B = 2, 6, 45181, 1 << 7, 9
+    _, evk, pkey, ct, acc = make_case(oracle, oracle.XZW, k, n, q, baseG, B, seed=77)
+    params = mk.make_params(mk.MKNTRU, k, n, N, Q_MK, q, baseG)
+    one = mk.MKAccumulatorEngine(params, 0)
+    one.upload_keys(evk.astype(np.uint32), pkey.astype(np.uint32))
+    want = one.eval_batch(ct.astype(np.uint32), acc.astype(np.uint32))
+    grp = mk.MKAccumulatorGroup(params, [0, 1])
+    grp.upload_keys(evk.astype(np.uint32), pkey.astype(np.uint32))
+    assert np.array_equal(grp.eval_batch(ct.astype(np.uint32), acc.astype(np.uint32)), want)
+
+
+@pytest.mark.gpu
+def test_ksk_reupload_with_another_digit_count_resizes_the_gate_workspace(oracle):
+    """a key-switching key re-uploaded with more digits (baseKS 32 -> 8,
+    dks 4 -> 6) must reallocate the digit workspace sized for the old key.  The
+    gates of the second key must equal those of a fresh context holding only it
+    (any key words: both contexts compute the same function of the same key)."""
+    import mkfhe_amd as mk
+    k, n, q, baseG, B = 2, 8, 45181, 1 << 9, 6
+    _, evk, pkey, _, _ = make_case(oracle, oracle.XZW, k, n, q, baseG, B, seed=91)
+    params = mk.make_params(mk.MKNTRU, k, n, N, Q_MK, q, baseG)
+    rng = np.random.default_rng(5)
+    nand = rng.integers(0, q, (k, n), dtype=np.uint32)
+    c1 = rng.integers(0, q, (B, k, n), dtype=np.uint32)
+    c2 = rng.integers(0, q, (B, k, n), dtype=np.uint32)
+    ksk = {}
+    for base in (32, 8):
+        dks = int(np.ceil(np.log(q) / np.log(base)))
+        ksk[base] = rng.integers(0, q, (k, N * dks, n), dtype=np.uint32)
+    reused = mk.MKAccumulatorEngine(params, 0)
+    reused.upload_keys(evk.astype(np.uint32), pkey.astype(np.uint32))
+    reused.upload_ksk_mntru(ksk[32], q, 32, n)
+    reused.eval_nand_mntru(nand, c1, c2)          # sizes the workspace for dks = 4
+    reused.upload_ksk_mntru(ksk[8], q, 8, n)
+    got = reused.eval_nand_mntru(nand, c1, c2)
+    fresh = mk.MKAccumulatorEngine(params, 0)
+    fresh.upload_keys(evk.astype(np.uint32), pkey.astype(np.uint32))
+    fresh.upload_ksk_mntru(ksk[8], q, 8, n)
+    assert np.array_equal(got, fresh.eval_nand_mntru(nand, c1, c2))
+
+
+@pytest.mark.gpu
+def test_failed_ksk_upload_leaves_no_key_of_another_shape(oracle):
+    """A key-switching upload that fails its range check must not leave the
+    context claiming a key (the shape used to be committed first)."""
+    import mkfhe_amd as mk
+    k, n, q, baseG, B = 2, 8, 45181, 1 << 9, 3
+    _, evk, pkey, _, _ = make_case(oracle, oracle.XZW, k, n, q, baseG, B, seed=92)
+    params = mk.make_params(mk.MKNTRU, k, n, N, Q_MK, q, baseG)
+    e = mk.MKAccumulatorEngine(params, 0)
+    e.upload_keys(evk.astype(np.uint32), pkey.astype(np.uint32))
+    rng = np.random.default_rng(6)
+    good = rng.integers(0, q, (k, N * 4, n), dtype=np.uint32)
+    e.upload_ksk_mntru(good, q, 32, n)
+    bad = rng.integers(0, q, (k, N * 6, n), dtype=np.uint32)
+    bad[1, 7, 3] = q                               # not a canonical residue
+    with pytest.raises(mk.MkaccError):
+        e.upload_ksk_mntru(bad, q, 8, n)
+    nand = rng.integers(0, q, (k, n), dtype=np.uint32)
+    c = rng.integers(0, q, (B, k, n), dtype=np.uint32)
+    # the old key (dks 4) is still the committed one: gates run with it
+    fresh = mk.MKAccumulatorEngine(params, 0)
+    fresh.upload_keys(evk.astype(np.uint32), pkey.astype(np.uint32))
+    fresh.upload_ksk_mntru(good, q, 32, n)
+    assert np.array_equal(e.eval_nand_mntru(nand, c, c[::-1].copy()), fresh.eval_nand_mntru(nand, c, c[::-1].copy()))

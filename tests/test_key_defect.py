@@ -22,6 +22,7 @@ def test_replayed_key_set_has_the_recorded_defect(oracle):
     from mkfhe_amd import keys as K
     p = K.paramset("STD128_MKNTRU", 0)
     orc = oracle.Oracle(oracle.XZW, p.acc.k, p.acc.n, 2048, p.acc.Q, p.acc.q, p.acc.baseG)
+    K.entropy_replay()
     saved = K.entropy_get()
     try:
         K.entropy_set(MASTER)
@@ -36,6 +37,7 @@ def test_r_defect_scan_is_clean_on_a_normal_set(oracle):
     import fresh_key_rate as F
     from mkfhe_amd import keys as K
     p = K.paramset("STD100_MKNTRU", 0)
+    K.entropy_replay()
     saved = K.entropy_get()
     try:
         K.entropy_set("00" * 32)

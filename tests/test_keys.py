@@ -287,7 +287,7 @@ def test_keys_header_symbols_bound_and_exported(lib):
     assert names == set(K.SIGNATURES)
     for n in names:
         assert hasattr(lib, n), n
-    assert lib.mkkg_abi_version() == 2
+    assert lib.mkkg_abi_version() == 3
 
 
 def test_key_files_roundtrip(mntru_keys, tmp_path):

@@ -107,7 +107,8 @@ def test_entropy_journal_replays_seed0_keys():
 
 
 def test_entropy_from_environment():
-    code = ("from mkfhe_amd import keys as K; p = K.paramset('STD100_MKNTRU', 0); "
+    """MKFHE_ENTROPY is read only by an explicit opt-in (entropy_replay)."""
+    code = ("from mkfhe_amd import keys as K; p = K.paramset('STD100_MKNTRU', 0); K.entropy_replay(); "
             "print(K.entropy_get()[0]); print(int(K.mntru_keygen(p, 0).F.sum()))")
     hexkey = "0123456789abcdef" * 4
     runs = [subprocess.run([sys.executable, "-c", code], cwd=ROOT, env={**os.environ, "MKFHE_ENTROPY": hexkey},
@@ -115,6 +116,27 @@ def test_entropy_from_environment():
     assert all(r.returncode == 0 for r in runs), runs[0].stderr
     assert runs[0].stdout.split()[0] == hexkey
     assert runs[0].stdout == runs[1].stdout
+
+
+def test_entropy_is_not_exported_or_overridden_without_opt_in():
+    """the master is secret material.  Without entropy_replay() the
+    environment does not fix the keys and the master cannot be read; a malformed
+    MKFHE_ENTROPY is an error at opt-in, not silently ignored."""
+    code = ("import sys; from mkfhe_amd import keys as K; p = K.paramset('STD100_MKNTRU', 0)\n"
+            "print(int(K.mntru_keygen(p, 0).F.sum()))\n"
+            "try:\n    K.entropy_get(); print('exported')\nexcept Exception as e:\n    print('refused')\n"
+            "try:\n    K.entropy_replay(); print('opted-in')\nexcept Exception as e:\n    print('bad-env', e)\n")
+    hexkey = "0123456789abcdef" * 4
+    runs = [subprocess.run([sys.executable, "-c", code], cwd=ROOT, env={**os.environ, "MKFHE_ENTROPY": hexkey},
+                           capture_output=True, text=True, timeout=120) for _ in range(2)]
+    assert all(r.returncode == 0 for r in runs), runs[0].stderr
+    out = [r.stdout.split() for r in runs]
+    assert out[0][1] == "refused" and out[0][2] == "opted-in"
+    assert out[0][0] != out[1][0]            # fresh keys: the environment was not read
+    bad = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env={**os.environ, "MKFHE_ENTROPY": "xyz"},
+                         capture_output=True, text=True, timeout=120)
+    assert bad.returncode == 0, bad.stderr
+    assert "bad-env" in bad.stdout and "64 hex digits" in bad.stdout
 
 
 def test_encrypt_count_limit_is_an_error_not_a_crash():
