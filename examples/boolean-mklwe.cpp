@@ -44,6 +44,11 @@ int main(int argc, char** argv) {
     // Generate the bootstrapping keys (refresh and switching keys)
     std::cout << "Generating the bootstrapping keys..." << std::endl;
     cc.MKBTKeyGen(sk);
+    if (cc.GetRDefects())   // the reference's KeyGenXZW r-defect (mk-acc-xzw.cpp:160-167), reported here
+        std::cout << "warning: " << cc.GetRDefects()
+                  << " bootstrapping key(s) drew a nonzero DggR sample r; gates using them may decrypt wrong "
+                     "(regenerate the keys, or MKBTKeyGen(sk, RDefectPolicy::RESAMPLE))"
+                  << std::endl;
     std::cout << "Completed the key generation." << std::endl;
 
     int bad = 0;

@@ -75,6 +75,34 @@ inline void check(int rc) {
     }
 }
 
+// MKBTKeyGen under RDefectPolicy::REJECT drew a bootstrapping key whose DggR
+// sample r is nonzero (the reference's KeyGenXZW defect, mk-acc-xzw.cpp:160-167;
+// include/mkfhe_keys.h)
+class key_defect_error : public config_error {
+public:
+    using config_error::config_error;
+};
+
+// Translate a status of the key library (libmkfhe_keys, same codes) with its own error text.
+inline void checkk(int rc) {
+    if (rc == MKACC_OK) return;
+    const std::string msg = mkkg_last_error();
+    switch (rc) {
+        case MKKG_E_RDEFECT: throw key_defect_error(msg);
+        case MKACC_E_ARG:
+        case MKACC_E_NOKEYS:
+        case MKACC_E_UNSUPPORTED: throw config_error(msg);
+        case MKACC_E_RANGE: throw math_error(msg);
+        default: throw device_error(msg);
+    }
+}
+
+// What MKBTKeyGen does about a bootstrapping key with DggR sample r != 0
+// (mkkg_acc_keygen_ex): KEEP = the reference's keys (counted, GetRDefects()),
+// REJECT = key_defect_error, RESAMPLE = redraw r in the affected slots.
+enum class RDefectPolicy : uint32_t { KEEP = MKKG_RDEFECT_KEEP, REJECT = MKKG_RDEFECT_REJECT,
+                                      RESAMPLE = MKKG_RDEFECT_RESAMPLE };
+
 // ---- enums (binfhe-constants.h:129-137) ---------------------------------------
 enum BINFHE_METHOD { INVALID_METHOD = 0, AP, GINX, LMKCDEY, MKNTRU, MKNTRU_B, MKNTRU_LWE };
 enum Format { EVALUATION = 0, COEFFICIENT = 1 };
@@ -606,7 +634,7 @@ public:
         if (devices.empty()) throw config_error("no device");
         m_method = method;
         m_params = UniEncCryptoParams::FromParamSet(ParamSetName(set), method);
-        check(mkkg_paramset(ParamSetName(set), to_abi_method(method), &m_kp));
+        checkk(mkkg_paramset(ParamSetName(set), to_abi_method(method), &m_kp));
         m_have_kp = true;
         reset(devices);
     }
@@ -632,12 +660,12 @@ public:
     // run that enabled replay with MKFHE_ENTROPY=<master> repeats every seed-0
     // key and encryption of a run that made the same calls
     // (tools/fresh_key_rate.py --replay recomputes its gates on the CPU oracle).
-    static void EnableEntropyReplay(bool enable = true) { check(mkkg_entropy_replay(enable ? 1 : 0)); }
+    static void EnableEntropyReplay(bool enable = true) { checkk(mkkg_entropy_replay(enable ? 1 : 0)); }
     // The 64-hex-digit master and the number of seed-0 calls made under it;
     // config_error unless EnableEntropyReplay() ran first.
     static std::string GetEntropy(uint64_t* calls = nullptr) {
         uint32_t m[8];
-        check(mkkg_entropy_get(m, calls));
+        checkk(mkkg_entropy_get(m, calls));
         char buf[65];
         for (int i = 0; i < 8; ++i) std::snprintf(buf + 8 * i, 9, "%08x", m[i]);
         return std::string(buf, 64);
@@ -654,7 +682,7 @@ public:
         need_keyparams();
         const uint32_t k = m_kp.acc.k, n = m_kp.acc.n;
         std::vector<uint32_t> F((size_t)k * n * n), Fi((size_t)k * n * n);
-        check(mkkg_mntru_keygen(&m_kp, next_seed(), F.data(), Fi.data()));
+        checkk(mkkg_mntru_keygen(&m_kp, next_seed(), F.data(), Fi.data()));
         return std::make_shared<const MNTRUPrivateKeyImpl>(k, n, m_kp.ks.qKS, std::move(F), std::move(Fi));
     }
     MKLWEPrivateKey MKLWE_KeyGen() const {
@@ -662,39 +690,45 @@ public:
         if (m_kp.lwe_keydist != MKKG_DIST_BINARY) throw config_error("Support BINARY PrivateKey Only");
         const uint32_t k = m_kp.acc.k, n = m_kp.acc.n;
         std::vector<uint32_t> s((size_t)k * n);
-        check(mkkg_mklwe_keygen(&m_kp, next_seed(), s.data()));
+        checkk(mkkg_mklwe_keygen(&m_kp, next_seed(), s.data()));
         return std::make_shared<const MKLWEPrivateKeyImpl>(k, n, m_kp.ks.qKS, std::move(s));
     }
-    void MKBTKeyGen(ConstMNTRUPrivateKey& sk) {
+    // policy (extension): the reference's r-defect handling (RDefectPolicy); the
+    // default keeps its keys bit for bit and counts the defective ones (GetRDefects).
+    void MKBTKeyGen(ConstMNTRUPrivateKey& sk, RDefectPolicy policy = RDefectPolicy::KEEP) {
         if (m_method == MKNTRU_LWE) throw config_error("MK-NTRU key for an MKNTRU_LWE context");
         std::vector<uint32_t> col0((size_t)sk->Getk() * sk->GetLength());
         const auto c = sk->GetF_col0();
         for (uint32_t u = 0; u < sk->Getk(); ++u)
             for (uint32_t l = 0; l < sk->GetLength(); ++l) col0[(size_t)u * sk->GetLength() + l] = (uint32_t)c[u][l];
-        UniEncBTKey ek = common_btkey(col0);
+        UniEncBTKey ek = common_btkey(col0, policy);
         ek.ksk.resize(mkkg_ksk_mntru_words(&m_kp));
-        check(mkkg_ksk_mntru(&m_kp, next_seed(), ek.fvec.data(), sk->Finv().data(), ek.ksk.data()));
+        checkk(mkkg_ksk_mntru(&m_kp, next_seed(), ek.fvec.data(), sk->Finv().data(), ek.ksk.data()));
         up_ksk_mntru(ek.ksk.data());
         m_BTKey = std::move(ek);
         m_keys = true;
     }
-    void MKBTKeyGen(ConstMKLWEPrivateKey& sk) {
+    void MKBTKeyGen(ConstMKLWEPrivateKey& sk, RDefectPolicy policy = RDefectPolicy::KEEP) {
         if (m_method != MKNTRU_LWE) throw config_error("MK-LWE key for an MK-NTRU context");
-        UniEncBTKey ek = common_btkey(sk->flat());
+        UniEncBTKey ek = common_btkey(sk->flat(), policy);
         ek.ksk_a.resize(mkkg_ksk_mklwe_a_words(&m_kp));
         ek.ksk_b.resize(mkkg_ksk_mklwe_b_words(&m_kp));
-        check(mkkg_ksk_mklwe(&m_kp, next_seed(), ek.fvec.data(), sk->flat().data(), ek.ksk_a.data(),
+        checkk(mkkg_ksk_mklwe(&m_kp, next_seed(), ek.fvec.data(), sk->flat().data(), ek.ksk_a.data(),
                              ek.ksk_b.data()));
         up_ksk_mklwe(ek.ksk_a.data(), ek.ksk_b.data());
         m_BTKey = std::move(ek);
         m_keys = true;
     }
+    // Extension: bootstrapping keys of the last MKBTKeyGen that drew DggR r != 0
+    // (under RESAMPLE: the slots that were redrawn).  Nonzero means gates using
+    // them may decrypt wrong (the reference's KeyGenXZW defect).
+    uint64_t GetRDefects() const { return m_rdefects; }
     // ctGateGen (binfhe-base-scheme.cpp:340-376)
     void ctGateGen(ConstMNTRUPrivateKey& sk, BINGATE gate) {
         if (gate != NAND) throw config_error("Support NAND gate Only");
         need_keyparams();
         std::vector<uint32_t> c((size_t)sk->Getk() * sk->GetLength());
-        check(mkkg_mntru_ctgate(&m_kp, next_seed(), sk->Finv().data(), c.data()));
+        checkk(mkkg_mntru_ctgate(&m_kp, next_seed(), sk->Finv().data(), c.data()));
         m_ctNAND = unpack_mntru(c.data(), sk->Getk(), sk->GetLength(), m_kp.acc.q);
     }
     const UniEncBTKey& GetBTKey() const { return m_BTKey; }
@@ -715,14 +749,14 @@ public:
         };
         add("crs", k.crs); add("skN", k.fvec); add("skN_eval", k.f_eval); add("skNinv_eval", k.finv_eval);
         add("pkey", k.pkey); add("evk", k.evk); add("ksk", k.ksk); add("ksk_a", k.ksk_a); add("ksk_b", k.ksk_b);
-        check(mkkg_file_write(path.c_str(), MKKG_FILE_BTKEY, &m_kp, s.data(), (uint32_t)s.size()));
+        checkk(mkkg_file_write(path.c_str(), MKKG_FILE_BTKEY, &m_kp, s.data(), (uint32_t)s.size()));
     }
     // Load a bootstrapping key written by SaveBTKey (or mkfhe_amd.keys.save_btkey) and upload it.
     void LoadBTKey(const std::string& path) {
         need_keyparams();
         uint32_t kind = 0;
         mkkg_params fp{};
-        check(mkkg_file_info(path.c_str(), &kind, &fp, nullptr));
+        checkk(mkkg_file_info(path.c_str(), &kind, &fp, nullptr));
         if (kind != MKKG_FILE_BTKEY) throw config_error(path + " is not a bootstrapping-key file");
         if (fp.acc.method != m_kp.acc.method || fp.acc.k != m_kp.acc.k || fp.acc.n != m_kp.acc.n ||
             fp.acc.Q != m_kp.acc.Q || fp.acc.baseG != m_kp.acc.baseG || fp.ks.qKS != m_kp.ks.qKS)
@@ -730,7 +764,7 @@ public:
         UniEncBTKey ek;
         auto get = [&](const char* nm, std::vector<uint32_t>& v) {
             v.resize(mkkg_file_section_words(path.c_str(), nm));
-            if (!v.empty()) check(mkkg_file_read_section(path.c_str(), nm, v.data(), v.size()));
+            if (!v.empty()) checkk(mkkg_file_read_section(path.c_str(), nm, v.data(), v.size()));
         };
         get("crs", ek.crs); get("skN", ek.fvec); get("skN_eval", ek.f_eval); get("skNinv_eval", ek.finv_eval);
         get("pkey", ek.pkey); get("evk", ek.evk); get("ksk", ek.ksk); get("ksk_a", ek.ksk_a); get("ksk_b", ek.ksk_b);
@@ -753,14 +787,14 @@ public:
         std::strncpy(s[1].name, "Finv", 15);
         s[1].words = sk->Finv().size();
         s[1].data = sk->Finv().data();
-        check(mkkg_file_write(path.c_str(), MKKG_FILE_MNTRU_SK, &m_kp, s, 2));
+        checkk(mkkg_file_write(path.c_str(), MKKG_FILE_MNTRU_SK, &m_kp, s, 2));
     }
     MNTRUPrivateKey LoadMNTRUSecretKey(const std::string& path) const {
         need_keyparams();
         const uint32_t k = m_kp.acc.k, n = m_kp.acc.n;
         std::vector<uint32_t> F((size_t)k * n * n), Fi((size_t)k * n * n);
-        check(mkkg_file_read_section(path.c_str(), "F", F.data(), F.size()));
-        check(mkkg_file_read_section(path.c_str(), "Finv", Fi.data(), Fi.size()));
+        checkk(mkkg_file_read_section(path.c_str(), "F", F.data(), F.size()));
+        checkk(mkkg_file_read_section(path.c_str(), "Finv", Fi.data(), Fi.size()));
         return std::make_shared<const MNTRUPrivateKeyImpl>(k, n, m_kp.ks.qKS, std::move(F), std::move(Fi));
     }
 
@@ -773,7 +807,7 @@ public:
         if (mod) kp.acc.q = mod;
         const uint32_t mm = (uint32_t)m;
         std::vector<uint32_t> c((size_t)sk->Getk() * sk->GetLength());
-        check(mkkg_mntru_encrypt(&kp, next_seed(), sk->Finv().data(), &mm, p, 1, c.data()));
+        checkk(mkkg_mntru_encrypt(&kp, next_seed(), sk->Finv().data(), &mm, p, 1, c.data()));
         auto ct = unpack_mntru(c.data(), sk->Getk(), sk->GetLength(), kp.acc.q);
         ct->SetptModulus(p);
         return ct;
@@ -787,7 +821,7 @@ public:
         const uint32_t mm = (uint32_t)m, k = sk->Getk(), n = sk->GetLength();
         std::vector<uint32_t> a((size_t)k * n);
         uint32_t b = 0;
-        check(mkkg_mklwe_encrypt(&kp, next_seed(), sk->flat().data(), &mm, p, 1, a.data(), &b));
+        checkk(mkkg_mklwe_encrypt(&kp, next_seed(), sk->flat().data(), &mm, p, 1, a.data(), &b));
         std::vector<NativeVector> av(k, NativeVector(n));
         for (uint32_t u = 0; u < k; ++u)
             for (uint32_t i = 0; i < n; ++i) av[u][i] = a[(size_t)u * n + i];
@@ -986,7 +1020,7 @@ private:
     }
     uint64_t next_seed() const { return m_seed ? m_seed + (m_calls++) * 0x9E3779B97F4A7C15ull : 0; }
     // CRS, ring secrets, P and the accumulator key (binfhe-base-scheme.cpp:198-338), uploaded
-    UniEncBTKey common_btkey(const std::vector<uint32_t>& lwe_sk) {
+    UniEncBTKey common_btkey(const std::vector<uint32_t>& lwe_sk, RDefectPolicy policy) {
         need_keyparams();
         const uint32_t k = m_kp.acc.k, N = m_kp.acc.N;
         const uint32_t dg = (m_kp.acc.digitsG ? m_kp.acc.digitsG : m_params->GetDigitsG()) - 1;
@@ -997,10 +1031,14 @@ private:
         ek.finv_eval.resize((size_t)k * N);
         ek.pkey.resize(mkkg_pkey_words(&m_kp));
         ek.evk.resize(mkkg_evk_words(&m_kp));
-        check(mkkg_crs(&m_kp, next_seed(), ek.crs.data()));
-        check(mkkg_ring_secrets(&m_kp, next_seed(), ek.fvec.data(), ek.f_eval.data(), ek.finv_eval.data()));
-        check(mkkg_pkey(&m_kp, next_seed(), ek.crs.data(), ek.f_eval.data(), ek.pkey.data()));
-        check(mkkg_acc_keygen(&m_kp, next_seed(), ek.crs.data(), ek.finv_eval.data(), lwe_sk.data(), ek.evk.data()));
+        checkk(mkkg_crs(&m_kp, next_seed(), ek.crs.data()));
+        checkk(mkkg_ring_secrets(&m_kp, next_seed(), ek.fvec.data(), ek.f_eval.data(), ek.finv_eval.data()));
+        checkk(mkkg_pkey(&m_kp, next_seed(), ek.crs.data(), ek.f_eval.data(), ek.pkey.data()));
+        uint64_t ndef = 0;
+        m_rdefects = 0;
+        checkk(mkkg_acc_keygen_ex(&m_kp, next_seed(), ek.crs.data(), ek.finv_eval.data(), lwe_sk.data(),
+                                  ek.evk.data(), static_cast<uint32_t>(policy), &ndef));
+        m_rdefects = ndef;
         up_keys(ek.evk.data(), ek.pkey.data());
         return ek;
     }
@@ -1018,7 +1056,7 @@ private:
         std::vector<uint32_t> c((size_t)k * n);
         pack(*ct, c.data(), k, n);
         uint32_t m = 0;
-        check(mkkg_mntru_decrypt(&m_kp, sk->F().data(), c.data(), ct->GetModulus(), p, variant, 1, &m));
+        checkk(mkkg_mntru_decrypt(&m_kp, sk->F().data(), c.data(), ct->GetModulus(), p, variant, 1, &m));
         *result = m;
     }
     void decrypt_mklwe(ConstMKLWEPrivateKey& sk, ConstMKLWECiphertext& ct, MKLWEPlaintext* result, uint32_t p,
@@ -1030,7 +1068,7 @@ private:
         packA(*ct, a.data(), k, n);
         const uint32_t b = (uint32_t)ct->GetB();
         uint32_t m = 0;
-        check(mkkg_mklwe_decrypt(&m_kp, sk->flat().data(), a.data(), &b, ct->GetModulus(), p, variant, 1, &m));
+        checkk(mkkg_mklwe_decrypt(&m_kp, sk->flat().data(), a.data(), &b, ct->GetModulus(), p, variant, 1, &m));
         *result = m;
     }
     void need_gate(BINGATE gate, BINFHE_METHOD family) const {
@@ -1068,6 +1106,7 @@ private:
     mkkg_params m_kp{};
     bool m_have_kp = false;
     uint64_t m_seed = 0;
+    uint64_t m_rdefects = 0;
     mutable uint64_t m_calls = 1;
     UniEncBTKey m_BTKey;
 };

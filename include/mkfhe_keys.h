@@ -123,6 +123,23 @@ int mkkg_pkey(const mkkg_params* p, uint64_t seed, const uint32_t* crs, const ui
  * F_col0 for MK-NTRU, s for MK-LWE) under 1/s_u. */
 int mkkg_acc_keygen(const mkkg_params* p, uint64_t seed, const uint32_t* crs, const uint32_t* skNinv_eval,
                     const uint32_t* lwe_sk, uint32_t* evk);
+/* Same with a policy for the reference's r-defect: KeyGenXZW / KDMKeyGenXZW
+ * (mk-acc-xzw.cpp:141-167, mk-acc-xzw_B.cpp:135-220) put the DggR sample r into
+ * f as the polynomial g_t*r but into d only as the scalar r^[t]*CRS_t, so the
+ * r-terms cancel in HbProd only when r = 0; a key with r != 0 (about 9e-7 per
+ * key, 2.8e-3 per STD128_MKNTRU key set) can break every gate that uses it.
+ *   MKKG_RDEFECT_KEEP     the reference's keys bit for bit (mkkg_acc_keygen);
+ *   MKKG_RDEFECT_REJECT   same keys, but MKKG_E_RDEFECT if any key has r != 0;
+ *   MKKG_RDEFECT_RESAMPLE redraw r from the slot's stream until it is zero
+ *                         (deviates from the reference only in affected slots).
+ * *defective (may be NULL) = the number of keys that drew r != 0 (under RESAMPLE:
+ * the number of slots that were redrawn). */
+#define MKKG_RDEFECT_KEEP     0u
+#define MKKG_RDEFECT_REJECT   1u
+#define MKKG_RDEFECT_RESAMPLE 2u
+#define MKKG_E_RDEFECT      -20  /* REJECT: a bootstrapping key drew r != 0 (keys are still written) */
+int mkkg_acc_keygen_ex(const mkkg_params* p, uint64_t seed, const uint32_t* crs, const uint32_t* skNinv_eval,
+                       const uint32_t* lwe_sk, uint32_t* evk, uint32_t rdefect_policy, uint64_t* defective);
 /* KeySwitchGen2 (MK-NTRU): ksk [k][N*dks][n] = KSK2[u][1]. */
 int mkkg_ksk_mntru(const mkkg_params* p, uint64_t seed, const uint32_t* skN, const uint32_t* Finv, uint32_t* ksk);
 /* KeySwitchGen (MK-LWE): A [k][N][baseKS][dks][n], B [k][N][baseKS][dks]. */

@@ -87,13 +87,24 @@ class BinFHEContext:
             raise ConfigError("Support BINARY PrivateKey Only")
         return K.mklwe_keygen(self.kp, self._next())
 
-    def MKBTKeyGen(self, sk):
-        """MKKeyGen (binfhe-base-scheme.cpp:198-338) + upload to the engine."""
+    def MKBTKeyGen(self, sk, rdefect: str = "keep"):
+        """MKKeyGen (binfhe-base-scheme.cpp:198-338) + upload to the engine.
+
+        rdefect (extension): "keep" (the reference's keys; GetRDefects() counts keys
+        whose DggR sample r is nonzero), "reject" (keys.KeyDefectError) or
+        "resample" -- the reference's KeyGenXZW defect, include/mkfhe_keys.h."""
         is_lwe = isinstance(sk, K.MKLWEPrivateKey)
         if is_lwe != (self.method == MKNTRU_LWE):
             raise ConfigError("secret key type does not match the context method")
         seed = self._next()
-        self._upload(K.bt_keygen(self.kp, sk, seed=seed, crs_seed=(seed ^ 0xC25) if seed else None))
+        self.rdefects = 0
+        bk = K.bt_keygen(self.kp, sk, seed=seed, crs_seed=(seed ^ 0xC25) if seed else None, rdefect=rdefect)
+        self.rdefects = bk.rdefects
+        self._upload(bk)
+
+    def GetRDefects(self) -> int:
+        """Bootstrapping keys of the last MKBTKeyGen that drew DggR r != 0 (gates may decrypt wrong)."""
+        return getattr(self, "rdefects", 0)
 
     def _upload(self, bk: K.UniEncBTKey):
         eng = self.engine()

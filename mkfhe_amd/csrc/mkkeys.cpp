@@ -462,12 +462,26 @@ void sample_poly_eval(const Ring& R, const Dgg& g, Rng& r, uint32_t* out) {
 //   f_t  = (NTT(e1) + g_t * r) * s^-1
 //   d_t  = NTT(e0) + [m] g_t (KeyGen) or [m] g_t * s^-1 (KDM) + r[t] * CRS_t
 // r[t] is the EVAL slot t of r (skrPoly[i] in the reference), a scalar.
-void unienc_key(const P& p, const Ring& R, const Dgg& dgg, const Dgg& dggR, Rng& rng, const uint32_t* crs,
-                const uint32_t* sinv, bool m, bool kdm, uint32_t* out) {
+//
+// The r-defect: the r-terms cancel in HbProd only when r = 0, so a key whose r
+// has a nonzero coefficient breaks the gates that use it.  The
+// default policy keeps the reference's keys bit for bit and only counts such
+// keys; MKKG_RDEFECT_RESAMPLE draws r again from the slot's own stream until it
+// is zero (r conditioned on 0).  Returns whether the slot's first r was nonzero.
+bool unienc_key(const P& p, const Ring& R, const Dgg& dgg, const Dgg& dggR, Rng& rng, const uint32_t* crs,
+                const uint32_t* sinv, bool m, bool kdm, uint32_t* out, uint32_t policy) {
     const uint32_t N = p.N;
     const uint32_t Q = (uint32_t)p.Q;
     std::vector<uint32_t> r(N), e0(N), e1(N);
-    sample_poly_eval(R, dggR, rng, r.data());
+    bool drew_defect = false;   // the slot's first r had a nonzero coefficient
+    for (int attempt = 0;; ++attempt) {
+        for (uint32_t j = 0; j < N; ++j) r[j] = to_mod(dggR.sample(rng), R.Q);
+        const bool defect = std::any_of(r.begin(), r.end(), [](uint32_t x) { return x != 0; });
+        if (attempt == 0) drew_defect = defect;
+        if (!defect || policy != MKKG_RDEFECT_RESAMPLE) break;
+        if (attempt == 64) throw std::runtime_error("DggR kept drawing nonzero samples");
+    }
+    R.fwd(r.data());
     for (uint32_t t = 0; t < p.dg; ++t) {
         sample_poly_eval(R, dgg, rng, e0.data());
         sample_poly_eval(R, dgg, rng, e1.data());
@@ -484,6 +498,7 @@ void unienc_key(const P& p, const Ring& R, const Dgg& dgg, const Dgg& dggR, Rng&
             d[j] = (uint32_t)(dv % Q);
         }
     }
+    return drew_defect;
 }
 
 }  // namespace
@@ -738,9 +753,16 @@ int mkkg_pkey(const mkkg_params* pp, uint64_t seed, const uint32_t* crs, const u
 //          is KDM, plus ek[0][0][n] = KDM-Enc(1).  Unset slots are zero.
 //   XZW_B: ek[u][0][i] = Enc(s == 1); slot (0,0) KDM, ek[0][0][n] = KDM-Enc(1).
 int mkkg_acc_keygen(const mkkg_params* pp, uint64_t seed, const uint32_t* crs, const uint32_t* skNinv_eval,
-                    const uint32_t* lwe_sk, uint32_t* evk) try {
+                    const uint32_t* lwe_sk, uint32_t* evk) {
+    return mkkg_acc_keygen_ex(pp, seed, crs, skNinv_eval, lwe_sk, evk, MKKG_RDEFECT_KEEP, nullptr);
+}
+
+int mkkg_acc_keygen_ex(const mkkg_params* pp, uint64_t seed, const uint32_t* crs, const uint32_t* skNinv_eval,
+                       const uint32_t* lwe_sk, uint32_t* evk, uint32_t rdefect_policy, uint64_t* defective) try {
     UNPACK(pp, p);
     if (!crs || !skNinv_eval || !lwe_sk || !evk) return fail(MKACC_E_ARG, "null argument");
+    if (rdefect_policy > MKKG_RDEFECT_RESAMPLE) return fail(MKACC_E_ARG, "unknown r-defect policy");
+    std::atomic<uint64_t> ndef{0};
     const Seed sd = resolve_seed(seed);
     const Ring R(p.N, p.Q, p.root);
     const Dgg dgg(pp->sigma_unienc), dggR(pp->sigma_r);
@@ -769,8 +791,13 @@ int mkkg_acc_keygen(const mkkg_params* pp, uint64_t seed, const uint32_t* crs, c
             return;
         }
         Rng r(sd, 6, idx);
-        unienc_key(p, R, dgg, dggR, r, crs, sinv, m, kdm, out);
+        if (unienc_key(p, R, dgg, dggR, r, crs, sinv, m, kdm, out, rdefect_policy)) ndef.fetch_add(1);
     });
+    if (defective) *defective = ndef.load();
+    if (ndef.load() && rdefect_policy == MKKG_RDEFECT_REJECT)
+        return fail(MKKG_E_RDEFECT, std::to_string(ndef.load()) +
+                                        " bootstrapping key(s) drew a nonzero DggR sample r (the reference's "
+                                        "KeyGenXZW defect, mk-acc-xzw.cpp:160-167): gates using them may decrypt wrong");
     return MKACC_OK;
 } catch (const std::exception& e) {
     return fail(MKACC_E_ARG, std::string("mkkg_acc_keygen: ") + e.what());

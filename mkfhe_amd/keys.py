@@ -57,6 +57,7 @@ SIGNATURES = {
     "mkkg_ring_secrets": (_int, [_pp, _u64, _u32p, _u32p, _u32p]),
     "mkkg_pkey": (_int, [_pp, _u64, _u32p, _u32p, _u32p]),
     "mkkg_acc_keygen": (_int, [_pp, _u64, _u32p, _u32p, _u32p, _u32p]),
+    "mkkg_acc_keygen_ex": (_int, [_pp, _u64, _u32p, _u32p, _u32p, _u32p, _u32, ctypes.POINTER(_u64)]),
     "mkkg_ksk_mntru": (_int, [_pp, _u64, _u32p, _u32p, _u32p]),
     "mkkg_ksk_mklwe": (_int, [_pp, _u64, _u32p, _u32p, _u32p, _u32p]),
     "mkkg_mntru_encrypt": (_int, [_pp, _u64, _u32p, _u32p, _u32, _sz, _u32p]),
@@ -133,7 +134,19 @@ def entropy_set(master_hex: str | None, calls: int = 0):
     _check(load().mkkg_entropy_set(_p(m), calls))
 
 
+# r-defect policies of mkkg_acc_keygen_ex (include/mkfhe_keys.h)
+RDEFECT = {"keep": 0, "reject": 1, "resample": 2}
+E_RDEFECT = -20
+
+
+class KeyDefectError(MkaccError):
+    """MKBTKeyGen with rdefect="reject" drew a bootstrapping key with DggR sample r != 0
+    (the reference's KeyGenXZW defect, mk-acc-xzw.cpp:160-167)."""
+
+
 def _check(rc: int):
+    if rc == E_RDEFECT:
+        raise KeyDefectError(rc, load().mkkg_last_error().decode())
     if rc != 0:
         raise MkaccError(rc, load().mkkg_last_error().decode())
 
@@ -211,6 +224,7 @@ class UniEncBTKey:
     ksk: np.ndarray | None = None      # MK-NTRU KSK2[u][1]: [k][N*dks][n]
     ksk_A: np.ndarray | None = None    # MK-LWE: [k][N][baseKS][dks][n]
     ksk_B: np.ndarray | None = None    # MK-LWE: [k][N][baseKS][dks]
+    rdefects: int = 0                  # keys that drew DggR r != 0 (mkkg_acc_keygen_ex)
 
 
 def crs(p: MkkgParams, seed: int) -> np.ndarray:
@@ -227,8 +241,14 @@ def ring_secrets(p: MkkgParams, seed: int):
     return c, e, ei
 
 
-def bt_keygen(p: MkkgParams, sk, seed: int = 0, crs_seed: int | None = None) -> UniEncBTKey:
-    """MKKeyGen for an MNTRU (binfhe-base-scheme.cpp:198-277) or MKLWE (:279-338) secret key."""
+def bt_keygen(p: MkkgParams, sk, seed: int = 0, crs_seed: int | None = None, rdefect: str = "keep") -> UniEncBTKey:
+    """MKKeyGen for an MNTRU (binfhe-base-scheme.cpp:198-277) or MKLWE (:279-338) secret key.
+
+    rdefect: "keep" (default, the reference's keys bit for bit; the count of keys
+    that drew DggR r != 0 is in .rdefects), "reject" (KeyDefectError if any) or
+    "resample" (redraw r in the affected slots) -- include/mkfhe_keys.h."""
+    if rdefect not in RDEFECT:
+        raise ValueError(f"rdefect must be one of {sorted(RDEFECT)}")
     # seed 0: every call below draws its own 256-bit key (ChaCha20, mkkeys.cpp),
     # the CRS included; a nonzero seed gives reproducible (non-cryptographic) keys
     def sub(i):
@@ -241,8 +261,10 @@ def bt_keygen(p: MkkgParams, sk, seed: int = 0, crs_seed: int | None = None) -> 
     _check(L.mkkg_pkey(ctypes.byref(p), sub(2), _p(c), _p(skN_eval), _p(pkey)))
     evk = np.empty((k, nk, n + 1, dg, 2, N), np.uint32)
     lwe_sk = _in(sk.F_col0 if isinstance(sk, MNTRUPrivateKey) else sk.s)
-    _check(L.mkkg_acc_keygen(ctypes.byref(p), sub(3), _p(c), _p(skNinv), _p(lwe_sk), _p(evk)))
-    key = UniEncBTKey(c, skN, skN_eval, skNinv, pkey, evk)
+    ndef = _u64()
+    _check(L.mkkg_acc_keygen_ex(ctypes.byref(p), sub(3), _p(c), _p(skNinv), _p(lwe_sk), _p(evk), RDEFECT[rdefect],
+                                ctypes.byref(ndef)))
+    key = UniEncBTKey(c, skN, skN_eval, skNinv, pkey, evk, rdefects=int(ndef.value))
     if isinstance(sk, MNTRUPrivateKey):
         key.ksk = np.empty((k, N * dks, n), np.uint32)
         _check(L.mkkg_ksk_mntru(ctypes.byref(p), sub(4), _p(skN), _p(_in(sk.Finv)), _p(key.ksk)))

@@ -61,10 +61,10 @@ def r_defects(oracle, p, bk):
     return out
 
 
-def example_run(K, oracle, p, orcs, lwe: bool, threads: int):
+def example_run(K, oracle, p, orcs, lwe: bool, threads: int, rdefect: str = "keep"):
     """The example's seed-0 calls in its order; returns the decrypted gates and the key set."""
     sk = K.mklwe_keygen(p, 0) if lwe else K.mntru_keygen(p, 0)
-    bk = K.bt_keygen(p, sk, seed=0)
+    bk = K.bt_keygen(p, sk, seed=0, rdefect=rdefect)
     ct_nand = None if lwe else K.mntru_ctgate(p, sk, 0)
     cts = []
     for m0, m1 in PAIRS:
