@@ -100,7 +100,7 @@ UNITS = [("engine", "mkacc_engine.hip", [])] + [
     (f"step_dg{d}", "mkacc_steps.hip", [f"-DMKACC_TU_DG={d}", "-DMKACC_TU_PART=0"]) for d in (2, 3, 4, 5)] + [
     (f"lat_dg{d}", "mkacc_steps.hip", [f"-DMKACC_TU_DG={d}", "-DMKACC_TU_PART=1"]) for d in (2, 3, 4)] + [
     (f"step2_dg{d}", "mkacc_steps.hip", [f"-DMKACC_TU_DG={d}", "-DMKACC_TU_PART=2"] + STEP2_SCHED.get(d, []))
-    for d in (2, 3)] + [
+    for d in (2, 3, 4)] + [
     ("wide", "mkacc_steps.hip", ["-DMKACC_TU_WIDE=1"]), ("widefp", "mkacc_steps.hip", ["-DMKACC_TU_WIDE=2"])]
 
 

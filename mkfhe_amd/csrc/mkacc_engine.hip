@@ -98,8 +98,9 @@ __global__ void wide_key_layout_kernel(const W* __restrict__ src, uint64_t* __re
 // mk_step_kernel; read once per context (mkacc_ctx::step_ver), which sizes its
 // workspace for that kernel.
 int step_version(int dg) {
-    if (dg > 3) return 1;
     const char* e = std::getenv("MKACC_STEP");
+    if (dg == 4) return e && e[0] == '2' ? 2 : 1;   // A/B: mk_step2_kernel at one wave per SIMD
+    if (dg > 4) return 1;
     if (e && e[0] == '1') return 1;
     return 2;
 }
@@ -109,6 +110,7 @@ const void* step_fn(int dg, int method, bool first, bool dscr, int ver) {
         switch (dg) {
             case 2: return mkacc_tu::step2_dg2(method, first);
             case 3: return mkacc_tu::step2_dg3(method, first);
+            case 4: return mkacc_tu::step2_dg4(method, first);
             default: return nullptr;
         }
     }

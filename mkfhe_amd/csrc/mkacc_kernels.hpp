@@ -899,6 +899,7 @@ MKACC_TU_API KernelPtr step_dg4(int method, bool first, bool dscr);
 MKACC_TU_API KernelPtr step_dg5(int method, bool first, bool dscr);
 MKACC_TU_API KernelPtr step2_dg2(int method, bool first);   // mk_step2_kernel (mkacc_step2.hpp)
 MKACC_TU_API KernelPtr step2_dg3(int method, bool first);
+MKACC_TU_API KernelPtr step2_dg4(int method, bool first);
 MKACC_TU_API KernelPtr lat_dg2(int method, bool first);
 MKACC_TU_API KernelPtr lat_dg3(int method, bool first);
 MKACC_TU_API KernelPtr lat_dg4(int method, bool first);

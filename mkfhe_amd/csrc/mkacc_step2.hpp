@@ -85,13 +85,14 @@ struct Step2Cfg {
 #ifndef MKACC_S2_GS
 #define MKACC_S2_GS 0
 #endif
-    static constexpr int kGS = MKACC_S2_GS ? MKACC_S2_GS : (DG <= 3 ? 4 : 2);
-    // load groups in flight ahead of the one being summed: 1 at dg <= 3 (at dg = 4,
-    // not built, the 4 x 32 G registers leave room for none without spills)
+    static constexpr int kGS = MKACC_S2_GS ? MKACC_S2_GS : 4;
+    // load groups in flight ahead of the one being summed: 1 at dg <= 3; at dg >= 4
+    // the 4 x 32 G registers need the whole 512-entry file (one wave per SIMD,
+    // kWavesPerSimd), which leaves room for two
 #ifndef MKACC_S2_PF
 #define MKACC_S2_PF -1
 #endif
-    static constexpr int kPf = MKACC_S2_PF >= 0 ? MKACC_S2_PF : (DG <= 3 ? 1 : 0);
+    static constexpr int kPf = MKACC_S2_PF >= 0 ? MKACC_S2_PF : (DG <= 3 ? 1 : 2);
     // X^(N-c) - 1 gathered with the group's key loads (1) or at use (0)
 #ifndef MKACC_S2_MONO
 #define MKACC_S2_MONO 0
@@ -240,8 +241,18 @@ __device__ __forceinline__ void digit_ntts(const StepCtx& s, uint32_t (&x)[kRegs
     }
 }
 
+// waves per SIMD the register budget is sized for: 2 (256 VGPRs) at dg <= 3;
+// 1 at dg >= 4 (512: the dg x 32 digit-NTT registers, the sumV and the key prefetch)
+template <int DG>
+constexpr int s2_waves_per_simd() {
+#ifdef MKACC_S2_WPS
+    return MKACC_S2_WPS;
+#else
+    return DG <= 3 ? 2 : 1;
+#endif
+}
 template <int DG, int METHOD, bool FIRST>
-__global__ __launch_bounds__(64 * kS2Waves, 8 / kS2Waves) void mk_step2_kernel(StepArgs a) {
+__global__ __launch_bounds__(64 * kS2Waves, 4 * s2_waves_per_simd<DG>() / kS2Waves) void mk_step2_kernel(StepArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     load_image(smem, a.img);
     const uint32_t l = threadIdx.x & 63u;
