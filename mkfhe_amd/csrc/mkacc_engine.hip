@@ -54,6 +54,7 @@ int fail(int code, const std::string& msg) {
 #include "mkacc_gate.hpp"
 #include "mkacc_wide.hpp"
 #include "mkacc_widefp.hpp"
+#include "mkacc_widereg.hpp"
 
 namespace {
 
@@ -63,7 +64,7 @@ namespace {
 template <typename W>
 __global__ void wide_key_layout_kernel(const W* __restrict__ src, uint64_t* __restrict__ dst, size_t npolys,
                                        uint32_t nk, uint32_t n1, uint32_t dg2, uint64_t Q, uint64_t r, uint64_t rp,
-                                       bool fp, uint32_t* __restrict__ bad) {
+                                       bool fp, bool c8, uint32_t* __restrict__ bad) {
     const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= npolys * kN) return;
     size_t p = idx / kN;
@@ -75,11 +76,12 @@ __global__ void wide_key_layout_kernel(const W* __restrict__ src, uint64_t* __re
     const size_t dpoly = ((u * n1 + i) * nk + jj) * dg2 + dp;
     const uint64_t x = (uint64_t)src[idx];
     if (x >= Q) *bad = 1u;
+    const uint32_t jd = c8 ? widereg::c8_index(j) : j;   // register-resident FP64 kernel: C8 layout
     if (fp) {
         const double d = (double)(x < Q ? x : 0) - (x > (Q >> 1) && x < Q ? (double)Q : 0.0);
-        dst[dpoly * kN + j] = (uint64_t)__double_as_longlong(d);
+        dst[dpoly * kN + jd] = (uint64_t)__double_as_longlong(d);
     } else {
-        dst[dpoly * kN + j] = wide::mul_shoup(x, r, rp, Q);
+        dst[dpoly * kN + jd] = wide::mul_shoup(x, r, rp, Q);
     }
 }
 
@@ -247,6 +249,9 @@ struct mkacc_ctx {
     bool wfp = false;
     widefp::FMod wfm{};
     double wfninv = 0, wfC = 0;
+    bool wfreg = false;            // FP64 register-resident kernel (mkacc_widereg.hpp), C8 layouts
+    double* d_rimg = nullptr;      // its LDS image (widereg::kImgD doubles)
+    double* d_rtis = nullptr;      // its inverse pass-1 table [32]
     double* d_ftwf = nullptr;      // forward / inverse twiddles and psi^e, balanced
     double* d_ftwi = nullptr;
     double* d_fpsi = nullptr;
@@ -601,9 +606,9 @@ int upload_keys_device_impl(mkacc_ctx* c, const W* d_evk, const W* d_pkey) {
         if (!c->d_wkeys) HIP_TRY(hipMalloc(&c->d_wkeys, ep * kN * 8));
         if (!c->d_wpkey) HIP_TRY(hipMalloc(&c->d_wpkey, pp * kN * 8));
         hipLaunchKernelGGL(wide_key_layout_kernel<W>, grid(ep), dim3(tpb), 0, c->stream, d_evk, c->d_wkeys, ep, nk,
-                           n1, dg * 2, Q, R, Rp, c->wfp, kbad);
+                           n1, dg * 2, Q, R, Rp, c->wfp, c->wfreg, kbad);
         hipLaunchKernelGGL(wide_key_layout_kernel<W>, grid(pp), dim3(tpb), 0, c->stream, d_pkey, c->d_wpkey, pp, 1u,
-                           1u, dg, Q, R, Rp, c->wfp, kbad);
+                           1u, dg, Q, R, Rp, c->wfp, c->wfreg, kbad);
     } else {
         if (!c->d_keys) HIP_TRY(hipMalloc(&c->d_keys, ep * kN * 4));
         if (!c->d_pkey) HIP_TRY(hipMalloc(&c->d_pkey, pp * kN * 4));
@@ -711,6 +716,48 @@ int wide_setup(mkacc_ctx* c) {
         HIP_TRY(hipMemcpy(c->d_ftwf, ftf.data(), kN * sizeof(double), hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(c->d_ftwi, fti.data(), kN * sizeof(double), hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(c->d_fpsi, fpw.data(), 2 * kN * sizeof(double), hipMemcpyHostToDevice));
+        // register-resident kernel (mkacc_widereg.hpp, default; MKACC_WFP_REG=0 keeps
+        // widefp::step_kernel): per-lane twiddle image in the 27-bit kernels' twl layout
+        const char* re = std::getenv("MKACC_WFP_REG");
+        c->wfreg = !(re && re[0] == '0');
+        if (c->wfreg) {
+            std::vector<double> img(widereg::kImgD), tis(32, 0.0);
+            double* F = img.data() + widereg::kImgFwd;
+            for (int st = 5; st <= 9; ++st) {
+                const int NP = 1 << (st - 5);
+                for (int lhi = 0; lhi < 32; ++lhi)
+                    for (int m = 0; m < NP; ++m) F[twl_off(st) + 32 * m + lhi] = ftf[(1 << st) + lhi * NP + m];
+            }
+            for (int ln = 0; ln < 64; ++ln)
+                for (int m = 0; m < 16; ++m) F[kTwlC + 64 * m + ln] = ftf[1024 + 16 * ln + m];
+            // psi^-e for e in [0, 2N): ti holds psi^-i at brv(i), pwi in natural order
+            std::vector<uint64_t> pwi(2 * kN);
+            {
+                uint64_t ei = 1;
+                for (uint32_t i = 0; i < 2u * kN; ++i) {
+                    pwi[i] = ei;
+                    ei = mulmod(ei, psii, Q);
+                }
+            }
+            double* I = img.data() + widereg::kImgInv;
+            for (int b = 5; b <= 9; ++b)
+                for (int m = 0; m < (1 << (b - 5)); ++m)
+                    for (int l31 = 0; l31 < 32; ++l31) I[twl_off(b) + 32 * m + l31] = bal(pwi[(size_t)(l31 | (m << 5)) << (11 - b)]);
+            for (int m = 0; m < 16; ++m)
+                for (int ln = 0; ln < 64; ++ln) I[kTwlC + 64 * m + ln] = bal(pwi[(size_t)((m << 6) | ln) << 1]);
+            // the twist psi^-i with the reference's N^-1 folded in
+            double* T = img.data() + widereg::kImgTwist;
+            for (int r = 0; r < 32; ++r)
+                for (int ln = 0; ln < 64; ++ln) T[64 * r + ln] = bal(mulmod(pwi[(r << 6) | ln], c->wninv, Q));
+            double* P = img.data() + widereg::kImgPsi;
+            for (uint32_t e = 0; e < 2u * kN; ++e) P[e] = fpw[e];
+            for (int b = 0; b < 5; ++b)
+                for (int t = 0; t < (1 << b); ++t) tis[(1 << b) + t] = bal(pwi[(size_t)t << (11 - b)]);
+            HIP_TRY(hipMalloc(&c->d_rimg, img.size() * sizeof(double)));
+            HIP_TRY(hipMalloc(&c->d_rtis, tis.size() * sizeof(double)));
+            HIP_TRY(hipMemcpy(c->d_rimg, img.data(), img.size() * sizeof(double), hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(c->d_rtis, tis.data(), tis.size() * sizeof(double), hipMemcpyHostToDevice));
+        }
     }
     return MKACC_OK;
 }
@@ -734,6 +781,10 @@ int wide_upload_keys(mkacc_ctx* c, const W* evk, const W* pkey) {
     };
     const uint32_t k = c->p.k, n = c->p.n, nk = c->nk, dg = c->dg;
     const size_t blk = (size_t)dg * 2 * kN;
+    // the register-resident FP64 kernel reads every polynomial in the C8 layout
+    auto pos = [c8 = c->wfreg](size_t s) {
+        return c8 ? (s & ~(size_t)(kN - 1)) | widereg::c8_index((uint32_t)(s & (kN - 1))) : s;
+    };
     std::vector<uint64_t> host((size_t)k * (n + 1) * nk * blk);
     for (uint32_t u = 0; u < k; ++u)
         for (uint32_t j = 0; j < nk; ++j)
@@ -742,14 +793,14 @@ int wide_upload_keys(mkacc_ctx* c, const W* evk, const W* pkey) {
                 uint64_t* dst = host.data() + (((size_t)u * (n + 1) + i) * nk + j) * blk;
                 for (size_t s = 0; s < blk; ++s) {
                     if ((uint64_t)src[s] >= Q) return fail(MKACC_E_RANGE, "evk word not a canonical residue mod Q");
-                    dst[s] = mont((uint64_t)src[s]);
+                    dst[pos(s)] = mont((uint64_t)src[s]);
                 }
             }
     const size_t pw = (size_t)k * dg * kN;
     std::vector<uint64_t> hp(pw);
     for (size_t s = 0; s < pw; ++s) {
         if ((uint64_t)pkey[s] >= Q) return fail(MKACC_E_RANGE, "pkey word not a canonical residue mod Q");
-        hp[s] = mont((uint64_t)pkey[s]);
+        hp[pos(s)] = mont((uint64_t)pkey[s]);
     }
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -791,6 +842,45 @@ int wide_launch_batch(mkacc_ctx* c, const uint32_t* d_ct, const uint64_t* d_in, 
     auto key = [&](uint32_t u, uint32_t i, uint32_t j) {
         return c->d_wkeys + (((size_t)u * (n + 1) + i) * c->nk + j) * blk;
     };
+    if (c->wfreg) {   // register-resident FP64 kernel: balanced doubles in the C8 layout
+        const size_t words = B * (size_t)k * kN;
+        const dim3 g((unsigned)((words + 255) / 256));
+        double* cur = reinterpret_cast<double*>(c->d_wacc0);
+        double* nxt = reinterpret_cast<double*>(c->d_wacc1);
+        hipLaunchKernelGGL(widereg::to_c8_kernel, g, dim3(256), 0, c->stream, d_in, cur, words, c->wfm, c->p.Q,
+                           c->d_bad);
+        auto dk = [](const uint64_t* p) { return reinterpret_cast<const double*>(p); };
+        // one workgroup of four gates per CU, looping over the batch
+        const size_t wgs = std::min<size_t>((B + widereg::kWaves - 1) / widereg::kWaves, (size_t)c->cus);
+        for (uint32_t u = 0; u < k; ++u)
+            for (uint32_t i = 0; i < n; ++i) {
+                const bool first = (u == 0 && i == 0);
+                widereg::StepArgs a;
+                a.acc_in = cur;
+                a.acc_out = nxt;
+                a.cvals = c->d_wcvals + ((size_t)u * n + i) * B;
+                a.key1 = dk(key(u, i, 0));
+                a.key2 = dk(c->nk == 2 ? key(u, i, 1) : key(u, i, 0));
+                a.keys = dk(key(0, n, 0));
+                a.pkey = dk(c->d_wpkey);
+                a.img = c->d_rimg;
+                a.twf = c->d_ftwf;
+                a.tis = c->d_rtis;
+                a.B = (uint32_t)B;
+                a.k = k;
+                a.index = u;
+                a.dg = c->dg;
+                a.C = c->wfC;
+                a.m = c->wfm;
+                a.sd = c->wsd;
+                launch_ptr(mkacc_tu::widereg_step(c->method_class, first), dim3((unsigned)wgs),
+                           dim3(64 * widereg::kWaves), widereg::kLdsBytes, c->stream, a);
+                std::swap(cur, nxt);
+            }
+        hipLaunchKernelGGL(widereg::from_c8_kernel, g, dim3(256), 0, c->stream, cur, d_out, words, c->wfm);
+        HIP_TRY(hipGetLastError());
+        return MKACC_OK;
+    }
     if (c->wfp) {   // FP64 variant: balanced doubles between the prologue and the epilogue
         const size_t words = B * (size_t)k * kN;
         const dim3 g((unsigned)((words + 255) / 256));
@@ -899,7 +989,14 @@ int wide_prim(mkacc_ctx* c, const uint64_t* in, uint64_t* out, size_t count, int
     HIP_TRY(hipMalloc(&din, count * kN * 8));
     HIP_TRY(hipMalloc(&dout, count * kN * 8 * out_mul));
     HIP_TRY(hipMemcpyAsync(din, in, count * kN * 8, hipMemcpyHostToDevice, c->stream));
-    if (which == 0 && c->wfp)
+    const unsigned rgrid = (unsigned)((count + widereg::kWaves - 1) / widereg::kWaves);
+    if (which == 0 && c->wfreg)
+        hipLaunchKernelGGL(widereg::ntt_fwd_kernel, dim3(rgrid), dim3(64 * widereg::kWaves), widereg::kLdsBytes,
+                           c->stream, din, dout, (uint32_t)count, c->d_rimg, c->d_ftwf, c->wfm);
+    else if (which == 1 && c->wfreg)
+        hipLaunchKernelGGL(widereg::ntt_inv_kernel, dim3(rgrid), dim3(64 * widereg::kWaves), widereg::kLdsBytes,
+                           c->stream, din, dout, (uint32_t)count, c->d_rimg, c->d_rtis, c->wfm);
+    else if (which == 0 && c->wfp)
         hipLaunchKernelGGL(widefp::ntt_fwd_kernel, dim3((unsigned)count), dim3(widefp::kThreads), 0, c->stream, din,
                            dout, c->d_ftwf, c->wfm);
     else if (which == 1 && c->wfp)
@@ -1161,7 +1258,7 @@ void mkacc_destroy(mkacc_ctx* c) {
                     (void*)c->d_acc0, (void*)c->d_acc1, (void*)c->d_cvals, (void*)c->d_dscr, (void*)c->d_ct,
                     (void*)c->d_io, (void*)c->d_ksk, (void*)c->d_lweA, (void*)c->d_lweB, (void*)c->d_tv,
                     (void*)c->d_digits, (void*)c->d_bh, (void*)c->d_gin, (void*)c->d_gout, (void*)c->d_wtwf,
-                    (void*)c->d_wtwi, (void*)c->d_wpsi, (void*)c->d_ftwf, (void*)c->d_ftwi, (void*)c->d_fpsi,
+                    (void*)c->d_wtwi, (void*)c->d_wpsi, (void*)c->d_ftwf, (void*)c->d_ftwi, (void*)c->d_fpsi, (void*)c->d_rimg, (void*)c->d_rtis,
                     (void*)c->d_wkeys, (void*)c->d_wpkey, (void*)c->d_wacc0,
                     (void*)c->d_wacc1, (void*)c->d_wcvals, (void*)c->d_wct, (void*)c->d_wio, (void*)c->d_bad})
         if (p) (void)hipFree(p);
@@ -1205,7 +1302,7 @@ int mkacc_upload_keys_device(mkacc_ctx* c, const void* d_evk, const void* d_pkey
 
 const char* mkacc_step_kernel_name(const mkacc_ctx* c, size_t B) {
     if (!c) return "";
-    if (c->wide) return c->wfp ? "widefp::step_kernel" : "wide::step_kernel";
+    if (c->wide) return c->wfreg ? "widereg::step_kernel" : (c->wfp ? "widefp::step_kernel" : "wide::step_kernel");
     if (use_lat(c, B)) return "mk_lat_kernel";
     return c->step_ver == 2 ? "mk_step2_kernel" : "mk_step_kernel";
 }

@@ -905,4 +905,5 @@ MKACC_TU_API KernelPtr lat_dg3(int method, bool first);
 MKACC_TU_API KernelPtr lat_dg4(int method, bool first);
 MKACC_TU_API KernelPtr wide_step(int method, bool first);     // mkacc_wide.hpp (integer 64-bit words)
 MKACC_TU_API KernelPtr widefp_step(int method, bool first);   // mkacc_widefp.hpp (FP64, Q < 2^50)
+MKACC_TU_API KernelPtr widereg_step(int method, bool first);  // mkacc_widereg.hpp (FP64, register-resident)
 }  // namespace mkacc_tu

@@ -3,15 +3,24 @@
 //   -DMKACC_TU_DG=d -DMKACC_TU_PART=0   mk_step_kernel instantiations of digit count d
 //   -DMKACC_TU_DG=d -DMKACC_TU_PART=1   mk_lat_kernel instantiations of digit count d
 //   -DMKACC_TU_DG=d -DMKACC_TU_PART=2   mk_step2_kernel instantiations of digit count d
-//   -DMKACC_TU_WIDE=1 / 2              64-bit word step kernels (integer / FP64)
+//   -DMKACC_TU_WIDE=1 / 2 / 3          64-bit word step kernels (integer / FP64 / FP64 register-resident)
 // and the host unit (mkacc_engine.hip) launches them through mkacc_tu.
 #include "mkacc_kernels.hpp"
 
 #if defined(MKACC_TU_WIDE)
 #include "mkacc_wide.hpp"
 #include "mkacc_widefp.hpp"
+#if MKACC_TU_WIDE == 3
+#include "mkacc_widereg.hpp"
+#endif
 namespace mkacc_tu {
-#if MKACC_TU_WIDE == 1
+#if MKACC_TU_WIDE == 3
+KernelPtr widereg_step(int method, bool first) {
+    if (method == XZW)
+        return first ? (KernelPtr)widereg::step_kernel<XZW, true> : (KernelPtr)widereg::step_kernel<XZW, false>;
+    return first ? (KernelPtr)widereg::step_kernel<XZW_B, true> : (KernelPtr)widereg::step_kernel<XZW_B, false>;
+}
+#elif MKACC_TU_WIDE == 1
 KernelPtr wide_step(int method, bool first) {
     if (method == XZW) return first ? (KernelPtr)wide::step_kernel<XZW, true> : (KernelPtr)wide::step_kernel<XZW, false>;
     return first ? (KernelPtr)wide::step_kernel<XZW_B, true> : (KernelPtr)wide::step_kernel<XZW_B, false>;

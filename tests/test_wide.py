@@ -76,19 +76,26 @@ def test_wide_evalacc_bitexact(mk_gpu, oracle, method, k, n, baseG, B):
     assert np.array_equal(got, exp), int(np.count_nonzero(got != exp))
 
 
+VARIANTS = {"reg": ("1", "1", "widereg::step_kernel"), "lds": ("1", "0", "widefp::step_kernel"),
+            "int": ("0", "1", "wide::step_kernel")}
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("fp", ["1", "0"])
+@pytest.mark.parametrize("variant", sorted(VARIANTS))
 @pytest.mark.parametrize("method", ["XZW", "XZW_B"])
-def test_wide_fp64_and_integer_variants(mk_gpu, oracle, monkeypatch, method, fp):
-    """Q < 2^50 runs the FP64 variant (mkacc_widefp.hpp) unless MKACC_WIDE_FP=0
-    keeps the integer kernels: both bit-exact.  The first step's digit
+def test_wide_fp64_and_integer_variants(mk_gpu, oracle, monkeypatch, method, variant):
+    """Q < 2^50 runs the register-resident FP64 kernel (mkacc_widereg.hpp) unless
+    MKACC_WFP_REG=0 selects the LDS-tile FP64 kernel (mkacc_widefp.hpp) or
+    MKACC_WIDE_FP=0 the integer kernels: all bit-exact.  The first step's digit
     decomposition sees chosen coefficients (acc = NTT(coefficients)): 0, 1,
     Q-1 and the centring boundary Q>>1, (Q>>1)+1 where the FP64 path picks the
     reference's representative explicitly; keys include all-maximal and
     balanced-boundary words.  (The device-pointer key upload of this path is
     exercised by every bench.py --q-bits 50 run, whose oracle check covers it.)"""
     mk = mk_gpu
+    fp, reg, kname = VARIANTS[variant]
     monkeypatch.setenv("MKACC_WIDE_FP", fp)
+    monkeypatch.setenv("MKACC_WFP_REG", reg)
     m = oracle.XZW if method == "XZW" else oracle.XZW_B
     k, n, B = 2, 3, 3
     orc, evk, pkey, ct, acc = make_case(oracle, m, k, n, 45181, 1 << 10, B, seed=50 + len(method), Q=Q50)
@@ -103,7 +110,7 @@ def test_wide_fp64_and_integer_variants(mk_gpu, oracle, monkeypatch, method, fp)
     pkey.reshape(-1)[:4] = [Q50 - 1, h, h + 1, 0]
     exp = orc.evalacc_batch(evk, pkey, ct, acc, 4)
     eng = _eng(mk, mk.MKNTRU if method == "XZW" else mk.MKNTRU_LWE, k, n, Q50, 45181, 1 << 10)
-    assert eng.wide
+    assert eng.wide and eng.step_kernel_name(B) == kname
     eng.upload_keys(evk.astype(np.uint64), pkey.astype(np.uint64))
     got = eng.eval_batch(ct.astype(np.uint32), acc.astype(np.uint64))
     assert np.array_equal(got, exp), int(np.count_nonzero(got != exp))
@@ -112,6 +119,28 @@ def test_wide_fp64_and_integer_variants(mk_gpu, oracle, monkeypatch, method, fp)
     f = eng.ntt_forward(a)
     assert np.array_equal(f, np.stack([oracle.ntt_forward(x, Q50, PSI50) for x in a]))
     assert np.array_equal(eng.ntt_inverse(f), a)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method", ["XZW", "XZW_B"])
+def test_wide_register_kernel_loops_over_gates(mk_gpu, oracle, method):
+    """The register-resident FP64 kernel runs one workgroup of four gates per CU
+    and loops over the batch: a batch of more than 4 x 256 gates (and not a
+    multiple of four) takes the loop; every gate equals the single-gate result,
+    and a spread sample of them equals the oracle."""
+    mk = mk_gpu
+    m = oracle.XZW if method == "XZW" else oracle.XZW_B
+    k, n, B = 2, 2, 1031
+    orc, evk, pkey, ct, acc = make_case(oracle, m, k, n, 45181, 1 << 10, B, seed=61 + len(method), Q=Q50)
+    eng = _eng(mk, mk.MKNTRU if method == "XZW" else mk.MKNTRU_LWE, k, n, Q50, 45181, 1 << 10)
+    assert eng.step_kernel_name(B) == "widereg::step_kernel"
+    eng.upload_keys(evk.astype(np.uint64), pkey.astype(np.uint64))
+    got = eng.eval_batch(ct.astype(np.uint32), acc.astype(np.uint64))
+    pick = [0, 1, 2, 3, 511, 1023, 1024, 1030]
+    exp = orc.evalacc_batch(evk, pkey, ct[pick], acc[pick], 8)
+    assert np.array_equal(got[pick], exp)
+    one = eng.eval_batch(ct[-3:].astype(np.uint32), acc[-3:].astype(np.uint64))
+    assert np.array_equal(one, got[-3:])
 
 
 @pytest.mark.gpu
