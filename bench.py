@@ -57,10 +57,16 @@ Q50 = 1125899906826241               # config 5 stress modulus (SURVEY.md s0 ite
 REF_CPU_S_PER_EVALACC = {            # reference EvalAcc, 1 core of the survey container
     "STD100_MKNTRU": 0.274, "STD128_MKNTRU": 0.475, "STD100_MKNTRU_LWE": 0.215,
     "STD100_MKNTRU_LWE_2": 0.721, "STD128_MKNTRU_3": 6.750, "STD100_MKNTRU_3": 2.872}
-# oracle / reference single-thread EvalAcc time on the same container type (BASELINE.md s3;
-# tools/oracle_calib.py, profiles/r3/oracle_calibration.json: the 32-bit word oracle path)
+# oracle / reference single-thread EvalAcc time (tools/oracle_calib.py,
+# profiles/r3/ and profiles/r4/oracle_calibration.json).  A CROSS-MACHINE estimate: the
+# oracle was timed on this repo's Intel Xeon (AVX-512) container, the reference by the
+# survey on an 8-vCPU AMD EPYC container; the reference cannot be rebuilt here to time
+# both on one CPU.  Repeat runs of the oracle side vary by ~15 %.
 ORACLE_OVER_REF = {"STD128_MKNTRU": 0.566, "STD100_MKNTRU": 0.575, "STD100_MKNTRU_LWE_2": 0.460,
                    "STD100_MKNTRU_3": 0.447, "STD128_MKNTRU_3": 0.432}
+CALIBRATION = {"same_machine": False, "oracle_cpu": "Intel Xeon (AVX-512), this repo's build container",
+               "reference_cpu": "8-vCPU AMD EPYC, the survey's probe container (SURVEY.md s6)",
+               "record": "profiles/r4/oracle_calibration.json"}
 
 
 def algorithmic_counts(k: int, n: int, dg: int, nk: int, N: int = 2048, B: int = 1, word: int = 4):
@@ -432,9 +438,12 @@ def run_rank(args, env: dict, make_engine, make_checker, torch_device: str, back
                 "host": cpu,
                 "reference_1core_s_per_evalacc": ref,
                 "oracle_over_reference_1core": ORACLE_OVER_REF.get(args.paramset) if ref else None,
-                # the reference's throughput on the same cores, scaled by the 1-core time ratio
-                "reference_equivalent_value": (G / dt_c * ORACLE_OVER_REF[args.paramset]
-                                               if ref and args.paramset in ORACLE_OVER_REF else None),
+                # the reference's throughput on the same cores, scaled by the 1-core time ratio:
+                # an estimate (the ratio compares two different CPUs, CALIBRATION); only
+                # "value" above is measured on this box
+                "reference_equivalent_estimate": (G / dt_c * ORACLE_OVER_REF[args.paramset]
+                                                  if ref and args.paramset in ORACLE_OVER_REF else None),
+                "calibration": CALIBRATION if ref else None,
                 "reference_source": "SURVEY.md s6: the reference's own EvalAcc, 1 thread of the survey container",
             }
     if world > 1:

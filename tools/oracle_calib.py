@@ -7,7 +7,7 @@ Each paramset: real keys from the keys library (seed 1), one NAND input's head
 (XZW) or the MK-LWE head (XZW_B) with the test-vector accumulator, evalacc on 1
 thread, best of --reps.  Writes JSON {paramset: {oracle_s, reference_s, ratio}}.
 
-usage: tools/oracle_calib.py [--reps 3] [--out profiles/r3/oracle_calibration.json]
+usage: tools/oracle_calib.py [--reps 3] [--out profiles/r4/oracle_calibration.json]
 """
 import argparse
 import json
@@ -57,7 +57,16 @@ def main():
     import pyoracle as oracle
     import bench
     from mkfhe_amd import keys as K
-    out = {"host": platform.processor() or platform.machine(), "threads": 1}
+    model = next((l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")),
+                 platform.processor() or platform.machine())
+    flags = next((l for l in open("/proc/cpuinfo") if l.startswith("flags")), "")
+    out = {"host": platform.machine(), "threads": 1,
+           "oracle_cpu": model + (" (AVX-512)" if "avx512f" in flags else ""),
+           "reference_cpu": "8-vCPU AMD EPYC (SURVEY.md s6: the survey's probe session)",
+           "same_machine": False,
+           "note": ("the reference cannot be rebuilt here under the rules for an oracle/_ref build (its headers "
+                    "need CMake-generated config_core.h and its library its own build system; DESIGN.md s3), so "
+                    "the ratio divides times from two different CPUs and is an estimate")}
     for ps in a.paramsets.split(","):
         t = time_one(K, oracle, ps, a.reps)
         ref = bench.REF_CPU_S_PER_EVALACC.get(ps)
