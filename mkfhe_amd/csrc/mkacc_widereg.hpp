@@ -323,35 +323,55 @@ __device__ __forceinline__ Mono make_mono(uint32_t e, uint32_t l) {
 // d_i / f_i of AddToAccXZW{0,} for one slot: widefp::key_eff (xzw.cpp:322-325,
 // 375-378; xzw_B.cpp:311-314, 368-371), |.| <= 1.13 Q (later steps), 2.75 Q (first)
 
-// One digit's MAC over the key words (2 slots per dwordx4):
-//   party (F = false): uj += g d_i, sv += g P[u][i];  f-part (F = true): uj += g f_i.
-// Digit-NTT outputs are reduced first (|g| <= Q/2 + 2), so each product is below
-// 0.8 Q (1.2 Q in the first step) and four digits keep every sum below 5.3 Q.
+// Key stream of one digit's MAC: 16 groups of 2 slots (one dwordx4 per key array),
+// kPf groups in flight.  One wave per SIMD has no other wave to hide a load behind,
+// so the first kPf groups are issued before the digit's NTT and every later group
+// kPf groups ahead of its use (the first build waited for each group right after
+// issuing it: 192 exposed L2 round trips per gate-step, 602 us per launch).
+#ifndef MKACC_WREG_PF
+#define MKACC_WREG_PF 4
+#endif
+constexpr int kPf = MKACC_WREG_PF;
+struct KGrp {
+    u32x4 a1, a2, as, ap;
+};
+struct KeySrc {
+    __amdgpu_buffer_rsrc_t rk1, rk2, rks, rpk;
+    uint32_t vo, ko, po;
+};
+template <int METHOD, bool FIRST, bool F>
+__device__ __forceinline__ void kissue(KGrp& t, const KeySrc& k, int gq) {
+    const uint32_t so = (uint32_t)gq * 1024u;
+    t.a1 = bload4(k.rk1, k.vo, k.ko + so);
+    if (METHOD == XZW) t.a2 = bload4(k.rk2, k.vo, k.ko + so);
+    if (FIRST) t.as = bload4(k.rks, k.vo, k.ko + so);
+    if (!F) t.ap = bload4(k.rpk, k.vo, k.po + so);
+}
+
+// One digit's MAC:  party (F = false): uj += g d_i, sv += g P[u][i];
+// f-part (F = true): uj += g f_i.  Digit-NTT outputs are reduced first
+// (|g| <= Q/2 + 2), so each product is below 0.8 Q (1.2 Q in the first step) and
+// four digits keep every sum below 5.3 Q.
 template <int METHOD, bool FIRST, bool F>
 __device__ __forceinline__ void mac(const double (&g)[kRegs], double (&uj)[kRegs], double (&sv)[kRegs],
-                                    const double (&mn)[kRegs], const Mono& mc, const double* psi,
-                                    __amdgpu_buffer_rsrc_t rk1, __amdgpu_buffer_rsrc_t rk2,
-                                    __amdgpu_buffer_rsrc_t rks, __amdgpu_buffer_rsrc_t rpk, uint32_t vo, uint32_t ko,
-                                    uint32_t po, const FMod& m) {
+                                    const double (&mn)[kRegs], const Mono& mc, const double* psi, KGrp (&kq)[kPf],
+                                    const KeySrc& ks, const FMod& m) {
 #pragma unroll
     for (int gq = 0; gq < kRegs / 2; ++gq) {
-        const uint32_t so = (uint32_t)gq * 1024u;
-        const u32x4 a1 = bload4(rk1, vo, ko + so);
-        const u32x4 a2 = METHOD == XZW ? bload4(rk2, vo, ko + so) : a1;
-        const u32x4 as = FIRST ? bload4(rks, vo, ko + so) : a1;
-        const u32x4 ap = F ? a1 : bload4(rpk, vo, po + so);
+        const KGrp t = kq[gq % kPf];
+        if (gq + kPf < kRegs / 2) kissue<METHOD, FIRST, F>(kq[gq % kPf], ks, gq + kPf);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int r = 2 * gq + h;
-            const double k1 = __builtin_bit_cast(double, h ? u32x2{a1.z, a1.w} : u32x2{a1.x, a1.y});
-            const double k2 = __builtin_bit_cast(double, h ? u32x2{a2.z, a2.w} : u32x2{a2.x, a2.y});
-            const double ks = __builtin_bit_cast(double, h ? u32x2{as.z, as.w} : u32x2{as.x, as.y});
+            const double k1 = __builtin_bit_cast(double, h ? u32x2{t.a1.z, t.a1.w} : u32x2{t.a1.x, t.a1.y});
+            const double k2 = METHOD == XZW ? __builtin_bit_cast(double, h ? u32x2{t.a2.z, t.a2.w} : u32x2{t.a2.x, t.a2.y}) : 0.0;
+            const double kst = FIRST ? __builtin_bit_cast(double, h ? u32x2{t.as.z, t.as.w} : u32x2{t.as.x, t.as.y}) : 0.0;
             const double gr = red(g[r], m);
             const double tp = FIRST ? mc.at(psi, r) : 0.0;
-            const double d = widefp::key_eff<METHOD, FIRST>(k1, k2, ks, tp, METHOD == XZW ? mn[r] : 0.0, m);
+            const double d = widefp::key_eff<METHOD, FIRST>(k1, k2, kst, tp, METHOD == XZW ? mn[r] : 0.0, m);
             uj[r] = __dadd_rn(uj[r], mm(gr, d, m));
             if (!F) {
-                const double pk = __builtin_bit_cast(double, h ? u32x2{ap.z, ap.w} : u32x2{ap.x, ap.y});
+                const double pk = __builtin_bit_cast(double, h ? u32x2{t.ap.z, t.ap.w} : u32x2{t.ap.x, t.ap.y});
                 sv[r] = __dadd_rn(sv[r], mm(gr, pk, m));
             }
         }
@@ -367,20 +387,24 @@ __device__ __forceinline__ void digits_pass(double (&x)[kRegs], double (&uj)[kRe
                                             __amdgpu_buffer_rsrc_t rk2, __amdgpu_buffer_rsrc_t rks,
                                             __amdgpu_buffer_rsrc_t rpk, uint32_t u) {
     const FMod& m = a.m;
-    const uint32_t vo = l * 16u, polyB = kN * 8u;
+    const uint32_t polyB = kN * 8u;
     ntt_inv(x, scr, a.tis, lds + kImgInv, lds + kImgTwist, l, m);
     uint64_t D[kRegs];
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) D[r] = offset_word(x[r], m, a.C);
 #pragma unroll 1
     for (uint32_t i = 0; i < a.dg; ++i) {
+        // key words of digit i: d-half (2i) for the parties, f-half (2i + 1) for the f-part
+        const KeySrc ks{rk1, rk2, rks, rpk, l * 16u, (2u * i + (F ? 1u : 0u)) * polyB, (u * a.dg + i) * polyB};
+        KGrp kq[kPf];
+#pragma unroll
+        for (int j = 0; j < kPf; ++j) kissue<METHOD, FIRST, F>(kq[j], ks, j);
+        sched_fence();   // in flight during the transform
         double g[kRegs];
 #pragma unroll
         for (int r = 0; r < kRegs; ++r) g[r] = digit_of(D[r], i + 1, a.sd);
         ntt_fwd<kFwd>(g, scr, a.twf, lds + kImgFwd, l, m);
-        // key words of digit i: d-half (2i) for the parties, f-half (2i + 1) for the f-part
-        const uint32_t ko = (2u * i + (F ? 1u : 0u)) * polyB, po = (u * a.dg + i) * polyB;
-        mac<METHOD, FIRST, F>(g, uj, sv, mn, mc, lds + kImgPsi, rk1, rk2, rks, rpk, vo, ko, po, m);
+        mac<METHOD, FIRST, F>(g, uj, sv, mn, mc, lds + kImgPsi, kq, ks, m);
         if ((i & 3u) == 3u) {
 #pragma unroll
             for (int r = 0; r < kRegs; ++r) {
