@@ -332,6 +332,12 @@ __device__ __forceinline__ Mono make_mono(uint32_t e, uint32_t l) {
 #define MKACC_WREG_PF 4
 #endif
 constexpr int kPf = MKACC_WREG_PF;
+// X^-c at the slots: hoisted into 64 registers once per step (1) or gathered from the
+// LDS psi table at every use (0: 64 registers free for the key stream)
+#ifndef MKACC_WREG_MN
+#define MKACC_WREG_MN 1
+#endif
+constexpr bool kHoistMn = MKACC_WREG_MN;
 struct KGrp {
     u32x4 a1, a2, as, ap;
 };
@@ -354,7 +360,8 @@ __device__ __forceinline__ void kissue(KGrp& t, const KeySrc& k, int gq) {
 // four digits keep every sum below 5.3 Q.
 template <int METHOD, bool FIRST, bool F>
 __device__ __forceinline__ void mac(const double (&g)[kRegs], double (&uj)[kRegs], double (&sv)[kRegs],
-                                    const double (&mn)[kRegs], const Mono& mc, const double* psi, KGrp (&kq)[kPf],
+                                    const double (&mn)[kRegs], const Mono& mc, const Mono& mneg, const double* psi,
+                                    KGrp (&kq)[kPf],
                                     const KeySrc& ks, const FMod& m) {
 #pragma unroll
     for (int gq = 0; gq < kRegs / 2; ++gq) {
@@ -368,7 +375,8 @@ __device__ __forceinline__ void mac(const double (&g)[kRegs], double (&uj)[kRegs
             const double kst = FIRST ? __builtin_bit_cast(double, h ? u32x2{t.as.z, t.as.w} : u32x2{t.as.x, t.as.y}) : 0.0;
             const double gr = red(g[r], m);
             const double tp = FIRST ? mc.at(psi, r) : 0.0;
-            const double d = widefp::key_eff<METHOD, FIRST>(k1, k2, kst, tp, METHOD == XZW ? mn[r] : 0.0, m);
+            const double tn = METHOD != XZW ? 0.0 : (kHoistMn ? mn[r] : mneg.at(psi, r));
+            const double d = widefp::key_eff<METHOD, FIRST>(k1, k2, kst, tp, tn, m);
             uj[r] = __dadd_rn(uj[r], mm(gr, d, m));
             if (!F) {
                 const double pk = __builtin_bit_cast(double, h ? u32x2{t.ap.z, t.ap.w} : u32x2{t.ap.x, t.ap.y});
@@ -382,7 +390,8 @@ __device__ __forceinline__ void mac(const double (&g)[kRegs], double (&uj)[kRegs
 // four digits (bound above) and at the end.
 template <int METHOD, bool FIRST, bool F>
 __device__ __forceinline__ void digits_pass(double (&x)[kRegs], double (&uj)[kRegs], double (&sv)[kRegs],
-                                            const double (&mn)[kRegs], const Mono& mc, const StepArgs& a,
+                                            const double (&mn)[kRegs], const Mono& mc, const Mono& mneg,
+                                            const StepArgs& a,
                                             double* scr, const double* lds, uint32_t l, __amdgpu_buffer_rsrc_t rk1,
                                             __amdgpu_buffer_rsrc_t rk2, __amdgpu_buffer_rsrc_t rks,
                                             __amdgpu_buffer_rsrc_t rpk, uint32_t u) {
@@ -404,7 +413,7 @@ __device__ __forceinline__ void digits_pass(double (&x)[kRegs], double (&uj)[kRe
 #pragma unroll
         for (int r = 0; r < kRegs; ++r) g[r] = digit_of(D[r], i + 1, a.sd);
         ntt_fwd<kFwd>(g, scr, a.twf, lds + kImgFwd, l, m);
-        mac<METHOD, FIRST, F>(g, uj, sv, mn, mc, lds + kImgPsi, kq, ks, m);
+        mac<METHOD, FIRST, F>(g, uj, sv, mn, mc, mneg, lds + kImgPsi, kq, ks, m);
         if ((i & 3u) == 3u) {
 #pragma unroll
             for (int r = 0; r < kRegs; ++r) {
@@ -440,12 +449,10 @@ __device__ __forceinline__ void one_gate(const StepArgs& a, uint32_t gate, doubl
     const double* psi = lds + kImgPsi;
     const Mono mc = make_mono(c, l);
     // X^-c at this lane's slots: the same for every digit and pass of the step
+    const Mono mneg = make_mono(cneg, l);
     double mn[kRegs];
-    {
-        const Mono mneg = make_mono(cneg, l);
 #pragma unroll
-        for (int r = 0; r < kRegs; ++r) mn[r] = METHOD == XZW ? mneg.at(psi, r) : 0.0;
-    }
+    for (int r = 0; r < kRegs; ++r) mn[r] = METHOD == XZW && kHoistMn ? mneg.at(psi, r) : 0.0;
     double sv[kRegs], uj[kRegs];
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) sv[r] = 0.0;
@@ -461,11 +468,11 @@ __device__ __forceinline__ void one_gate(const StepArgs& a, uint32_t gate, doubl
             // acctemp = acc (X^c - 1)      (xzw.cpp:336-338); the first step overwrites acc
             if (!FIRST) x[r] = __dsub_rn(mm(x[r], mc.at(psi, r), m), x[r]);
         }
-        digits_pass<METHOD, FIRST, false>(x, uj, sv, mn, mc, a, scr, lds, l, rk1, rk2, rks, rpk, u);
+        digits_pass<METHOD, FIRST, false>(x, uj, sv, mn, mc, mneg, a, scr, lds, l, rk1, rk2, rks, rpk, u);
         if (tt < k) store_poly(uj, rout, vo, u * polyB);
     }
     // f-part: iNTT(sumV) -> SDD -> NTT -> acc[index] += <., f>      (xzw.cpp:272-289)
-    digits_pass<METHOD, FIRST, true>(sv, uj, sv, mn, mc, a, scr, lds, l, rk1, rk2, rks, rpk, index);
+    digits_pass<METHOD, FIRST, true>(sv, uj, sv, mn, mc, mneg, a, scr, lds, l, rk1, rk2, rks, rpk, index);
     store_poly(uj, rout, vo, index * polyB);
 }
 
