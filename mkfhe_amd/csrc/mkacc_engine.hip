@@ -306,6 +306,8 @@ bool use_lat(const mkacc_ctx* c, size_t B) {
 // Step2Cfg::kSvMem).
 size_t step_scratch_words(const mkacc_ctx* c) {
     if (use_dscr(c)) return (size_t)c->dg * kN;
+    // mk_step2_kernel at dg = 4 in two halves parks its ev2 partial sums there
+    if (c->step_ver == 2 && c->dg == 4 && s2_halves<4>()) return kN;
 #if defined(MKACC_S2_SVMEM) && MKACC_S2_SVMEM
     if (c->step_ver == 2) return kN;   // A/B build only: the default kernel keeps sumV in registers
 #endif

@@ -218,6 +218,136 @@ __device__ __forceinline__ void mac2(const StepCtx& s, uint32_t u, const uint32_
     vcc_fence();   // the caller's branches follow the last reductions
 }
 
+// ---- dg = 4 in two halves (config 4, STD128_MKNTRU_3) ----------------------------
+// The 4 x 32 digit-NTT registers of the one-stream form need the whole register
+// file (one wave per SIMD, 1.46 ms per launch against 1.19 ms for mk_step_kernel).
+// Two streams of two digits each keep 2 x 32 G registers and two waves per SIMD:
+//   half 0: G = NTT(digits 1, 2); a1 = start + sum G ev1', a2 = sum G ev2 (split form)
+//           -> p1 = redc(a1) into acc_out[u], p2 = redc(a2) into the gate's scratch
+//   half 1: G = NTT(digits 3, 4); a1 = p1 r32 + sum G ev1', a2 = p2 r32 + sum G ev2
+//           -> acc_out[u] = redc(a1) + (X^(N-c) - 1) redc(a2)
+// sumV is reduced after each stream as in mac2.  Same sums mod Q, so bit-exact.
+#ifndef MKACC_S2_HALVES
+#define MKACC_S2_HALVES 1
+#endif
+template <int DG>
+constexpr bool s2_halves() { return DG == 4 && MKACC_S2_HALVES; }
+
+template <int METHOD, bool FIRST>
+struct HalfCfg {
+    static constexpr bool kSplit = METHOD == XZW && !FIRST;
+    static constexpr bool kK2 = METHOD == XZW;
+#ifndef MKACC_S2H_GS
+#define MKACC_S2H_GS 2
+#endif
+#ifndef MKACC_S2H_PF
+#define MKACC_S2H_PF 2
+#endif
+    static constexpr int kGS = MKACC_S2H_GS;
+    static constexpr int kPf = MKACC_S2H_PF;
+    static constexpr int kGroups = kRegs / kGS;
+    static constexpr int kBuf = kPf + 1;
+    __device__ __forceinline__ static constexpr uint32_t soff(int g) {
+        return (uint32_t)(((g * kGS) >> 2) * 1024 + ((g * kGS) & 3) * 4);
+    }
+};
+template <int METHOD, bool FIRST>
+struct GrpH {
+    using L = VecLd<HalfCfg<METHOD, FIRST>::kGS>;
+    using V = typename L::T;
+    V k1[2];
+    V k2[HalfCfg<METHOD, FIRST>::kK2 ? 2 : 1];
+    V ks[FIRST ? 2 : 1];
+    V pk[2];
+    V st, st2;
+};
+
+__device__ __forceinline__ void hstore(u32x4 v, __amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so) { bstore4(v, r, vo, so); }
+__device__ __forceinline__ void hstore(u32x2 v, __amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so) {
+    __builtin_amdgcn_raw_buffer_store_b64(v, r, vo, so, 0);
+}
+__device__ __forceinline__ void hstore(u32x1 v, __amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so) {
+    __builtin_amdgcn_raw_buffer_store_b32(v.v, r, vo, so, 0);
+}
+// One stream of half H (digits 2H + 1, 2H + 2) of party u (F = false) or the f-part (F = true).
+template <int METHOD, bool FIRST, bool F, int H>
+__device__ __forceinline__ void mac2h(const StepCtx& s, uint32_t u, const uint32_t (&G)[2][kRegs],
+                                      uint32_t (&sv)[kRegs]) {
+    using C = HalfCfg<METHOD, FIRST>;
+    using Grp = GrpH<METHOD, FIRST>;
+    using L = typename Grp::L;
+    const uint32_t Q = s.m.Q, polyB = kN * 4u, vo = s.vo;
+    const uint32_t half = F ? polyB : 0u;
+    const uint32_t uoff = u * polyB;
+    const uint32_t poff = (u * 4u + 2u * H) * polyB;
+    // start value: half 0 -- acc_u (party; none in the first step, which overwrites
+    // acc) or the index party's output (f-part); half 1 -- the parked p1 (+ p2)
+    constexpr bool kStart = H == 1 || F || !FIRST;
+    auto issue = [&](Grp& t, int g) {
+        const uint32_t so = C::soff(g);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const uint32_t ko = (uint32_t)(2 * (2 * H + j)) * polyB + half + so;
+            t.k1[j] = L::ld(s.rk1, vo, ko);
+            if (C::kK2) t.k2[j] = L::ld(s.rk2, vo, ko);
+            if (FIRST) t.ks[j] = L::ld(s.rks, vo, ko);
+            if (!F) t.pk[j] = L::ld(s.rpk, vo, poff + (uint32_t)j * polyB + so);
+        }
+        if (kStart) t.st = L::ld(H == 1 || F ? s.rout : s.rin, vo, uoff + so);
+        if (H == 1 && C::kSplit) t.st2 = L::ld(s.rds, vo, so);
+    };
+    Grp kg[C::kBuf];
+#pragma unroll
+    for (int j = 0; j < C::kPf; ++j) issue(kg[j], j);
+#pragma unroll
+    for (int g = 0; g < C::kGroups; ++g) {
+        if (g + C::kPf < C::kGroups) issue(kg[(g + C::kPf) % C::kBuf], g + C::kPf);
+        const Grp& t = kg[g % C::kBuf];
+        typename L::T ov, o2;
+#pragma unroll
+        for (int e = 0; e < C::kGS; ++e) {
+            const int r = g * C::kGS + e;
+            uint64_t a1 = kStart ? mad64(t.st[e], s.m.r32, 0) : 0ull;
+            uint64_t a2 = (H == 1 && C::kSplit) ? mad64(t.st2[e], s.m.r32, 0) : 0ull;
+            uint64_t sa = F ? 0ull : mad64(sv[r], s.m.r32, 0);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                if constexpr (C::kSplit) {
+                    a1 = mad64(G[j][r], t.k1[j][e], a1);
+                    a2 = mad64(G[j][r], t.k2[j][e], a2);
+                } else {
+                    const uint32_t ke = key_eff<METHOD, FIRST, 1>(t.k1[j][e], C::kK2 ? t.k2[j][e] : 0u,
+                                                                 FIRST ? t.ks[j][e] : 0u, s.tb.psi, s.mp, s.mn, r, Q);
+                    a1 = mad64(G[j][r], ke, a1);
+                }
+                if (!F) sa = mad64(G[j][r], t.pk[j][e], sa);
+            }
+            uint32_t v = redc(a1, Q, s.m.qinv);                                   // [0, 2Q)
+            if constexpr (C::kSplit) {
+                const uint32_t v2 = redc(a2, Q, s.m.qinv);                        // [0, 2Q)
+                if (H == 0) {
+                    o2[e] = v2;                                                   // parked p2
+                } else {
+                    v += mul_shoup_lazy(v2, s.mn.at(s.tb.psi, r), Q);             // [0, 4Q)
+                    v = min(v, v - 2u * Q);
+                }
+            }
+            ov[e] = v;
+            if (!F) sv[r] = redc(sa, Q, s.m.qinv);
+        }
+        // default write policy for the parked p1 / p2 (read back by this wave after
+        // two digit NTTs); VecLd::st's L2-bypassing policy for the final outputs
+        if (H == 0) {
+            hstore(ov, s.rout, vo, uoff + C::soff(g));
+            if (C::kSplit) hstore(o2, s.rds, vo, C::soff(g));
+        } else {
+            L::st(ov, s.rout, vo, uoff + C::soff(g));
+        }
+        sched_fence();
+    }
+    vcc_fence();
+}
+
 // iNTT -> SDD -> dg forward NTTs: x (layout C, [0, 2Q)) -> G[i] = NTT(digit i + 1)
 template <int DG>
 __device__ __forceinline__ void digit_ntts(const StepCtx& s, uint32_t (&x)[kRegs], uint32_t (&G)[DG][kRegs]) {
@@ -248,7 +378,7 @@ constexpr int s2_waves_per_simd() {
 #ifdef MKACC_S2_WPS
     return MKACC_S2_WPS;
 #else
-    return DG <= 3 ? 2 : 1;
+    return DG <= 3 || s2_halves<DG>() ? 2 : 1;
 #endif
 }
 template <int DG, int METHOD, bool FIRST>
@@ -280,8 +410,9 @@ __global__ __launch_bounds__(64 * kS2Waves, 4 * s2_waves_per_simd<DG>() / kS2Wav
                     make_rsrc(a.key2, DG * 2 * polyB),
                     make_rsrc(a.keys, DG * 2 * polyB),
                     make_rsrc(a.pkey, k * DG * polyB),
-                    make_rsrc(Step2Cfg<DG, METHOD, FIRST>::kSvMem ? a.dscr + (size_t)gate * kN : a.acc_in,
-                              Step2Cfg<DG, METHOD, FIRST>::kSvMem ? polyB : 0u)};
+                    make_rsrc(Step2Cfg<DG, METHOD, FIRST>::kSvMem || s2_halves<DG>() ? a.dscr + (size_t)gate * kN
+                                                                                    : a.acc_in,
+                              Step2Cfg<DG, METHOD, FIRST>::kSvMem || s2_halves<DG>() ? polyB : 0u)};
     const uint32_t Q = s.m.Q;
     uint32_t sv[kRegs];
 #pragma unroll
@@ -324,12 +455,46 @@ __global__ __launch_bounds__(64 * kS2Waves, 4 * s2_waves_per_simd<DG>() / kS2Wav
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         vcc_fence();   // the branch above follows the rotation's multiply-adds
-        uint32_t G[DG][kRegs];
-        digit_ntts<DG>(s, x, G);
-        vcc_fence();   // the MAC branch follows the last butterflies
-        if (!fpart)
-            mac2<DG, METHOD, FIRST, false>(s, u, G, sv, t == 0 ? 0u : s.m.r32);
-        else
-            mac2<DG, METHOD, FIRST, true>(s, index, G, sv);
+        if constexpr (s2_halves<DG>()) {
+            const uint32_t Q = s.m.Q;
+            ntt_inv(x, s.lds, s.tw_inv, s.tb.twi, s.l, Q);
+            PackedDigits<DG> pd;
+            uint32_t G[2][kRegs];
+#pragma unroll
+            for (int r = 0; r < kRegs; ++r) {
+                G[0][r] = pd.put(r, sdd_offset(x[r], s.sd), s.sd);
+                if ((r & 7) == 7) sched_fence();
+            }
+            ntt_fwd(G[0], s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, s.l, Q, s.m.m1);
+#pragma unroll
+            for (int r = 0; r < kRegs; ++r) G[1][r] = pd.get(r, 2, s.sd);
+            ntt_fwd(G[1], s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, s.l, Q, s.m.m1);
+            vcc_fence();
+            if (!fpart)
+                mac2h<METHOD, FIRST, false, 0>(s, u, G, sv);
+            else
+                mac2h<METHOD, FIRST, true, 0>(s, index, G, sv);
+#pragma unroll
+            for (int r = 0; r < kRegs; ++r) G[0][r] = pd.get(r, 3, s.sd);
+            ntt_fwd(G[0], s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, s.l, Q, s.m.m1);
+#pragma unroll
+            for (int r = 0; r < kRegs; ++r) G[1][r] = pd.get(r, 4, s.sd);
+            ntt_fwd(G[1], s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, s.l, Q, s.m.m1);
+            vcc_fence();
+            // the parked p1 / p2 of this wave are read back in the next stream
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (!fpart)
+                mac2h<METHOD, FIRST, false, 1>(s, u, G, sv);
+            else
+                mac2h<METHOD, FIRST, true, 1>(s, index, G, sv);
+        } else {
+            uint32_t G[DG][kRegs];
+            digit_ntts<DG>(s, x, G);
+            vcc_fence();   // the MAC branch follows the last butterflies
+            if (!fpart)
+                mac2<DG, METHOD, FIRST, false>(s, u, G, sv, t == 0 ? 0u : s.m.r32);
+            else
+                mac2<DG, METHOD, FIRST, true>(s, index, G, sv);
+        }
     }
 }
