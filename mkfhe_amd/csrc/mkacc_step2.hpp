@@ -43,6 +43,9 @@ template <>
 struct VecLd<4> {
     using T = u32x4;
     __device__ __forceinline__ static T ld(__amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so) { return bload4(r, vo, so); }
+    __device__ __forceinline__ static T ld_sc1(__amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so) {
+        return __builtin_amdgcn_raw_buffer_load_b128(r, vo, so, 16);
+    }
     __device__ __forceinline__ static void st(T v, __amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so) {
         __builtin_amdgcn_raw_buffer_store_b128(v, r, vo, so, MKACC_S2_STAUX);
         __builtin_amdgcn_sched_barrier(0);
@@ -54,6 +57,9 @@ template <>
 struct VecLd<2> {
     using T = u32x2;
     __device__ __forceinline__ static T ld(__amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so) { return bload2(r, vo, so); }
+    __device__ __forceinline__ static T ld_sc1(__amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so) {
+        return __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, 16);
+    }
     // 8-byte stores carry no store-data hazard (bstore4)
     __device__ __forceinline__ static void st(T v, __amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so) {
         __builtin_amdgcn_raw_buffer_store_b64(v, r, vo, so, MKACC_S2_STAUX);
@@ -70,6 +76,9 @@ struct VecLd<1> {
     using T = u32x1;
     __device__ __forceinline__ static T ld(__amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so) {
         return T{__builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0)};
+    }
+    __device__ __forceinline__ static T ld_sc1(__amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so) {
+        return T{__builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 16)};
     }
     __device__ __forceinline__ static void st(T v, __amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so) {
         __builtin_amdgcn_raw_buffer_store_b32(v.v, r, vo, so, MKACC_S2_STAUX);
@@ -293,8 +302,12 @@ __device__ __forceinline__ void mac2h(const StepCtx& s, uint32_t u, const uint32
             if (FIRST) t.ks[j] = L::ld(s.rks, vo, ko);
             if (!F) t.pk[j] = L::ld(s.rpk, vo, poff + (uint32_t)j * polyB + so);
         }
-        if (kStart) t.st = L::ld(H == 1 || F ? s.rout : s.rin, vo, uoff + so);
-        if (H == 1 && C::kSplit) t.st2 = L::ld(s.rds, vo, so);
+        // this wave's own earlier stores are read back L1-bypassing (sc1): p1 / p2 are
+        // rewritten every pass, and acc_out[index] was read as p1 before the f-part, so
+        // the CU's L1 can hold a stale line of either (first build: 14 of 16 gates wrong
+        // at full size with 4-slot groups)
+        if (kStart) t.st = (H == 1 || F) ? L::ld_sc1(s.rout, vo, uoff + so) : L::ld(s.rin, vo, uoff + so);
+        if (H == 1 && C::kSplit) t.st2 = L::ld_sc1(s.rds, vo, so);
     };
     Grp kg[C::kBuf];
 #pragma unroll
