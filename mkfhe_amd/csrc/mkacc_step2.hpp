@@ -303,9 +303,12 @@ __device__ __forceinline__ void mac2h(const StepCtx& s, uint32_t u, const uint32
             if (!F) t.pk[j] = L::ld(s.rpk, vo, poff + (uint32_t)j * polyB + so);
         }
         // this wave's own earlier stores are read back L1-bypassing (sc1): p1 / p2 are
-        // rewritten every pass, and acc_out[index] was read as p1 before the f-part, so
-        // the CU's L1 can hold a stale line of either (first build: 14 of 16 gates wrong
-        // at full size with 4-slot groups)
+        // rewritten every pass, and acc_out[index] is read as p1 before the f-part reads
+        // it again, so correctness does not rest on the vector L1's write policy.  (The
+        // 4-slot-group build's 14 of 16 wrong gates at full size were a store-data
+        // hazard instead: under its 60+ spilled VGPRs the register allocator put a copy
+        // into a dwordx4 store's data registers ahead of bstore4's s_nop -- found by
+        // tools/isa_audit.py, which tools/build_variant.sh now runs on every variant.)
         if (kStart) t.st = (H == 1 || F) ? L::ld_sc1(s.rout, vo, uoff + so) : L::ld(s.rin, vo, uoff + so);
         if (H == 1 && C::kSplit) t.st2 = L::ld_sc1(s.rds, vo, so);
     };

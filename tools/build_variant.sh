@@ -9,4 +9,8 @@ python3 -m mkfhe_amd.build --variant "$NAME" "$@" > /dev/null   # add --units a,
 rc=$?
 grep -A9 "mk_step2_kernelILi3ELi0ELb0E" mkfhe_amd/lib/variants/$NAME.res | grep -E "VGPRs( Spill)?:" | sed 's/.*remark: *//' | tr '\n' ' '
 echo " [$NAME rc=$rc]"
+# store-data / VCC hazard audit of the variant (a violation corrupts stores under load)
+python3 tools/isa_audit.py mkfhe_amd/lib/variants/$NAME.so > /tmp/isa_audit_$$.txt; a=$?
+tail -1 /tmp/isa_audit_$$.txt; rm -f /tmp/isa_audit_$$.txt
+[ $a -eq 0 ] || rc=1
 exit $rc
