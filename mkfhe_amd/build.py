@@ -25,7 +25,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(_HERE)
 SOURCES = [os.path.join(_HERE, "csrc", f) for f in ("mkacc_engine.hip", "mkacc_steps.hip")]
 HEADERS = [os.path.join(_HERE, "csrc", f) for f in ("mkacc_kernels.hpp", "mkacc_step2.hpp", "mkacc_device.hpp", "mkacc_host_math.hpp",
-                                                    "mkacc_gate.hpp", "mkacc_wide.hpp", "mkacc_widefp.hpp", "mkacc_widereg.hpp")] + [
+                                                    "mkacc_gate.hpp", "mkacc_wide.hpp", "mkacc_widefp.hpp", "mkacc_widereg.hpp",
+                                                    "mkacc_widereg2.hpp")] + [
     os.path.join(ROOT, "include", "mkfhe_amd.h")]
 OUT = os.path.join(_HERE, "lib", "libmkfhe_amd.so")
 KEYS_SOURCES = [os.path.join(_HERE, "csrc", "mkkeys.cpp")]

@@ -55,6 +55,7 @@ int fail(int code, const std::string& msg) {
 #include "mkacc_wide.hpp"
 #include "mkacc_widefp.hpp"
 #include "mkacc_widereg.hpp"
+#include "mkacc_widereg2.hpp"
 
 namespace {
 
@@ -64,7 +65,7 @@ namespace {
 template <typename W>
 __global__ void wide_key_layout_kernel(const W* __restrict__ src, uint64_t* __restrict__ dst, size_t npolys,
                                        uint32_t nk, uint32_t n1, uint32_t dg2, uint64_t Q, uint64_t r, uint64_t rp,
-                                       bool fp, bool c8, uint32_t* __restrict__ bad) {
+                                       bool fp, uint32_t lay, uint32_t* __restrict__ bad) {
     const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= npolys * kN) return;
     size_t p = idx / kN;
@@ -76,7 +77,8 @@ __global__ void wide_key_layout_kernel(const W* __restrict__ src, uint64_t* __re
     const size_t dpoly = ((u * n1 + i) * nk + jj) * dg2 + dp;
     const uint64_t x = (uint64_t)src[idx];
     if (x >= Q) *bad = 1u;
-    const uint32_t jd = c8 ? widereg::c8_index(j) : j;   // register-resident FP64 kernel: C8 layout
+    // register-resident FP64 kernels: C8 (one wave per gate) or C16 (two) layout
+    const uint32_t jd = lay == 1 ? widereg::c8_index(j) : lay == 2 ? widereg2::c16_index(j) : j;
     if (fp) {
         const double d = (double)(x < Q ? x : 0) - (x > (Q >> 1) && x < Q ? (double)Q : 0.0);
         dst[dpoly * kN + jd] = (uint64_t)__double_as_longlong(d);
@@ -249,7 +251,11 @@ struct mkacc_ctx {
     bool wfp = false;
     widefp::FMod wfm{};
     double wfninv = 0, wfC = 0;
+    double wfcL = 0, wfCm = 0;     // widereg offset-word constants (mkacc_widereg.hpp offset_word)
     bool wfreg = false;            // FP64 register-resident kernel (mkacc_widereg.hpp), C8 layouts
+    bool wfreg2 = false;           // ... with two waves per gate (mkacc_widereg2.hpp), C16 layouts
+    double* d_r2tab = nullptr;     // its per-lane twiddle table (widereg2::kTabD doubles)
+    uint32_t wlay() const { return wfreg2 ? 2u : (wfreg ? 1u : 0u); }
     double* d_rimg = nullptr;      // its LDS image (widereg::kImgD doubles)
     double* d_rtis = nullptr;      // its inverse pass-1 table [32]
     double* d_ftwf = nullptr;      // forward / inverse twiddles and psi^e, balanced
@@ -608,9 +614,9 @@ int upload_keys_device_impl(mkacc_ctx* c, const W* d_evk, const W* d_pkey) {
         if (!c->d_wkeys) HIP_TRY(hipMalloc(&c->d_wkeys, ep * kN * 8));
         if (!c->d_wpkey) HIP_TRY(hipMalloc(&c->d_wpkey, pp * kN * 8));
         hipLaunchKernelGGL(wide_key_layout_kernel<W>, grid(ep), dim3(tpb), 0, c->stream, d_evk, c->d_wkeys, ep, nk,
-                           n1, dg * 2, Q, R, Rp, c->wfp, c->wfreg, kbad);
+                           n1, dg * 2, Q, R, Rp, c->wfp, c->wlay(), kbad);
         hipLaunchKernelGGL(wide_key_layout_kernel<W>, grid(pp), dim3(tpb), 0, c->stream, d_pkey, c->d_wpkey, pp, 1u,
-                           1u, dg, Q, R, Rp, c->wfp, c->wfreg, kbad);
+                           1u, dg, Q, R, Rp, c->wfp, c->wlay(), kbad);
     } else {
         if (!c->d_keys) HIP_TRY(hipMalloc(&c->d_keys, ep * kN * 4));
         if (!c->d_pkey) HIP_TRY(hipMalloc(&c->d_pkey, pp * kN * 4));
@@ -721,7 +727,11 @@ int wide_setup(mkacc_ctx* c) {
         // register-resident kernel (mkacc_widereg.hpp, default; MKACC_WFP_REG=0 keeps
         // widefp::step_kernel): per-lane twiddle image in the 27-bit kernels' twl layout
         const char* re = std::getenv("MKACC_WFP_REG");
-        c->wfreg = !(re && re[0] == '0');
+        // offset_word's 2^52 form needs C + L >= 0 and C + (Q - 1) / 2 < 2^52
+        const uint64_t cL = (Q + 1) / 2;
+        c->wfreg = !(re && re[0] == '0') && C >= cL && C + (Q >> 1) < (1ull << 52);
+        c->wfcL = (double)cL;
+        c->wfCm = (double)((1ull << 52) + (C - std::min(C, cL)));
         if (c->wfreg) {
             std::vector<double> img(widereg::kImgD), tis(32, 0.0);
             double* F = img.data() + widereg::kImgFwd;
@@ -755,6 +765,48 @@ int wide_setup(mkacc_ctx* c) {
             for (uint32_t e = 0; e < 2u * kN; ++e) P[e] = fpw[e];
             for (int b = 0; b < 5; ++b)
                 for (int t = 0; t < (1 << b); ++t) tis[(1 << b) + t] = bal(pwi[(size_t)t << (11 - b)]);
+            // two waves per gate (mkacc_widereg2.hpp, default; MKACC_WREG2=0 keeps one): its
+            // per-lane twiddle table, value k of sub-table T for (w, l) at
+            // ((kTG0[T] + k / 2) * 128 + w * 64 + l) * 2 + k % 2 (index maps checked against
+            // the oracle by tools/widereg2_model.py)
+            const char* r2 = std::getenv("MKACC_WREG2");
+            c->wfreg2 = !(r2 && r2[0] == '0');
+            if (c->wfreg2) {
+                using namespace widereg2;
+                std::vector<double> tab(kTabD, 0.0);
+                auto put = [&](int T, uint32_t w, uint32_t l, int k, double v) {
+                    tab[((size_t)(kTG0[T] + k / 2) * 128 + w * 64 + l) * 2 + (k & 1)] = v;
+                };
+                auto lg = [](int v) { int b = 0; while ((2 << b) <= v) ++b; return b; };   // floor(log2 v)
+                for (uint32_t w = 0; w < 2; ++w)
+                    for (uint32_t l = 0; l < 64; ++l) {
+                        const uint32_t l3 = (l >> 3) & 1u, l4 = (l >> 4) & 1u, l5 = (l >> 5) & 1u;
+                        auto pb = [&](uint32_t r) { return (r << 3) | (l & 7u) | (l3 << 7) | (l4 << 8) | (l5 << 9) | (w << 10); };
+                        auto pd = [&](uint32_t r) { return (r << 4) | (l & 15u) | (l4 << 8) | (l5 << 9) | (w << 10); };
+                        for (int k = 0; k < 7; ++k) {          // forward B2, stages 4..6
+                            const int st = 4 + lg(k + 1), m = k - ((1 << (st - 4)) - 1);
+                            put(TFB, w, l, k, ftf[(1u << st) + (pb((uint32_t)m << (8 - st)) >> (11 - st))]);
+                        }
+                        for (int k = 0; k < 15; ++k) {         // forward C2, stages 7..10
+                            const int st = 7 + lg(k + 1), m = k - ((1 << (st - 7)) - 1);
+                            put(TFC, w, l, k, ftf[(1u << st) + (pos_c(w, l, (uint32_t)m << (11 - st)) >> (11 - st))]);
+                        }
+                        for (int k = 0; k < 15; ++k) {         // inverse D2, bits 4..7
+                            const int b = 4 + lg(k + 1), H = 1 << (b - 4);
+                            const uint32_t t = pd((uint32_t)(k - (H - 1))) & ((1u << b) - 1u);
+                            put(TID, w, l, k, bal(pwi[(size_t)t << (11 - b)]));
+                        }
+                        for (int k = 0; k < 14; ++k) {         // inverse A2, bits 8..10
+                            const int b = k < 2 ? 8 : (k < 6 ? 9 : 10), H = 1 << (b - 7);
+                            const uint32_t t = pos_a(w, l, (uint32_t)(k - (H - 2))) & ((1u << b) - 1u);
+                            put(TIA, w, l, k, bal(pwi[(size_t)t << (11 - b)]));
+                        }
+                        for (int k = 0; k < 16; ++k)           // twist psi^-p N^-1
+                            put(TTW, w, l, k, bal(mulmod(pwi[pos_a(w, l, (uint32_t)k)], c->wninv, Q)));
+                    }
+                HIP_TRY(hipMalloc(&c->d_r2tab, tab.size() * sizeof(double)));
+                HIP_TRY(hipMemcpy(c->d_r2tab, tab.data(), tab.size() * sizeof(double), hipMemcpyHostToDevice));
+            }
             HIP_TRY(hipMalloc(&c->d_rimg, img.size() * sizeof(double)));
             HIP_TRY(hipMalloc(&c->d_rtis, tis.size() * sizeof(double)));
             HIP_TRY(hipMemcpy(c->d_rimg, img.data(), img.size() * sizeof(double), hipMemcpyHostToDevice));
@@ -784,8 +836,9 @@ int wide_upload_keys(mkacc_ctx* c, const W* evk, const W* pkey) {
     const uint32_t k = c->p.k, n = c->p.n, nk = c->nk, dg = c->dg;
     const size_t blk = (size_t)dg * 2 * kN;
     // the register-resident FP64 kernel reads every polynomial in the C8 layout
-    auto pos = [c8 = c->wfreg](size_t s) {
-        return c8 ? (s & ~(size_t)(kN - 1)) | widereg::c8_index((uint32_t)(s & (kN - 1))) : s;
+    auto pos = [lay = c->wlay()](size_t s) {
+        const uint32_t j = (uint32_t)(s & (kN - 1));
+        return (s & ~(size_t)(kN - 1)) | (lay == 1 ? widereg::c8_index(j) : lay == 2 ? widereg2::c16_index(j) : j);
     };
     std::vector<uint64_t> host((size_t)k * (n + 1) * nk * blk);
     for (uint32_t u = 0; u < k; ++u)
@@ -844,6 +897,47 @@ int wide_launch_batch(mkacc_ctx* c, const uint32_t* d_ct, const uint64_t* d_in, 
     auto key = [&](uint32_t u, uint32_t i, uint32_t j) {
         return c->d_wkeys + (((size_t)u * (n + 1) + i) * c->nk + j) * blk;
     };
+    if (c->wfreg2) {   // two waves per gate: balanced doubles in the C16 layout
+        const size_t words = B * (size_t)k * kN;
+        const dim3 g((unsigned)((words + 255) / 256));
+        double* cur = reinterpret_cast<double*>(c->d_wacc0);
+        double* nxt = reinterpret_cast<double*>(c->d_wacc1);
+        hipLaunchKernelGGL(widereg2::to_c16_kernel, g, dim3(256), 0, c->stream, d_in, cur, words, c->wfm, c->p.Q,
+                           c->d_bad);
+        auto dk = [](const uint64_t* p) { return reinterpret_cast<const double*>(p); };
+        // four 2-wave workgroups per CU, looping over the batch
+        const size_t wgs = std::min<size_t>(B, (size_t)c->cus * 4);
+        for (uint32_t u = 0; u < k; ++u)
+            for (uint32_t i = 0; i < n; ++i) {
+                const bool first = (u == 0 && i == 0);
+                widereg2::StepArgs a;
+                a.acc_in = cur;
+                a.acc_out = nxt;
+                a.cvals = c->d_wcvals + ((size_t)u * n + i) * B;
+                a.key1 = dk(key(u, i, 0));
+                a.key2 = dk(c->nk == 2 ? key(u, i, 1) : key(u, i, 0));
+                a.keys = dk(key(0, n, 0));
+                a.pkey = dk(c->d_wpkey);
+                a.tab = c->d_r2tab;
+                a.psi = c->d_fpsi;
+                a.twf = c->d_ftwf;
+                a.tis = c->d_rtis;
+                a.B = (uint32_t)B;
+                a.k = k;
+                a.index = u;
+                a.dg = c->dg;
+                a.cL = c->wfcL;
+                a.Cm = c->wfCm;
+                a.m = c->wfm;
+                a.sd = c->wsd;
+                launch_ptr(mkacc_tu::widereg2_step(c->method_class, first), dim3((unsigned)wgs), dim3(128),
+                           widereg2::kLdsBytes, c->stream, a);
+                std::swap(cur, nxt);
+            }
+        hipLaunchKernelGGL(widereg2::from_c16_kernel, g, dim3(256), 0, c->stream, cur, d_out, words, c->wfm);
+        HIP_TRY(hipGetLastError());
+        return MKACC_OK;
+    }
     if (c->wfreg) {   // register-resident FP64 kernel: balanced doubles in the C8 layout
         const size_t words = B * (size_t)k * kN;
         const dim3 g((unsigned)((words + 255) / 256));
@@ -872,7 +966,8 @@ int wide_launch_batch(mkacc_ctx* c, const uint32_t* d_ct, const uint64_t* d_in, 
                 a.k = k;
                 a.index = u;
                 a.dg = c->dg;
-                a.C = c->wfC;
+                a.cL = c->wfcL;
+                a.Cm = c->wfCm;
                 a.m = c->wfm;
                 a.sd = c->wsd;
                 launch_ptr(mkacc_tu::widereg_step(c->method_class, first), dim3((unsigned)wgs),
@@ -992,7 +1087,13 @@ int wide_prim(mkacc_ctx* c, const uint64_t* in, uint64_t* out, size_t count, int
     HIP_TRY(hipMalloc(&dout, count * kN * 8 * out_mul));
     HIP_TRY(hipMemcpyAsync(din, in, count * kN * 8, hipMemcpyHostToDevice, c->stream));
     const unsigned rgrid = (unsigned)((count + widereg::kWaves - 1) / widereg::kWaves);
-    if (which == 0 && c->wfreg)
+    if (which == 0 && c->wfreg2)
+        hipLaunchKernelGGL(widereg2::ntt_fwd_kernel, dim3((unsigned)count), dim3(128), widereg2::kLdsBytes, c->stream,
+                           din, dout, c->d_r2tab, c->d_ftwf, c->wfm);
+    else if (which == 1 && c->wfreg2)
+        hipLaunchKernelGGL(widereg2::ntt_inv_kernel, dim3((unsigned)count), dim3(128), widereg2::kLdsBytes, c->stream,
+                           din, dout, c->d_r2tab, c->d_rtis, c->wfm);
+    else if (which == 0 && c->wfreg)
         hipLaunchKernelGGL(widereg::ntt_fwd_kernel, dim3(rgrid), dim3(64 * widereg::kWaves), widereg::kLdsBytes,
                            c->stream, din, dout, (uint32_t)count, c->d_rimg, c->d_ftwf, c->wfm);
     else if (which == 1 && c->wfreg)
@@ -1260,7 +1361,7 @@ void mkacc_destroy(mkacc_ctx* c) {
                     (void*)c->d_acc0, (void*)c->d_acc1, (void*)c->d_cvals, (void*)c->d_dscr, (void*)c->d_ct,
                     (void*)c->d_io, (void*)c->d_ksk, (void*)c->d_lweA, (void*)c->d_lweB, (void*)c->d_tv,
                     (void*)c->d_digits, (void*)c->d_bh, (void*)c->d_gin, (void*)c->d_gout, (void*)c->d_wtwf,
-                    (void*)c->d_wtwi, (void*)c->d_wpsi, (void*)c->d_ftwf, (void*)c->d_ftwi, (void*)c->d_fpsi, (void*)c->d_rimg, (void*)c->d_rtis,
+                    (void*)c->d_wtwi, (void*)c->d_wpsi, (void*)c->d_ftwf, (void*)c->d_ftwi, (void*)c->d_fpsi, (void*)c->d_rimg, (void*)c->d_rtis, (void*)c->d_r2tab,
                     (void*)c->d_wkeys, (void*)c->d_wpkey, (void*)c->d_wacc0,
                     (void*)c->d_wacc1, (void*)c->d_wcvals, (void*)c->d_wct, (void*)c->d_wio, (void*)c->d_bad})
         if (p) (void)hipFree(p);
@@ -1304,7 +1405,10 @@ int mkacc_upload_keys_device(mkacc_ctx* c, const void* d_evk, const void* d_pkey
 
 const char* mkacc_step_kernel_name(const mkacc_ctx* c, size_t B) {
     if (!c) return "";
-    if (c->wide) return c->wfreg ? "widereg::step_kernel" : (c->wfp ? "widefp::step_kernel" : "wide::step_kernel");
+    if (c->wide)
+        return c->wfreg2  ? "widereg2::step_kernel"
+               : c->wfreg ? "widereg::step_kernel"
+                          : (c->wfp ? "widefp::step_kernel" : "wide::step_kernel");
     if (use_lat(c, B)) return "mk_lat_kernel";
     return c->step_ver == 2 ? "mk_step2_kernel" : "mk_step_kernel";
 }

@@ -906,4 +906,5 @@ MKACC_TU_API KernelPtr lat_dg4(int method, bool first);
 MKACC_TU_API KernelPtr wide_step(int method, bool first);     // mkacc_wide.hpp (integer 64-bit words)
 MKACC_TU_API KernelPtr widefp_step(int method, bool first);   // mkacc_widefp.hpp (FP64, Q < 2^50)
 MKACC_TU_API KernelPtr widereg_step(int method, bool first);  // mkacc_widereg.hpp (FP64, register-resident)
+MKACC_TU_API KernelPtr widereg2_step(int method, bool first);  // mkacc_widereg2.hpp (FP64, two waves per gate)
 }  // namespace mkacc_tu

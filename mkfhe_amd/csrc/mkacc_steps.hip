@@ -12,6 +12,7 @@
 #include "mkacc_widefp.hpp"
 #if MKACC_TU_WIDE == 3
 #include "mkacc_widereg.hpp"
+#include "mkacc_widereg2.hpp"
 #endif
 namespace mkacc_tu {
 #if MKACC_TU_WIDE == 3
@@ -19,6 +20,11 @@ KernelPtr widereg_step(int method, bool first) {
     if (method == XZW)
         return first ? (KernelPtr)widereg::step_kernel<XZW, true> : (KernelPtr)widereg::step_kernel<XZW, false>;
     return first ? (KernelPtr)widereg::step_kernel<XZW_B, true> : (KernelPtr)widereg::step_kernel<XZW_B, false>;
+}
+KernelPtr widereg2_step(int method, bool first) {
+    if (method == XZW)
+        return first ? (KernelPtr)widereg2::step_kernel<XZW, true> : (KernelPtr)widereg2::step_kernel<XZW, false>;
+    return first ? (KernelPtr)widereg2::step_kernel<XZW_B, true> : (KernelPtr)widereg2::step_kernel<XZW_B, false>;
 }
 #elif MKACC_TU_WIDE == 1
 KernelPtr wide_step(int method, bool first) {

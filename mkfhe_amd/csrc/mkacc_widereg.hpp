@@ -127,9 +127,12 @@ constexpr InvPlan1 make_inv1(int x0, int thr) {
     return p;
 }
 
-// forward: digits (|x| < 2^25 < Q / 4) or balanced residues (primitive kernel)
+// forward: balanced residues (primitive kernel), and the step's digits
+// (|x| <= 2^(b-1) <= 2^25, below Q / 1000 at the config-5 modulus): starting the
+// plan from 0.001 Q drops one of the two 16-element reductions per digit NTT
 constexpr FPlan kFwd = make_plan(510, 0, 11);
-static_assert(kFwd.out <= kLim, "forward bounds");
+constexpr FPlan kFwdDig = make_plan(1, 0, 11);
+static_assert(kFwd.out <= kLim && kFwdDig.out <= kLim, "forward bounds");
 // inverse: the rotated accumulator (< 1.14 Q) or sumV (< 0.51 Q)
 constexpr InvPlan1 kInv1 = make_inv1(1140, 1200);
 constexpr FPlan kInv23 = make_plan(kInv1.out, 5, 11);
@@ -278,10 +281,21 @@ __device__ __forceinline__ void store_poly(const double (&x)[kRegs], __amdgpu_bu
     }
 }
 
-// the reference's centred coefficient, offset for the closed-form digits
-// (widefp::sdd_offset; D < 2^53 since b * digitsG <= 52)
-__device__ __forceinline__ uint64_t offset_word(double t, const FMod& m, double C) {
-    return (uint64_t)__dadd_rn(widefp::centred(t, m), C);
+// The offset word D = centred(t) + C of the closed-form digits (widefp::sdd_offset),
+// with centred(t) in [L, L + Q), L = -(Q + 1) / 2 (mk-acc.cpp:60-64), in 9 FP64
+// operations and no integer conversion:
+//   s = t - L, y = s - Q floor(s / Q) in [0, Q)   (|t| <= 2.5 Q, so |s / Q| < 3.5 and the
+//       product s * RN(1/Q) is within 3.5 * 2^-52 < 1/Q of s / Q: floor is exact except
+//       when s is a multiple of Q, where it can come out one short -- y = Q, mapped to 0)
+//   D = y + (C + L): added to 2^52 the sum is an exact double in [2^52, 2^53) whose
+//       low 52 bits ARE D (C + L >= 0 and D < 2^52 when b * digitsG <= 52, host-checked),
+//       and every digit field lies below bit 52
+__device__ __forceinline__ uint64_t offset_word(double t, const FMod& m, double cL, double Cm) {
+    const double s = __dadd_rn(t, cL);
+    const double q = floor(__dmul_rn(s, m.Qi));
+    double y = __fma_rn(-q, m.Q, s);
+    y = y >= m.Q ? __dsub_rn(y, m.Q) : y;
+    return __builtin_bit_cast(uint64_t, __dadd_rn(y, Cm));   // 2^52 + D
 }
 __device__ __forceinline__ double digit_of(uint64_t D, uint32_t i, const wide::Sdd64& s) {
     const uint32_t f = (uint32_t)(D >> (s.gbits * i)) & (uint32_t)((s.half << 1) - 1);
@@ -300,7 +314,8 @@ struct StepArgs {
     const double* twf;        // forward table, reference order (pass A reads [1, 32))
     const double* tis;        // inverse pass-1 table [(1 << b) + t]
     uint32_t B, k, index, dg;
-    double C;                 // SDD offset constant
+    double cL;                // (Q + 1) / 2 = -L
+    double Cm;                // 2^52 + C + L (C: SDD offset constant)
     FMod m;
     wide::Sdd64 sd;
 };
@@ -387,7 +402,9 @@ __device__ __forceinline__ void mac(const double (&g)[kRegs], double (&uj)[kRegs
 }
 
 // iNTT(x) -> offset words -> for each digit: NTT, MAC.  uj / sv reduced every
-// four digits (bound above) and at the end.
+// kRedEvery digits and at the end: from |.| <= Q/2 + 2, a later step's products stay
+// below 0.78 Q (d_i, |d| <= 1.13 Q) and 0.63 Q (P), so seven digits keep the sums
+// below 6 Q; the first step's d_i (<= 2.75 Q) gives 1.19 Q per product: four digits.
 template <int METHOD, bool FIRST, bool F>
 __device__ __forceinline__ void digits_pass(double (&x)[kRegs], double (&uj)[kRegs], double (&sv)[kRegs],
                                             const double (&mn)[kRegs], const Mono& mc, const Mono& mneg,
@@ -397,10 +414,11 @@ __device__ __forceinline__ void digits_pass(double (&x)[kRegs], double (&uj)[kRe
                                             __amdgpu_buffer_rsrc_t rpk, uint32_t u) {
     const FMod& m = a.m;
     const uint32_t polyB = kN * 8u;
+    constexpr uint32_t kRedEvery = FIRST ? 4u : 7u;
     ntt_inv(x, scr, a.tis, lds + kImgInv, lds + kImgTwist, l, m);
     uint64_t D[kRegs];
 #pragma unroll
-    for (int r = 0; r < kRegs; ++r) D[r] = offset_word(x[r], m, a.C);
+    for (int r = 0; r < kRegs; ++r) D[r] = offset_word(x[r], m, a.cL, a.Cm);
 #pragma unroll 1
     for (uint32_t i = 0; i < a.dg; ++i) {
         // key words of digit i: d-half (2i) for the parties, f-half (2i + 1) for the f-part
@@ -412,9 +430,9 @@ __device__ __forceinline__ void digits_pass(double (&x)[kRegs], double (&uj)[kRe
         double g[kRegs];
 #pragma unroll
         for (int r = 0; r < kRegs; ++r) g[r] = digit_of(D[r], i + 1, a.sd);
-        ntt_fwd<kFwd>(g, scr, a.twf, lds + kImgFwd, l, m);
+        ntt_fwd<kFwdDig>(g, scr, a.twf, lds + kImgFwd, l, m);
         mac<METHOD, FIRST, F>(g, uj, sv, mn, mc, mneg, lds + kImgPsi, kq, ks, m);
-        if ((i & 3u) == 3u) {
+        if (i % kRedEvery == kRedEvery - 1) {
 #pragma unroll
             for (int r = 0; r < kRegs; ++r) {
                 uj[r] = red(uj[r], m);
