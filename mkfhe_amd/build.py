@@ -26,7 +26,8 @@ ROOT = os.path.dirname(_HERE)
 SOURCES = [os.path.join(_HERE, "csrc", f) for f in ("mkacc_engine.hip", "mkacc_steps.hip")]
 HEADERS = [os.path.join(_HERE, "csrc", f) for f in ("mkacc_kernels.hpp", "mkacc_step2.hpp", "mkacc_device.hpp", "mkacc_host_math.hpp",
                                                     "mkacc_gate.hpp", "mkacc_wide.hpp", "mkacc_widefp.hpp", "mkacc_widereg.hpp",
-                                                    "mkacc_widereg2.hpp")] + [
+                                                    "mkacc_widereg2.hpp", "mkacc_layout2.hpp",
+                                                    "mkacc_step3.hpp")] + [
     os.path.join(ROOT, "include", "mkfhe_amd.h")]
 OUT = os.path.join(_HERE, "lib", "libmkfhe_amd.so")
 KEYS_SOURCES = [os.path.join(_HERE, "csrc", "mkkeys.cpp")]
@@ -102,6 +103,7 @@ UNITS = [("engine", "mkacc_engine.hip", [])] + [
     (f"lat_dg{d}", "mkacc_steps.hip", [f"-DMKACC_TU_DG={d}", "-DMKACC_TU_PART=1"]) for d in (2, 3, 4)] + [
     (f"step2_dg{d}", "mkacc_steps.hip", [f"-DMKACC_TU_DG={d}", "-DMKACC_TU_PART=2"] + STEP2_SCHED.get(d, []))
     for d in (2, 3, 4)] + [
+    (f"step3_dg{d}", "mkacc_steps.hip", [f"-DMKACC_TU_DG={d}", "-DMKACC_TU_PART=3"]) for d in (2, 3, 4)] + [
     ("wide", "mkacc_steps.hip", ["-DMKACC_TU_WIDE=1"]), ("widefp", "mkacc_steps.hip", ["-DMKACC_TU_WIDE=2"]),
     ("widereg", "mkacc_steps.hip", ["-DMKACC_TU_WIDE=3"])]
 

@@ -638,11 +638,11 @@ __device__ __forceinline__ uint32_t sdd_digit(uint32_t D, uint32_t i, const SddC
 //            elements per register (16 VGPRs).
 //   DG >= 4: (DG-1) b <= 20 (b = 6 at DG = 4, b = 5 at DG = 5): the low 16 bits
 //            two per register, the high 4 bits eight per register (20 VGPRs).
-template <int DG>
+template <int DG, int R = kRegs>
 struct PackedDigits {
     static constexpr bool kWide = DG > 3;
-    uint32_t lo[kRegs / 2];
-    uint32_t hi[kWide ? kRegs / 8 : 1];
+    uint32_t lo[R / 2];
+    uint32_t hi[kWide ? R / 8 : 1];
 
     // element r with offset word D: returns digit 1 (NTT input), stores the rest
     __device__ __forceinline__ uint32_t put(int r, uint32_t D, const SddConsts& s) {

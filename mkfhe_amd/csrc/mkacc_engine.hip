@@ -103,13 +103,22 @@ __global__ void wide_key_layout_kernel(const W* __restrict__ src, uint64_t* __re
 // workspace for that kernel.
 int step_version(int dg) {
     const char* e = std::getenv("MKACC_STEP");
-    if (dg == 4) return e && e[0] == '2' ? 2 : 1;   // A/B: mk_step2_kernel at one wave per SIMD
     if (dg > 4) return 1;
+    if (e && e[0] == '3') return 3;                 // mk_step3_kernel (two waves per gate)
+    if (dg == 4) return e && e[0] == '2' ? 2 : 1;   // A/B: mk_step2_kernel at one wave per SIMD
     if (e && e[0] == '1') return 1;
     return 2;
 }
 
 const void* step_fn(int dg, int method, bool first, bool dscr, int ver) {
+    if (ver == 3) {
+        switch (dg) {
+            case 2: return mkacc_tu::step3_dg2(method, first);
+            case 3: return mkacc_tu::step3_dg3(method, first);
+            case 4: return mkacc_tu::step3_dg4(method, first);
+            default: return nullptr;
+        }
+    }
     if (ver == 2) {
         switch (dg) {
             case 2: return mkacc_tu::step2_dg2(method, first);
@@ -200,6 +209,7 @@ struct mkacc_ctx {
     int cus = 256;                // compute units of the device (mk_lat_kernel residency)
     int method_class = XZW;   // XZW or XZW_B
     int step_ver = 1;         // batch step kernel generation (step_version)
+    uint2* d_tab3 = nullptr;  // mk_step3_kernel per-lane twiddle table (lay2::kTabE pairs)
     uint32_t dg = 0, nk = 0;
     Mod mod{};
     SddConsts sd{};
@@ -370,6 +380,7 @@ uint32_t* launch_steps(mkacc_ctx* c, size_t B) {
             a.m = c->mod;
             a.sd = c->sd;
             a.dscr = c->d_dscr;
+            a.tab3 = c->d_tab3;
             // a null kernel must never reach hipLaunchKernelGGL (mkacc_create checks the set)
             if (lat) {
                 const void* fn = lat_fn((int)c->dg, c->method_class, first);
@@ -378,7 +389,9 @@ uint32_t* launch_steps(mkacc_ctx* c, size_t B) {
             } else {
                 const void* fn = step_fn((int)c->dg, c->method_class, first, !first && use_dscr(c), c->step_ver);
                 if (!fn) return nullptr;
-                if (c->step_ver == 2)
+                if (c->step_ver == 3)   // one 2-wave workgroup per gate
+                    launch_ptr(fn, dim3((unsigned)B), dim3(128), s3::kLdsBytes + (lds - kStepLdsBytes), c->stream, a);
+                else if (c->step_ver == 2)
                     launch_ptr(fn, dim3((unsigned)((B + kS2Waves - 1) / kS2Waves)), dim3(64 * kS2Waves),
                                kStep2LdsBytes + (lds - kStepLdsBytes), c->stream, a);
                 else
@@ -772,11 +785,9 @@ int wide_setup(mkacc_ctx* c) {
             const char* r2 = std::getenv("MKACC_WREG2");
             c->wfreg2 = !(r2 && r2[0] == '0');
             if (c->wfreg2) {
-                using namespace widereg2;
-                std::vector<double> tab(kTabD, 0.0);
-                auto put = [&](int T, uint32_t w, uint32_t l, int k, double v) {
-                    tab[((size_t)(kTG0[T] + k / 2) * 128 + w * 64 + l) * 2 + (k & 1)] = v;
-                };
+                using namespace lay2;
+                std::vector<double> tab(kTabE, 0.0);
+                auto put = [&](int T, uint32_t w, uint32_t l, int k, double v) { tab[tab_index(T, w, l, k)] = v; };
                 auto lg = [](int v) { int b = 0; while ((2 << b) <= v) ++b; return b; };   // floor(log2 v)
                 for (uint32_t w = 0; w < 2; ++w)
                     for (uint32_t l = 0; l < 64; ++l) {
@@ -1345,6 +1356,37 @@ int mkacc_create(const mkacc_params* pin, int device, mkacc_ctx** out) {
             img[kPsm1Off + psi_pos(e)] = pair((pw[e] + Q - 1) % Q);
         }
     }
+    // mk_step3_kernel's per-lane twiddle pairs (mkacc_layout2.hpp tables, EVAL layout LC4;
+    // index maps checked against the oracle by tools/widereg2_model.py)
+    std::vector<uint2> t3(lay2::kTabE, make_uint2(0, 0));
+    {
+        using namespace lay2;
+        auto lg = [](int v) { int b = 0; while ((2 << b) <= v) ++b; return b; };   // floor(log2 v)
+        for (uint32_t w = 0; w < 2; ++w)
+            for (uint32_t l = 0; l < 64; ++l) {
+                for (int k = 0; k < 7; ++k) {          // forward LB, stages 4..6
+                    const int st = 4 + lg(k + 1), m = k - ((1 << (st - 4)) - 1);
+                    t3[tab_index(TFB, w, l, k)] = htf[(1u << st) + (pos_b(w, l, (uint32_t)m << (8 - st)) >> (11 - st))];
+                }
+                for (int k = 0; k < 15; ++k) {         // forward LC4, stages 7..10
+                    const int st = 7 + lg(k + 1), m = k - ((1 << (st - 7)) - 1);
+                    t3[tab_index(TFC, w, l, k)] = htf[(1u << st) + (pos_c4(w, l, (uint32_t)m << (11 - st)) >> (11 - st))];
+                }
+                for (int k = 0; k < 15; ++k) {         // inverse LD, bits 4..7
+                    const int b = 4 + lg(k + 1), H = 1 << (b - 4);
+                    const uint32_t t = pos_d(w, l, (uint32_t)(k - (H - 1))) & ((1u << b) - 1u);
+                    t3[tab_index(TID, w, l, k)] = npair(pwi[(size_t)t << (11 - b)]);
+                }
+                for (int k = 0; k < 14; ++k) {         // inverse LA, bits 8..10
+                    const int b = k < 2 ? 8 : (k < 6 ? 9 : 10), H = 1 << (b - 7);
+                    const uint32_t t = pos_a(w, l, (uint32_t)(k - (H - 2))) & ((1u << b) - 1u);
+                    t3[tab_index(TIA, w, l, k)] = npair(pwi[(size_t)t << (11 - b)]);
+                }
+                for (int k = 0; k < 16; ++k) t3[tab_index(TTW, w, l, k)] = pair(pwi[pos_a(w, l, (uint32_t)k)]);
+            }
+    }
+    HIP_TRY(hipMalloc(&c->d_tab3, t3.size() * sizeof(uint2)));
+    HIP_TRY(hipMemcpy(c->d_tab3, t3.data(), t3.size() * sizeof(uint2), hipMemcpyHostToDevice));
     HIP_TRY(hipMalloc(&c->d_img, img.size() * sizeof(uint2)));
     HIP_TRY(hipMemcpy(c->d_twf, htf.data(), htf.size() * sizeof(uint2), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->d_twi, hti.data(), hti.size() * sizeof(uint2), hipMemcpyHostToDevice));
@@ -1361,7 +1403,7 @@ void mkacc_destroy(mkacc_ctx* c) {
                     (void*)c->d_acc0, (void*)c->d_acc1, (void*)c->d_cvals, (void*)c->d_dscr, (void*)c->d_ct,
                     (void*)c->d_io, (void*)c->d_ksk, (void*)c->d_lweA, (void*)c->d_lweB, (void*)c->d_tv,
                     (void*)c->d_digits, (void*)c->d_bh, (void*)c->d_gin, (void*)c->d_gout, (void*)c->d_wtwf,
-                    (void*)c->d_wtwi, (void*)c->d_wpsi, (void*)c->d_ftwf, (void*)c->d_ftwi, (void*)c->d_fpsi, (void*)c->d_rimg, (void*)c->d_rtis, (void*)c->d_r2tab,
+                    (void*)c->d_wtwi, (void*)c->d_wpsi, (void*)c->d_ftwf, (void*)c->d_ftwi, (void*)c->d_fpsi, (void*)c->d_rimg, (void*)c->d_rtis, (void*)c->d_r2tab, (void*)c->d_tab3,
                     (void*)c->d_wkeys, (void*)c->d_wpkey, (void*)c->d_wacc0,
                     (void*)c->d_wacc1, (void*)c->d_wcvals, (void*)c->d_wct, (void*)c->d_wio, (void*)c->d_bad})
         if (p) (void)hipFree(p);
@@ -1410,7 +1452,7 @@ const char* mkacc_step_kernel_name(const mkacc_ctx* c, size_t B) {
                : c->wfreg ? "widereg::step_kernel"
                           : (c->wfp ? "widefp::step_kernel" : "wide::step_kernel");
     if (use_lat(c, B)) return "mk_lat_kernel";
-    return c->step_ver == 2 ? "mk_step2_kernel" : "mk_step_kernel";
+    return c->step_ver == 3 ? "mk_step3_kernel" : (c->step_ver == 2 ? "mk_step2_kernel" : "mk_step_kernel");
 }
 int mkacc_is_wide(const mkacc_ctx* c) { return c && c->wide ? (c->wfp ? 2 : 1) : 0; }
 

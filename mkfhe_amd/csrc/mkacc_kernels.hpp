@@ -94,6 +94,7 @@ struct StepArgs {
     const uint2* tw_fwd;       // [N] reference forward table (pass A, scalar reads)
     const uint2* tw_inv;       // [32] inverse pass-1 table (ntt_inv)
     uint32_t* dscr;            // [B][dg][N] C4 scratch of the step's d_i (mk_step_kernel DSCR) or null
+    const uint2* tab3;         // mk_step3_kernel: per-lane twiddle pairs (mkacc_layout2.hpp tables)
     uint32_t B, k, index;
     Mod m;
     SddConsts sd;
@@ -191,9 +192,9 @@ __device__ __forceinline__ uint32_t from3q(uint32_t d, uint32_t Q) {
 
 // Effective key word d_i / f_i of mk-acc-xzw(_B).cpp AddToAccXZW{,0}, below KD Q.
 // k1 is the stored ev1 word (ev1 + ev2 for MKNTRU, StepArgs), k2 = ev2, ks = evs.
-template <int METHOD, bool FIRST, int KD>
+template <int METHOD, bool FIRST, int KD, class M>
 __device__ __forceinline__ uint32_t key_eff(uint32_t k1, uint32_t k2, uint32_t ks, const uint2* psi,
-                                            const Mono& mp, const Mono& mn, int r, uint32_t Q) {
+                                            const M& mp, const M& mn, int r, uint32_t Q) {
     if (METHOD == XZW) {
         if (FIRST) {
             // evs + ev1*(X^c-1) + ev2*(X^-c-1)          (xzw.cpp:375-378)
@@ -215,11 +216,11 @@ __device__ __forceinline__ uint32_t key_eff(uint32_t k1, uint32_t k2, uint32_t k
 }
 
 // digit NTT outputs: [0, 4Q) for DG <= 4, brought to [0, 2Q) at DG = 5 (Bounds::kG)
-template <int DG>
-__device__ __forceinline__ void digit_range(uint32_t (&x)[kRegs], uint32_t Q) {
+template <int DG, int R>
+__device__ __forceinline__ void digit_range(uint32_t (&x)[R], uint32_t Q) {
     if (DG > 4) {
 #pragma unroll
-        for (int r = 0; r < kRegs; ++r) x[r] = min(x[r], x[r] - 2u * Q);
+        for (int r = 0; r < R; ++r) x[r] = min(x[r], x[r] - 2u * Q);
     }
 }
 
@@ -872,6 +873,8 @@ StepFn pick_step(int method, bool first, bool dscr) {
 
 
 #include "mkacc_step2.hpp"
+#include "mkacc_layout2.hpp"
+#include "mkacc_step3.hpp"
 
 template <int DG>
 StepFn pick_step2(int method, bool first) {
@@ -900,6 +903,9 @@ MKACC_TU_API KernelPtr step_dg5(int method, bool first, bool dscr);
 MKACC_TU_API KernelPtr step2_dg2(int method, bool first);   // mk_step2_kernel (mkacc_step2.hpp)
 MKACC_TU_API KernelPtr step2_dg3(int method, bool first);
 MKACC_TU_API KernelPtr step2_dg4(int method, bool first);
+MKACC_TU_API KernelPtr step3_dg2(int method, bool first);   // mk_step3_kernel (mkacc_step3.hpp)
+MKACC_TU_API KernelPtr step3_dg3(int method, bool first);
+MKACC_TU_API KernelPtr step3_dg4(int method, bool first);
 MKACC_TU_API KernelPtr lat_dg2(int method, bool first);
 MKACC_TU_API KernelPtr lat_dg3(int method, bool first);
 MKACC_TU_API KernelPtr lat_dg4(int method, bool first);

@@ -52,9 +52,13 @@ KernelPtr MKACC_CAT(step_dg, MKACC_TU_DG)(int method, bool first, bool dscr) {
 KernelPtr MKACC_CAT(lat_dg, MKACC_TU_DG)(int method, bool first) {
     return (KernelPtr)pick_lat<MKACC_TU_DG>(method, first);
 }
-#else
+#elif MKACC_TU_PART == 2
 KernelPtr MKACC_CAT(step2_dg, MKACC_TU_DG)(int method, bool first) {
     return (KernelPtr)pick_step2<MKACC_TU_DG>(method, first);
+}
+#else
+KernelPtr MKACC_CAT(step3_dg, MKACC_TU_DG)(int method, bool first) {
+    return (KernelPtr)pick_step3<MKACC_TU_DG>(method, first);
 }
 #endif
 }  // namespace mkacc_tu

@@ -17,7 +17,7 @@
 // (wave w, lane l, register r) in one of four layouts:
 //   A2  r = p10..p7, w = p6,  l = p5..p0                  coefficients
 //   B2  r = p6..p3,  w = p10, l = (p9, p8, p7, p2, p1, p0)
-//   C2  r = p3..p0,  w = p10, l = (p8, p9, p7, p6, p5, p4) EVAL slots
+//   C2  r = p3..p0,  w = p10, l = (p8, p4, p7, p9, p6, p5) EVAL slots
 //   D2  r = p7..p4,  w = p10, l = (p9, p8, p3, p2, p1, p0)
 // (l written l5..l0).  Forward: A2 stages 0-3 (wave-uniform twiddles) -> B2 stages
 // 4-6 -> C2 stages 7-10; inverse: C2 bits 0-3 (wave-uniform) -> D2 bits 4-7 ->
@@ -45,84 +45,39 @@ using widereg::kRedB;
 using widereg::tbound;
 using widereg::make_plan;
 
-constexpr int kR = 16;                 // doubles per lane and polynomial
-constexpr int kBufD = 2175;            // LDS words of one transpose buffer (max address 2174)
-constexpr size_t kLdsBytes = 2 * kBufD * 8;   // two ping-pong buffers per gate
+using lay2::kR;
+using lay2::Lane;
+using lay2::LA;
+using lay2::LB;
+using lay2::LC;
+using lay2::LD;
+using lay2::pos_a;
+using lay2::pos_c;
+using lay2::tload;
+using lay2::transpose;
+using lay2::TFB;
+using lay2::TFC;
+using lay2::TID;
+using lay2::TIA;
+using lay2::TTW;
+constexpr int kBufD = lay2::kBufE;                 // doubles of one transpose buffer
+constexpr size_t kLdsBytes = 2 * kBufD * 8;        // two ping-pong buffers per gate
 static_assert(4 * kLdsBytes <= 160 * 1024, "four gates (eight waves) per CU");
+constexpr int kTabD = lay2::kTabE;
 
-// ---- layouts --------------------------------------------------------------------
-enum { LA = 0, LB = 1, LC = 2, LD = 3 };
-constexpr int kW[11] = {1, 2, 4, 8, 16, 33, 66, 136, 272, 548, 1088};
-// register offset of register r in layout L (compile time)
-template <int L>
-__host__ __device__ constexpr int roff(int r) {
-    const int b0 = r & 1, b1 = (r >> 1) & 1, b2 = (r >> 2) & 1, b3 = (r >> 3) & 1;
-    return L == LA   ? b0 * kW[7] + b1 * kW[8] + b2 * kW[9] + b3 * kW[10]
-           : L == LB ? b0 * kW[3] + b1 * kW[4] + b2 * kW[5] + b3 * kW[6]
-           : L == LC ? r
-                     : b0 * kW[4] + b1 * kW[5] + b2 * kW[6] + b3 * kW[7];
-}
-// lane / wave base of layout L
-template <int L>
-__host__ __device__ __forceinline__ uint32_t lbase(uint32_t l, uint32_t w) {
-    const uint32_t l0 = l & 1u, l1 = (l >> 1) & 1u, l2 = (l >> 2) & 1u, l3 = (l >> 3) & 1u, l4 = (l >> 4) & 1u,
-                   l5 = (l >> 5) & 1u;
-    if (L == LA) return (l & 31u) + l5 * kW[5] + w * kW[6];
-    if (L == LB) return (l & 7u) + l3 * kW[7] + l4 * kW[8] + l5 * kW[9] + w * kW[10];
-    if (L == LC) return l0 * kW[4] + l1 * kW[5] + l2 * kW[6] + l3 * kW[7] + l4 * kW[9] + l5 * kW[8] + w * kW[10];
-    return (l & 15u) + l4 * kW[8] + l5 * kW[9] + w * kW[10];
-}
-// position p of (w, l, r) in layout C2 (EVAL slot) and A2 (coefficient)
-__host__ __device__ __forceinline__ uint32_t pos_c(uint32_t w, uint32_t l, uint32_t r) {
-    return r | ((l & 15u) << 4) | (((l >> 5) & 1u) << 8) | (((l >> 4) & 1u) << 9) | (w << 10);
-}
-__host__ __device__ __forceinline__ uint32_t pos_a(uint32_t w, uint32_t l, uint32_t r) {
-    return (r << 7) | (w << 6) | l;
-}
 // device ("C16") word of EVAL slot p: wave half, then register pair, lane, pair element
 // -- a wave moves its half of a polynomial with 8 dwordx4 accesses of 1 KiB
 __host__ __device__ __forceinline__ uint32_t c16_index(uint32_t p) {
     const uint32_t r = p & 15u;
-    const uint32_t l = ((p >> 4) & 15u) | (((p >> 9) & 1u) << 4) | (((p >> 8) & 1u) << 5);
+    const uint32_t l = ((p >> 5) & 1u) | (((p >> 6) & 1u) << 1) | (((p >> 9) & 1u) << 2) | (((p >> 7) & 1u) << 3) |
+                       (((p >> 4) & 1u) << 4) | (((p >> 8) & 1u) << 5);   // lay2 LC lane of p
     return ((p >> 10) << 10) | ((r >> 1) << 7) | (l << 1) | (r & 1u);
 }
 
-// ---- per-lane twiddle table (HBM, built by the host) ------------------------------
-// value k of sub-table T for (w, l) at double ((kG0[T] + k / 2) * 128 + w * 64 + l) * 2 + k % 2
-enum { TFB = 0, TFC = 1, TID = 2, TIA = 3, TTW = 4 };
-constexpr int kTG0[5] = {0, 4, 12, 20, 27};   // first pair of FB (7 values), FC (15), ID (15), IA (14), TW (16)
-constexpr int kTPairs = 35;
-constexpr int kTabD = kTPairs * 128 * 2;
-
 template <int NP>
-struct TwPairs {
-    u32x4 v[NP];
-    __device__ __forceinline__ double at(int k) const {
-        const u32x4& q = v[k >> 1];
-        return __builtin_bit_cast(double, (k & 1) ? u32x2{q.z, q.w} : u32x2{q.x, q.y});
-    }
+struct TwPairs : lay2::TwPairs<NP> {
+    __device__ __forceinline__ double at(int k) const { return __builtin_bit_cast(double, this->raw(k)); }
 };
-template <int T, int NP>
-__device__ __forceinline__ void tload(TwPairs<NP>& t, __amdgpu_buffer_rsrc_t rt, uint32_t vo) {
-#pragma unroll
-    for (int g = 0; g < NP; ++g) t.v[g] = bload4(rt, vo, (uint32_t)(kTG0[T] + g) * 2048u);
-}
-
-// ---- cross-wave transpose ------------------------------------------------------------
-__device__ __forceinline__ void pair_sync() {
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
-template <int SRC, int DST>
-__device__ __forceinline__ void transpose(double (&x)[kR], double* buf, uint32_t l, uint32_t w) {
-    double* ws = buf + lbase<SRC>(l, w);
-#pragma unroll
-    for (int r = 0; r < kR; ++r) ws[roff<SRC>(r)] = x[r];
-    pair_sync();
-    const double* rs = buf + lbase<DST>(l, w);
-#pragma unroll
-    for (int r = 0; r < kR; ++r) x[r] = rs[roff<DST>(r)];
-    asm volatile("" ::: "memory");
-}
 
 // ---- inverse pass-1 plan (bits 0..3, 16 registers) ------------------------------------
 struct InvPlan1 {
@@ -181,11 +136,6 @@ __device__ __forceinline__ const_f64* opaque_c(const double* p) {
     asm volatile("" : "+s"(v));
     return (const_f64*)v;
 }
-
-struct Lane {
-    uint32_t l, w;      // lane, wave of the gate (0 / 1)
-    uint32_t vt;        // byte offset of this lane in a twiddle-table pair row: (w * 64 + l) * 16
-};
 
 // Forward negacyclic NTT (reference EVAL order): coefficients in A2 -> slots in C2.
 //   tws: reference forward table (balanced), wave-uniform indices 1..15
@@ -302,7 +252,7 @@ __device__ __forceinline__ void store_poly(const double (&x)[kR], __amdgpu_buffe
 }
 
 // X^e at slot p = pos_c(w, l, r): psi^(e (2 brv11(p) + 1)); brv11(p) = (brv4(r) << 7) + Lw,
-// Lw = 64 l0 + 32 l1 + 16 l2 + 8 l3 + 2 l4 + 4 l5 + w, so the exponent is
+// Lw = 32 l0 + 16 l1 + 2 l2 + 8 l3 + 64 l4 + 4 l5 + w (p5, p6, p9, p7, p4, p8), so the exponent is
 // e (2 Lw + 1) + (e brv4(r) << 8) mod 2N.  psi: the balanced psi^e table in HBM.
 struct Mono {
     uint32_t wp, e;
@@ -312,8 +262,8 @@ struct Mono {
     }
 };
 __device__ __forceinline__ Mono make_mono(uint32_t e, uint32_t l, uint32_t w) {
-    const uint32_t Lw = ((l & 1u) << 6) | (((l >> 1) & 1u) << 5) | (((l >> 2) & 1u) << 4) | (((l >> 3) & 1u) << 3) |
-                        (((l >> 4) & 1u) << 1) | (((l >> 5) & 1u) << 2) | w;
+    const uint32_t Lw = ((l & 1u) << 5) | (((l >> 1) & 1u) << 4) | (((l >> 2) & 1u) << 1) | (((l >> 3) & 1u) << 3) |
+                        (((l >> 4) & 1u) << 6) | (((l >> 5) & 1u) << 2) | w;
     return Mono{(e * (2u * Lw + 1u)) & (2u * kN - 1u), e};
 }
 __device__ __forceinline__ double ldd(__amdgpu_buffer_rsrc_t r, uint32_t vo) {

@@ -125,11 +125,12 @@ def test_evalacc_dscr_modes(mk, oracle, case, dscr, monkeypatch):
     assert np.array_equal(got, exp.astype(np.uint32))
 
 
-@pytest.mark.parametrize("step", ["1", "2"])
+@pytest.mark.parametrize("step", ["1", "2", "3"])
 @pytest.mark.parametrize("case", CASES, ids=[f"{c[0]}-k{c[1]}-logB{c[4].bit_length() - 1}" for c in CASES])
 def test_evalacc_step_kernels(mk, oracle, case, step, monkeypatch):
-    """Both batch step kernels -- mk_step_kernel (1) and mk_step2_kernel (2, digit
-    NTTs first, one key stream per pass; built for dg <= 4) -- give the oracle's
+    """The batch step kernels -- mk_step_kernel (1), mk_step2_kernel (2, digit
+    NTTs first, one key stream per pass) and mk_step3_kernel (3, the same with a
+    gate split over two waves); 2 and 3 are built for dg <= 4 -- give the oracle's
     accumulators for every case shape; MKACC_STEP is read when the context is
     created (it sizes the workspace), MKACC_LAT=0 keeps small batches off the
     one-wave-per-party kernel."""
@@ -144,7 +145,8 @@ def test_evalacc_step_kernels(mk, oracle, case, step, monkeypatch):
     exp = orc.evalacc_batch(evk, pkey, ct, acc, 8)
     eng = mk.MKAccumulatorEngine(mk.make_params(em, k, n, 2048, Q_MK, q, baseG))
     dg = eng.dg
-    assert eng.step_kernel_name(B + 3) == ("mk_step2_kernel" if step == "2" and dg <= 4 else "mk_step_kernel")
+    names = {"1": "mk_step_kernel", "2": "mk_step2_kernel", "3": "mk_step3_kernel"}
+    assert eng.step_kernel_name(B + 3) == (names[step] if dg <= 4 else "mk_step_kernel")
     eng.upload_keys(evk.astype(np.uint32), pkey.astype(np.uint32))
     got = eng.eval_batch(ct.astype(np.uint32), acc.astype(np.uint32))
     assert np.array_equal(got, exp.astype(np.uint32))

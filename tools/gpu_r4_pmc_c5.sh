@@ -2,6 +2,7 @@
 # round 4: PMC of the config-5 register-resident FP64 step kernel (widereg::step_kernel), one rocprofv3 run per pass
 export TMPDIR=/tmp
 D=gpurun_out/pmc_c5reg_$TAG
+K=${KNAME:-widereg2::step_kernel}
 mkdir -p $D
 i=0
 for CS in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
@@ -13,9 +14,9 @@ for CS in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ
       python3 bench.py --steps 1 --warmup 0 --cpu-baseline 0 --n-override 32 --paramset STD100_MKNTRU --q-bits 50 --stage evalacc \
       > $D/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $D/p$i.log; exit 1; }
 done
-python3 tools/pmc_summary.py $D widereg::step_kernel
+python3 tools/pmc_summary.py $D $K
 # instruction-cache pass (its own run; counter names per the gfx9 SQC block)
 timeout -s KILL 60 rocprofv3 --pmc SQC_ICACHE_REQ SQC_ICACHE_HITS SQC_ICACHE_MISSES -d $D/pic -o run --output-format csv -- \
     python3 bench.py --steps 1 --warmup 0 --cpu-baseline 0 --n-override 32 --paramset STD100_MKNTRU --q-bits 50 --stage evalacc \
     > $D/pic.log 2>&1 || { echo "icache pass failed"; tail -3 $D/pic.log; }
-python3 tools/pmc_summary.py $D widereg::step_kernel | grep SQC || true
+python3 tools/pmc_summary.py $D $K | grep SQC || true

@@ -16,9 +16,11 @@ def bit(p,k): return (p>>k)&1
 # layouts: position p -> (w, l, r)
 def A2(p): return (bit(p,6), p&63, p>>7)
 def B2(p): return (bit(p,10), (p&7)|(bit(p,7)<<3)|(bit(p,8)<<4)|(bit(p,9)<<5), (p>>3)&15)
-def C2(p): return (bit(p,10), bit(p,4)|(bit(p,5)<<1)|(bit(p,6)<<2)|(bit(p,7)<<3)|(bit(p,9)<<4)|(bit(p,8)<<5), p&15)
+def C2(p): return (bit(p,10), bit(p,5)|(bit(p,6)<<1)|(bit(p,9)<<2)|(bit(p,7)<<3)|(bit(p,4)<<4)|(bit(p,8)<<5), p&15)
 def D2(p): return (bit(p,10), (p&15)|(bit(p,8)<<4)|(bit(p,9)<<5), (p>>4)&15)
-L={'A':A2,'B':B2,'C':C2,'D':D2}
+# the 27-bit kernel's EVAL layout (mk_step3_kernel): the one-wave layout C split at slot bit 4
+def C4(p): return (bit(p,4), p>>5, p&15)
+L={'A':A2,'B':B2,'C':C2,'D':D2,'E':C4}
 inv={}
 for n,f in L.items():
     m={}
@@ -26,13 +28,20 @@ for n,f in L.items():
     assert len(m)==N; inv[n]=m
 def pad(p): return p + bit(p,5)*1 + bit(p,6)*2 + bit(p,7)*8 + bit(p,8)*16 + bit(p,9)*36 + bit(p,10)*64
 assert len({pad(p) for p in range(N)})==N and max(pad(p) for p in range(N))==2174
-# bank check: fixed (w, r), half-wave lanes -> distinct pad mod 32
+# bank check, fixed (w, r): each 32-lane half distinct mod 32 (ds_read_b64 / ds_*_b32 lane
+# groups) and, for the 8-byte layouts, each 16-lane group distinct mod 16 (ds_write_b64 and
+# ds_read2/write2_b64 lane groups, banks (a/4) mod 32: MI355X_MICROARCH.md s LDS)
 for n in L:
     for w in range(2):
         for r in range(16):
             for h in range(2):
                 banks=[pad(inv[n][(w,l,r)])%32 for l in range(32*h,32*h+32)]
                 assert len(set(banks))==32, (n,w,r,h)
+            if n == 'E':   # 27-bit words only
+                continue
+            for q in range(4):
+                banks=[pad(inv[n][(w,l,r)])%16 for l in range(16*q,16*q+16)]
+                assert len(set(banks))==16, (n,w,r,q)
 # additivity: pad(p) for layout = base(w,l) + off(r)
 for n in L:
     for w in range(2):
@@ -67,10 +76,10 @@ def FB(w,l,k):   # fwd B2 stage s=4..6, k = (2^(s-4)-1) + (r >> (8-s)); need r b
     r = m << (8-s)                     # register bits above the operated one
     p = pos('B',w,l,r)
     return tw[(1<<s) + (p >> (11-s))]
-def FC(w,l,k):
+def FC(w,l,k,CL='C'):
     s = 7 + (k+1).bit_length()-1; m = k - ((1<<(s-7))-1)
     r = m << (11-s)
-    p = pos('C',w,l,r)
+    p = pos(CL,w,l,r)
     return tw[(1<<s) + (p >> (11-s))]
 def ID(w,l,k):
     b = 4 + (k+1).bit_length()-1; H = 1<<(b-4); m = k-(H-1)
@@ -84,7 +93,7 @@ def IA(w,l,k):
     return pwi[(t << (11-b)) % (2*N)]
 def TW(w,l,k): return pwi[pos('A',w,l,k)] * Ninv % Q
 def bf(a,b,wt): T=b*wt%Q; return (a+T)%Q, (a-T)%Q
-def fwd(vec):
+def fwd(vec, CL='C'):
     X=regs_from('A',vec)
     for w in range(2):
         for l in range(64):
@@ -104,7 +113,7 @@ def fwd(vec):
                     if r&H: continue
                     k=((1<<(s-4))-1)+(r>>(8-s))
                     x[r],x[r+H]=bf(x[r],x[r+H],FB(w,l,k))
-    X=transpose(X,'B','C')
+    X=transpose(X,'B',CL)
     for w in range(2):
         for l in range(64):
             x=X[w][l]
@@ -113,10 +122,10 @@ def fwd(vec):
                 for r in range(16):
                     if r&H: continue
                     k=((1<<(s-7))-1)+(r>>(11-s))
-                    x[r],x[r+H]=bf(x[r],x[r+H],FC(w,l,k))
-    return vec_from('C',X)
-def inv_(vec):
-    X=regs_from('C',vec)
+                    x[r],x[r+H]=bf(x[r],x[r+H],FC(w,l,k,CL))
+    return vec_from(CL,X)
+def inv_(vec, CL='C'):
+    X=regs_from(CL,vec)
     for w in range(2):
         for l in range(64):
             x=X[w][l]
@@ -126,7 +135,7 @@ def inv_(vec):
                     if r&H: continue
                     t=r&(H-1)
                     x[r],x[r+H]=bf(x[r],x[r+H],pwi[(t<<(11-b))])
-    X=transpose(X,'C','D')
+    X=transpose(X,CL,'D')
     for w in range(2):
         for l in range(64):
             x=X[w][l]
@@ -150,14 +159,16 @@ a=[int(v) for v in O.fill_uniform(N,Q,5)]
 e=fwd(a)
 ref=[int(v) for v in O.ntt_forward(np.array(a,dtype=np.uint64),Q,PSI)]
 assert e == ref, "forward transform"
+assert fwd(a, 'E') == ref, "forward transform (27-bit EVAL layout)"
 print("forward transform ok")
 b=inv_(ref)
 assert b == a, "inverse transform"
+assert inv_(ref, 'E') == a, "inverse transform (27-bit EVAL layout)"
 print("inverse transform ok")
 # mono: slot p (C2) exponent e*(2*brv11(p)+1) = e*(2*Lw+1) + ((e*brv4(r))<<8)
 for p in range(N):
     w,l,r=C2(p)
-    Lw = 64*bit(l,0)+32*bit(l,1)+16*bit(l,2)+8*bit(l,3)+2*bit(l,4)+4*bit(l,5)+w
+    Lw = 32*bit(l,0)+16*bit(l,1)+2*bit(l,2)+8*bit(l,3)+64*bit(l,4)+4*bit(l,5)+w
     for e in (1,7,2047,4095):
         assert (e*(2*brv(p,11)+1))%(2*N) == (e*(2*Lw+1) + ((e*brv(r,4))<<8))%(2*N)
 print("mono ok")
