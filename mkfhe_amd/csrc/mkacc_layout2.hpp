@@ -125,4 +125,37 @@ __device__ __forceinline__ void transpose(T (&x)[kR], T* buf, uint32_t l, uint32
     asm volatile("" ::: "memory");
 }
 
+// Transposes between layouts with the same wave bit (LB, LC and LD all have w = p10)
+// stay inside the wave's own half of the buffer (p10 carries W_10 = 1088, every other
+// bit sums to at most 1086): no barrier, and no s_waitcnt either -- a wave's LDS
+// accesses execute in order.  Buffer rule (ping-pong with one barrier per cross-wave
+// transpose, Bufs below): a cross-wave transpose moves to the other buffer, a local
+// one uses the buffer of the latest cross-wave transpose.  Then every write into a
+// region the partner reads is separated from that read by a barrier both waves pass:
+// LA -> LB (partner reads only its own half) may be followed by a local transpose in
+// the same buffer; LD -> LA (partner reads both halves) is always followed by the
+// next transform's LA -> LB, which moves to the other buffer.
+template <int SRC, int DST, typename T>
+__device__ __forceinline__ void transpose_local(T (&x)[kR], T* buf, uint32_t l, uint32_t w) {
+    static_assert(SRC != LA && DST != LA && SRC != LC4 && DST != LC4, "wave-local transposes keep w = p10");
+    T* ws = buf + lbase<SRC>(l, w);
+#pragma unroll
+    for (int r = 0; r < kR; ++r) ws[roff<SRC>(r)] = x[r];
+    asm volatile("" ::: "memory");
+    const T* rs = buf + lbase<DST>(l, w);
+#pragma unroll
+    for (int r = 0; r < kR; ++r) x[r] = rs[roff<DST>(r)];
+    asm volatile("" ::: "memory");
+}
+template <typename T>
+struct Bufs {
+    T* base;
+    uint32_t cb;   // buffer of the latest cross-wave transpose (wave-uniform)
+    __device__ __forceinline__ T* cross() {
+        cb ^= 1u;
+        return base + cb * kBufE;
+    }
+    __device__ __forceinline__ T* cur() const { return base + cb * kBufE; }
+};
+
 }  // namespace lay2

@@ -11,9 +11,9 @@
 // 128-thread workgroup, 16 doubles per lane each, so the per-wave state halves
 // and two waves share a SIMD.
 //
-// A transform is still three register passes and two LDS transposes, now across
-// the gate's two waves (s_barrier of the 2-wave workgroup, two ping-pong buffers
-// so one barrier per transpose).  Position p (11 bits) of a polynomial sits at
+// A transform is still three register passes and two LDS transposes: one across
+// the gate's two waves (s_barrier of the 2-wave workgroup, two ping-pong buffers),
+// one inside each wave's half of the buffer (no barrier; mkacc_layout2.hpp Bufs).  Position p (11 bits) of a polynomial sits at
 // (wave w, lane l, register r) in one of four layouts:
 //   A2  r = p10..p7, w = p6,  l = p5..p0                  coefficients
 //   B2  r = p6..p3,  w = p10, l = (p9, p8, p7, p2, p1, p0)
@@ -55,6 +55,20 @@ using lay2::pos_a;
 using lay2::pos_c;
 using lay2::tload;
 using lay2::transpose;
+using lay2::transpose_local;
+using Bufs = lay2::Bufs<double>;
+// 1: the LB -> LC and LC -> LD transposes stay inside each wave (no barrier); 0 (A/B):
+// every transpose crosses the 2-wave barrier
+#ifndef MKACC_WREG2_LOCAL
+#define MKACC_WREG2_LOCAL 1
+#endif
+template <int SRC, int DST>
+__device__ __forceinline__ void transpose2(double (&x)[kR], Bufs& b, uint32_t l, uint32_t w) {
+    if constexpr (MKACC_WREG2_LOCAL)
+        transpose_local<SRC, DST>(x, b.cur(), l, w);
+    else
+        transpose<SRC, DST>(x, b.cross(), l, w);
+}
 using lay2::TFB;
 using lay2::TFC;
 using lay2::TID;
@@ -140,7 +154,7 @@ __device__ __forceinline__ const_f64* opaque_c(const double* p) {
 // Forward negacyclic NTT (reference EVAL order): coefficients in A2 -> slots in C2.
 //   tws: reference forward table (balanced), wave-uniform indices 1..15
 template <const FPlan& P>
-__device__ __forceinline__ void ntt_fwd(double (&x)[kR], double* bufs, const double* tws, __amdgpu_buffer_rsrc_t rt,
+__device__ __forceinline__ void ntt_fwd(double (&x)[kR], Bufs& bufs, const double* tws, __amdgpu_buffer_rsrc_t rt,
                                         const Lane& ln, const FMod& m) {
     TwPairs<4> fb;
     tload<TFB>(fb, rt, ln.vt);
@@ -154,7 +168,7 @@ __device__ __forceinline__ void ntt_fwd(double (&x)[kR], double* bufs, const dou
             bfly(x[r], x[r + H], tw[(1 << s) + (r >> (4 - s))], m, P.redA[s], P.redB[s]);
         }
     }
-    transpose<LA, LB>(x, bufs, ln.l, ln.w);
+    transpose<LA, LB>(x, bufs.cross(), ln.l, ln.w);
     TwPairs<8> fc;
     tload<TFC>(fc, rt, ln.vt);
 #pragma unroll
@@ -166,7 +180,7 @@ __device__ __forceinline__ void ntt_fwd(double (&x)[kR], double* bufs, const dou
             bfly(x[r], x[r + H], fb.at(((1 << (s - 4)) - 1) + (r >> (8 - s))), m, P.redA[s], P.redB[s]);
         }
     }
-    transpose<LB, LC>(x, bufs + kBufD, ln.l, ln.w);
+    transpose2<LB, LC>(x, bufs, ln.l, ln.w);
 #pragma unroll
     for (int s = 7; s < 11; ++s) {
         const int H = 8 >> (s - 7);
@@ -182,7 +196,7 @@ __device__ __forceinline__ void ntt_fwd(double (&x)[kR], double* bufs, const dou
 // coefficients in A2, |.| <= 2.5 Q.  DIT over the slot bits, twiddle
 // psi^-(t 2^(11-b)) with t = p mod 2^b: bits 0-3 wave-uniform (tis[(1 << b) + t]),
 // bits 4-7 and 8-10 per lane, then x_p *= psi^-p N^-1.
-__device__ __forceinline__ void ntt_inv(double (&x)[kR], double* bufs, const double* tis, __amdgpu_buffer_rsrc_t rt,
+__device__ __forceinline__ void ntt_inv(double (&x)[kR], Bufs& bufs, const double* tis, __amdgpu_buffer_rsrc_t rt,
                                         const Lane& ln, const FMod& m) {
     TwPairs<8> id;
     tload<TID>(id, rt, ln.vt);
@@ -207,7 +221,7 @@ __device__ __forceinline__ void ntt_inv(double (&x)[kR], double* bufs, const dou
         if (kInv1.redOut[r]) x[r] = red(x[r], m);
     TwPairs<7> ia;
     tload<TIA>(ia, rt, ln.vt);
-    transpose<LC, LD>(x, bufs, ln.l, ln.w);
+    transpose2<LC, LD>(x, bufs, ln.l, ln.w);
 #pragma unroll
     for (int b = 4; b < 8; ++b) {
         const int H = 1 << (b - 4);
@@ -219,7 +233,7 @@ __device__ __forceinline__ void ntt_inv(double (&x)[kR], double* bufs, const dou
     }
     TwPairs<8> tt;
     tload<TTW>(tt, rt, ln.vt);
-    transpose<LD, LA>(x, bufs + kBufD, ln.l, ln.w);
+    transpose<LD, LA>(x, bufs.cross(), ln.l, ln.w);
 #pragma unroll
     for (int b = 8; b < 11; ++b) {
         const int H = 1 << (b - 7);
@@ -341,7 +355,7 @@ __device__ __forceinline__ void mac(const double (&g)[kR], double (&uj)[kR], dou
 // iNTT(x) -> offset words -> per digit: NTT, MAC (widereg::digits_pass)
 template <int METHOD, bool FIRST, bool F>
 __device__ __forceinline__ void digits_pass(double (&x)[kR], double (&uj)[kR], double (&sv)[kR], const double (&mn)[kR],
-                                            const double (&mcv)[kR], const StepArgs& a, double* bufs,
+                                            const double (&mcv)[kR], const StepArgs& a, Bufs& bufs,
                                             __amdgpu_buffer_rsrc_t rt, const Lane& ln, const KeySrc& ks0, uint32_t u) {
     const FMod& m = a.m;
     constexpr uint32_t polyB = kN * 8u;
@@ -384,7 +398,7 @@ __device__ __forceinline__ void digits_pass(double (&x)[kR], double (&uj)[kR], d
 // xzw.cpp:292-381; parties index + 1, ..., index, the index party's sum kept for
 // the f-part).
 template <int METHOD, bool FIRST>
-__device__ __forceinline__ void one_gate(const StepArgs& a, uint32_t gate, double* bufs, const Lane& ln) {
+__device__ __forceinline__ void one_gate(const StepArgs& a, uint32_t gate, Bufs& bufs, const Lane& ln) {
     const FMod& m = a.m;
     const uint32_t k = a.k, index = a.index;
     const uint32_t c = __builtin_amdgcn_readfirstlane(a.cvals[gate]);
@@ -439,7 +453,8 @@ __global__ __launch_bounds__(128, 2) void step_kernel(StepArgs a) {
     const uint32_t l = threadIdx.x & 63u;
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const Lane ln{l, w, (w * 64u + l) * 16u};
-    for (uint32_t gate = blockIdx.x; gate < a.B; gate += gridDim.x) one_gate<METHOD, FIRST>(a, gate, smem, ln);
+    Bufs bufs{smem, 0u};
+    for (uint32_t gate = blockIdx.x; gate < a.B; gate += gridDim.x) one_gate<METHOD, FIRST>(a, gate, bufs, ln);
 }
 
 // primitive kernels for parity tests: one polynomial per 2-wave workgroup, canonical
@@ -453,7 +468,8 @@ __global__ __launch_bounds__(128, 2) void ntt_fwd_kernel(const uint64_t* __restr
     double x[kR];
 #pragma unroll
     for (int r = 0; r < kR; ++r) x[r] = widefp::balanced(src[pos_a(w, l, r)], m);
-    ntt_fwd<kFwd>(x, smem, twf, make_rsrc(tab, kTabD * 8u), ln, m);
+    Bufs bufs{smem, 0u};
+    ntt_fwd<kFwd>(x, bufs, twf, make_rsrc(tab, kTabD * 8u), ln, m);
 #pragma unroll
     for (int r = 0; r < kR; ++r) out[(size_t)blockIdx.x * kN + pos_c(w, l, r)] = widefp::canon(x[r], m);
 }
@@ -466,7 +482,8 @@ __global__ __launch_bounds__(128, 2) void ntt_inv_kernel(const uint64_t* __restr
     double x[kR];
 #pragma unroll
     for (int r = 0; r < kR; ++r) x[r] = widefp::balanced(src[pos_c(w, l, r)], m);
-    ntt_inv(x, smem, tis, make_rsrc(tab, kTabD * 8u), ln, m);
+    Bufs bufs{smem, 0u};
+    ntt_inv(x, bufs, tis, make_rsrc(tab, kTabD * 8u), ln, m);
 #pragma unroll
     for (int r = 0; r < kR; ++r) out[(size_t)blockIdx.x * kN + pos_a(w, l, r)] = widefp::canon(x[r], m);
 }

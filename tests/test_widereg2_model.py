@@ -16,7 +16,7 @@ def test_widereg2_model_matches_oracle():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "widereg2_model.py")], capture_output=True,
                        text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
-    for line in ("layouts ok", "forward transform ok", "inverse transform ok", "mono ok"):
+    for line in ("layouts ok", "forward transform ok", "inverse transform ok", "mono ok", "buffer schedule ok"):
         assert line in r.stdout
 
 

@@ -5,7 +5,10 @@ word map (injective, additive in every bit, and conflict-free: the 32 lanes of
 every half-wave hit 32 distinct bank pairs in every layout), the per-lane twiddle
 indexing of every pass, and the monomial exponent split -- the forward and
 inverse transform pair run on (wave, lane, register) arrays and must equal the
-oracle's NTT (reference order).  Test infrastructure: imports oracle/ only.
+oracle's NTT (reference order) -- for the FP64 kernel's EVAL layout and the 27-bit
+kernel's (mk_step3_kernel) -- and the two-buffer LDS schedule with a barrier only in
+the cross-wave transposes is checked race-free over a sequence of gate-steps.
+Test infrastructure: imports oracle/ only.
 usage: python3 tools/widereg2_model.py      (about a minute)"""
 import sys, numpy as np
 import os
@@ -172,3 +175,37 @@ for p in range(N):
     for e in (1,7,2047,4095):
         assert (e*(2*brv(p,11)+1))%(2*N) == (e*(2*Lw+1) + ((e*brv(r,4))<<8))%(2*N)
 print("mono ok")
+# ---- buffer schedule of widereg2::step_kernel (mkacc_layout2.hpp Bufs): two ping-pong
+# buffers, a barrier only in the cross-wave transposes (LA <-> LB / LD), the local ones
+# (LB -> LC, LC -> LD: w = p10 on both sides) in the buffer of the latest cross-wave one.
+# Every pair of accesses by different waves to one LDS element, at least one a write,
+# must be ordered the way the program means it: the earlier transpose's access (or, in
+# one transpose, the write) in an earlier barrier epoch than the later one.
+def addr_set(lay, w):
+    return {pad(p) for p in range(N) if L[lay](p)[0] == w}
+def schedule(ntrans):
+    seq = []
+    for t in ntrans:   # 'i' inverse (local C->D, cross D->A), 'f' forward (cross A->B, local B->C)
+        seq += [('C', 'D', False), ('D', 'A', True)] if t == 'i' else [('A', 'B', True), ('B', 'C', False)]
+    cb, ops, epoch = 0, {0: [], 1: []}, 0
+    for ti, (src, dst, cross) in enumerate(seq):
+        if cross:
+            cb ^= 1
+        for w in (0, 1):
+            ops[w].append((ti, 0, 'W', cb, addr_set(src, w), epoch))
+        if cross:
+            epoch += 1
+        for w in (0, 1):
+            ops[w].append((ti, 1, 'R', cb, addr_set(dst, w), epoch))
+    return ops
+def check_schedule(ntrans):
+    ops = schedule(ntrans)
+    for a in ops[0]:
+        for b in ops[1]:
+            if a[3] != b[3] or 'W' not in (a[2], b[2]) or not (a[4] & b[4]):
+                continue
+            first, second = (a, b) if (a[0], a[1]) < (b[0], b[1]) else (b, a)
+            assert first[5] < second[5], ("LDS race", first[:4], second[:4])
+check_schedule('i' + 'f' * 4 + 'i' + 'f' * 4 + 'i' + 'f' * 4 + 'i' + 'f' * 4)   # two gates at k = 2, dg = 4
+check_schedule('ififf')
+print("buffer schedule ok")
