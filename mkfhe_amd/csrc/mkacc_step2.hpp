@@ -85,6 +85,14 @@ struct VecLd<1> {
     }
 };
 
+// MKACC_S2_NXPF / MKACC_S2_NXAT: the accumulator copy of mac2 (below)
+#ifndef MKACC_S2_NXPF
+#define MKACC_S2_NXPF 0
+#endif
+#ifndef MKACC_S2_NXAT
+#define MKACC_S2_NXAT 5
+#endif
+
 // Key-stream shape of one pass.  kGS slots per load group (C4 layout: slot r of
 // lane l at byte (r >> 2) * 1024 + l * 16 + (r & 3) * 4), kPf groups in flight.
 template <int DG, int METHOD, bool FIRST>
@@ -119,6 +127,18 @@ struct Step2Cfg {
     __device__ __forceinline__ static constexpr uint32_t soff(int g) {
         return (uint32_t)(((g * kGS) >> 2) * 1024 + ((g * kGS) & 3) * 4);
     }
+    // MKACC_S2_NXPF: vector memory ops a party stream issues after its accumulator copies
+    // (group MKACC_S2_NXAT): that group's store, then per later group its key loads
+    // (if any) and its store
+    static constexpr int kLoadsPerGroup = DG * (1 + (kK2 ? 1 : 0) + (FIRST ? 1 : 0) + 1) + (FIRST ? 0 : 1) +
+                                          (kSvMem ? 1 : 0);
+    static constexpr int young() {
+        int n = 1 + (kSvMem ? 1 : 0);
+        for (int g = MKACC_S2_NXAT + 1; g < kGroups; ++g) n += (g + kPf < kGroups ? kLoadsPerGroup : 0) + 1 + (kSvMem ? 1 : 0);
+        return n;
+    }
+    static constexpr int kNxYoung = young();
+    static_assert(!MKACC_S2_NXPF || (MKACC_S2_NXAT < kGroups && kNxYoung <= 63), "accumulator copy placement");
     // redc bound (units of Q^2, below 32): digit-NTT outputs < kG Q, canonical keys,
     // plus a 32-bit start value in [0, 2Q) times 2^32 mod Q (< 2 Q^2)
     static constexpr int kG = DG > 4 ? 2 : 4;
@@ -148,9 +168,15 @@ struct Grp2 {
 //                        sv is returned in registers and also stored)
 //   F = true  (f-part):  keys f-half (2i + 1); start = acc_out[index] (the index
 //                        party's output); out -> acc_out[index]
+// MKACC_S2_NXPF=1 (A/B): a party pass also copies the NEXT pass's accumulator (party
+// nu) from HBM straight into the wave's LDS transpose scratch (idle during the key
+// stream) with direct-to-LDS buffer loads, so the next pass reads it from LDS instead
+// of starting with an exposed HBM load, and no VGPR is spent (prefetching it into
+// registers spilled 53-60 VGPRs).  The last party reloads its own, L2-resident, words
+// (no branch in the stream); every pass waits for the copies before its first transform.
 template <int DG, int METHOD, bool FIRST, bool F>
 __device__ __forceinline__ void mac2(const StepCtx& s, uint32_t u, const uint32_t (&G)[DG][kRegs],
-                                     uint32_t (&sv)[kRegs], uint32_t svf = 0) {
+                                     uint32_t (&sv)[kRegs], uint32_t svf = 0, uint32_t nu = 0) {
     using C = Step2Cfg<DG, METHOD, FIRST>;
     using L = VecLd<C::kGS>;
     using Grp = Grp2<DG, METHOD, FIRST>;
@@ -184,6 +210,13 @@ __device__ __forceinline__ void mac2(const StepCtx& s, uint32_t u, const uint32_
 #pragma unroll
     for (int g = 0; g < C::kGroups; ++g) {
         if (g + C::kPf < C::kGroups) issue(kg[(g + C::kPf) % C::kBuf], g + C::kPf);
+        if (MKACC_S2_NXPF && !F && g == MKACC_S2_NXAT) {
+#pragma unroll
+            for (int gq = 0; gq < 8; ++gq)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    s.rin, (__attribute__((address_space(3))) void*)(s.lds + gq * 256), 16, vo,
+                    nu * polyB + gq * 1024u, 0, 0);
+        }
         const Grp& t = kg[g % C::kBuf];
         typename L::T ov;
 #pragma unroll
@@ -447,10 +480,24 @@ __global__ __launch_bounds__(64 * kS2Waves, 4 * s2_waves_per_simd<DG>() / kS2Wav
         const uint32_t u = MKACC_S2_ORDER ? (index + 1 + t < k ? index + 1 + t : index + 1 + t - k) : t;
         uint32_t x[kRegs];
         if (!fpart) {
+            if (MKACC_S2_NXPF && !s2_halves<DG>() && t > 0) {
+                // copied into this wave's scratch by the previous pass's stream (C4 order):
+                // wait for those copies only -- the stream issued kNxYoung memory ops after them
+                // (vector memory returns in issue order)
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(Step2Cfg<DG, METHOD, FIRST>::kNxYoung) : "memory");
+                const u32x4* q = reinterpret_cast<const u32x4*>(s.lds);
 #pragma unroll
-            for (int gq = 0; gq < 8; ++gq) {
-                const u32x4 v = aload4(s.rin, s.vo, u * polyB + gq * 1024u);
-                x[4 * gq] = v.x; x[4 * gq + 1] = v.y; x[4 * gq + 2] = v.z; x[4 * gq + 3] = v.w;
+                for (int gq = 0; gq < 8; ++gq) {
+                    const u32x4 v = q[gq * 64 + s.l];
+                    x[4 * gq] = v.x; x[4 * gq + 1] = v.y; x[4 * gq + 2] = v.z; x[4 * gq + 3] = v.w;
+                }
+                asm volatile("" ::: "memory");
+            } else {
+#pragma unroll
+                for (int gq = 0; gq < 8; ++gq) {
+                    const u32x4 v = aload4(s.rin, s.vo, u * polyB + gq * 1024u);
+                    x[4 * gq] = v.x; x[4 * gq + 1] = v.y; x[4 * gq + 2] = v.z; x[4 * gq + 3] = v.w;
+                }
             }
             if (!FIRST) {
                 // acctemp = acc * (X^c - 1)                 (xzw.cpp:336-338)
@@ -507,10 +554,15 @@ __global__ __launch_bounds__(64 * kS2Waves, 4 * s2_waves_per_simd<DG>() / kS2Wav
             uint32_t G[DG][kRegs];
             digit_ntts<DG>(s, x, G);
             vcc_fence();   // the MAC branch follows the last butterflies
+            // next pass: party u + 1 (mod k), or u itself after the last party (unused)
+            const uint32_t nu = t + 1 < k ? (u + 1 < k ? u + 1 : 0u) : u;
             if (!fpart)
-                mac2<DG, METHOD, FIRST, false>(s, u, G, sv, t == 0 ? 0u : s.m.r32);
+                mac2<DG, METHOD, FIRST, false>(s, u, G, sv, t == 0 ? 0u : s.m.r32, nu);
             else
                 mac2<DG, METHOD, FIRST, true>(s, index, G, sv);
         }
+        // the f-part is the last pass: no back edge from it, so nothing a party
+        // pass leaves for the next one (xn) is live across the f-part's transforms
+        if (fpart) break;
     }
 }
