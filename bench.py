@@ -416,7 +416,8 @@ def run_rank(args, env: dict, make_engine, make_checker, torch_device: str, back
                        "reference's KATs, the EvalAcc composition is 'parity unpinned' beyond them (DESIGN.md s3)"),
             "roofline": {"bound": "hbm", "achieved": by / pl / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": by / pl / 1e9 / PEAK_HBM_GBS,
-                         "traffic": measured_traffic(args.paramset, kname) if not (args.n_override or wide) else None,
+                         "traffic": (measured_traffic(args.paramset + ("_q50" if args.q_bits == 50 else ""), kname)
+                                     if not args.n_override else None),
                          "kernel": kname,
                          "per_launch_us": pl * 1e6,
                          "bytes_per_launch": by},

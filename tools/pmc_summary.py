@@ -7,7 +7,7 @@ agg = collections.defaultdict(float); cnt = collections.Counter()
 for f in sorted(glob.glob(f"{d}/**/*counter_collection.csv", recursive=True)):
     for r in csv.DictReader(open(f)):
         # the later steps only: skip the FIRST instantiation (<DG, METHOD, true, ...>)
-        if pat not in r["Kernel_Name"] or re.search(r"<\d+, \d+, true", r["Kernel_Name"]):
+        if pat not in r["Kernel_Name"] or re.search(r"<(\d+, )+true", r["Kernel_Name"]):
             continue
         agg[r["Counter_Name"]] += float(r["Counter_Value"]); cnt[r["Counter_Name"]] += 1
 for k in sorted(agg):
