@@ -483,15 +483,32 @@ __global__ __launch_bounds__(64 * kS2Waves, 4 * s2_waves_per_simd<DG>() / kS2Wav
             if (MKACC_S2_NXPF && !s2_halves<DG>() && t > 0) {
                 // copied into this wave's scratch by the previous pass's stream (C4 order):
                 // wait for those copies only -- the stream issued kNxYoung memory ops after them
-                // (vector memory returns in issue order)
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(Step2Cfg<DG, METHOD, FIRST>::kNxYoung) : "memory");
-                const u32x4* q = reinterpret_cast<const u32x4*>(s.lds);
+                // (vector memory returns in issue order).  The reads are inline asm: for a
+                // compiled LDS read after LDS-DMA writes hipcc inserts s_waitcnt vmcnt(0),
+                // i.e. waits for every store of the previous stream as well.
+                // (the lane term recomputed here, opaque to hoisting: a loop-invariant address
+                // kept live across the pass was the one VGPR the kernel spilled)
+                const uint32_t la = (uint32_t)(size_t)(__attribute__((address_space(3))) char*)(s.lds) + opaque_v(s.l) * 16u;
+                u32x4 v0, v1, v2, v3, v4, v5, v6, v7;
+                asm volatile(
+                    "s_waitcnt vmcnt(%8)\n\t"
+                    "ds_read_b128 %0, %9\n\t"
+                    "ds_read_b128 %1, %9 offset:1024\n\t"
+                    "ds_read_b128 %2, %9 offset:2048\n\t"
+                    "ds_read_b128 %3, %9 offset:3072\n\t"
+                    "ds_read_b128 %4, %9 offset:4096\n\t"
+                    "ds_read_b128 %5, %9 offset:5120\n\t"
+                    "ds_read_b128 %6, %9 offset:6144\n\t"
+                    "ds_read_b128 %7, %9 offset:7168\n\t"
+                    "s_waitcnt lgkmcnt(0)"
+                    : "=&v"(v0), "=&v"(v1), "=&v"(v2), "=&v"(v3), "=&v"(v4), "=&v"(v5), "=&v"(v6), "=&v"(v7)
+                    : "n"(Step2Cfg<DG, METHOD, FIRST>::kNxYoung), "v"(la)
+                    : "memory");
+                const u32x4 vv[8] = {v0, v1, v2, v3, v4, v5, v6, v7};
 #pragma unroll
                 for (int gq = 0; gq < 8; ++gq) {
-                    const u32x4 v = q[gq * 64 + s.l];
-                    x[4 * gq] = v.x; x[4 * gq + 1] = v.y; x[4 * gq + 2] = v.z; x[4 * gq + 3] = v.w;
+                    x[4 * gq] = vv[gq].x; x[4 * gq + 1] = vv[gq].y; x[4 * gq + 2] = vv[gq].z; x[4 * gq + 3] = vv[gq].w;
                 }
-                asm volatile("" ::: "memory");
             } else {
 #pragma unroll
                 for (int gq = 0; gq < 8; ++gq) {
