@@ -386,6 +386,16 @@ def run_rank(args, env: dict, make_engine, make_checker, torch_device: str, back
         pl = per_launch_s or float("nan")
         wide_fp = wide and getattr(eng, "wide_fp", False)
         kname = eng.step_kernel_name(B) if hasattr(eng, "step_kernel_name") else "mk_step_kernel"
+        # the engine cuts a batch of >= 2 units of (CUs x 4) gates into MKACC_STREAMS (default 2)
+        # slices whose step launches run concurrently on streams of their own
+        # (mkacc_engine.hip launch_steps / wide_launch_batch): one accumulator step of the
+        # batch is then `slices` launches, and per_launch_us is the time of one such step
+        slices = 1
+        if is_cuda and kname in ("mk_step_kernel", "mk_step2_kernel", "mk_step3_kernel", "widereg2::step_kernel"):
+            import torch
+            cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+            ev = os.environ.get("MKACC_STREAMS", "")
+            slices = max(1, min(int(ev) if ev in ("1", "2", "3", "4") else 2, B // (cus * 4)))
         peak_mm, peak_src = ((PEAK_FP64_MULMOD_TPS, "exact FP64 product, profiles/r2/ubench_wide.txt") if wide_fp else
                              (PEAK_INT64_MULMOD_TPS, "64-bit Shoup product, profiles/r2/ubench_wide.txt") if wide else
                              (PEAK_SHOUP_MULMOD_TPS, "27-bit Shoup product, profiles/round1_ubench_intops.txt"))
@@ -420,7 +430,11 @@ def run_rank(args, env: dict, make_engine, make_checker, torch_device: str, back
                                      if not args.n_override else None),
                          "kernel": kname,
                          "per_launch_us": pl * 1e6,
-                         "bytes_per_launch": by},
+                         "bytes_per_launch": by,
+                         "slices_per_step": slices,
+                         "launch_note": ("one accumulator step of the whole batch: " + (
+                             f"{slices} concurrent launches of {B // slices}+ gates on {slices} streams; rocprof lists each "
+                             "slice launch with its own (overlapping) duration" if slices > 1 else "one launch"))},
             # VALU view: algorithmic mod-muls per launch against the measured rate of the
             # product the kernel is built on (32-bit Shoup; FP64 or 64-bit Shoup on the wide path)
             "roofline_valu": {

@@ -216,6 +216,11 @@ struct mkacc_ctx {
     uint32_t ninv = 0, ninvp = 0, nval = 0, nvalp = 0;
     uint32_t kscale = 0, kscalep = 0;   // key words: N^-1 2^32 mod Q and its companion
     hipStream_t stream = nullptr;
+    // step chains of batch slices on streams of their own (launch_steps)
+    static constexpr int kMaxStreams = 4;
+    int nstreams = 1;
+    hipStream_t xs[kMaxStreams - 1] = {};   // extra streams
+    hipEvent_t ev_fork = nullptr, ev_join[kMaxStreams - 1] = {};
     uint2* d_twf = nullptr;
     uint2* d_twi = nullptr;
     uint32_t* d_img = nullptr;    // LDS image: per-lane twiddles + psi table
@@ -350,57 +355,108 @@ int ensure_ws(mkacc_ctx* c, size_t B) {
 // The k*n accumulator steps over a batch whose monomial exponents are in
 // d_cvals and whose C4 accumulators are in d_acc0; returns the buffer holding
 // the result (nullptr if the build has no kernel for the context's digit count).
+// Gates [g0, g0 + Bh) of a batch of B on stream st: the k*n accumulator steps, one
+// launch per step() call, ping-ponging between d_acc0 and d_acc1 at this half's offset.
+struct StepChain {
+    mkacc_ctx* c;
+    size_t B, g0, Bh, ao;
+    hipStream_t st;
+    uint32_t* cur;
+    uint32_t* nxt;
+    bool lat;
+    StepChain(mkacc_ctx* c_, size_t B_, size_t g0_, size_t Bh_, hipStream_t st_)
+        : c(c_), B(B_), g0(g0_), Bh(Bh_), ao(g0_ * c_->p.k * kN), st(st_), cur(c_->d_acc0 + ao), nxt(c_->d_acc1 + ao),
+          lat(use_lat(c_, Bh_)) {}
+    // one accumulator step (u, i); false if the build has no kernel for it
+    bool step(uint32_t u, uint32_t i, size_t lds) {
+        const uint32_t k = c->p.k, n = c->p.n;
+        const bool first = (u == 0 && i == 0);
+        StepArgs a;
+        a.acc_in = cur;
+        a.acc_out = nxt;
+        a.cvals = c->d_cvals + ((size_t)u * n + i) * B + g0;
+        a.key1 = key_step(c, u, i, 0);
+        a.key2 = c->nk == 2 ? key_step(c, u, i, 1) : a.key1;
+        a.keys = key_step(c, 0, n, 0);
+        a.pkey = c->d_pkey;
+        a.tw_fwd = c->d_twf;
+        a.tw_inv = c->d_twi;
+        a.img = c->d_img;
+        a.B = (uint32_t)Bh;
+        a.k = k;
+        a.index = u;
+        a.m = c->mod;
+        a.sd = c->sd;
+        a.dscr = c->d_dscr ? c->d_dscr + g0 * step_scratch_words(c) : nullptr;
+        a.tab3 = c->d_tab3;
+        // a null kernel must never reach hipLaunchKernelGGL (mkacc_create checks the set)
+        if (lat) {
+            const void* fn = lat_fn((int)c->dg, c->method_class, first);
+            if (!fn) return false;
+            launch_ptr(fn, dim3((unsigned)Bh), dim3(64 * k), lat_lds_bytes(k), st, a);
+        } else {
+            const void* fn = step_fn((int)c->dg, c->method_class, first, !first && use_dscr(c), c->step_ver);
+            if (!fn) return false;
+            if (c->step_ver == 3)   // one 2-wave workgroup per gate
+                launch_ptr(fn, dim3((unsigned)Bh), dim3(128), s3::kLdsBytes + (lds - kStepLdsBytes), st, a);
+            else if (c->step_ver == 2)
+                launch_ptr(fn, dim3((unsigned)((Bh + kS2Waves - 1) / kS2Waves)), dim3(64 * kS2Waves),
+                           kStep2LdsBytes + (lds - kStepLdsBytes), st, a);
+            else
+                launch_ptr(fn, dim3((unsigned)((Bh + kWavesPerBlock - 1) / kWavesPerBlock)), dim3(kThreads), lds, st,
+                           a);
+        }
+        std::swap(cur, nxt);
+        return true;
+    }
+    uint32_t* result() const { return cur - ao; }   // the full-batch buffer holding the result
+};
+
+// The k*n accumulator steps over a batch whose monomial exponents are in
+// d_cvals and whose C4 accumulators are in d_acc0; returns the buffer holding
+// the result (nullptr if the build has no kernel for the context's digit count).
+// A batch of at least two units of cus x 4 gates (one 4-gate workgroup per CU, half
+// a round of resident gates) is cut into up to nstreams slices of whole units
+// (MKACC_STREAMS, default 2), each slice's launches
+// on a stream of its own, enqueued step by step and forked after / joined before
+// the main stream's work.  Gates are independent, so the slices need no other
+// ordering, and one slice's next launch takes the CUs another slice's tail leaves
+// idle: STD128_MKNTRU 238.4 -> 211.1 ms per batch, STD128_MKNTRU_3 7.27 -> 6.65 s
+// (profiles/r4/ab_streams.txt).
 uint32_t* launch_steps(mkacc_ctx* c, size_t B) {
     const uint32_t k = c->p.k, n = c->p.n;
-    uint32_t* cur = c->d_acc0;
-    uint32_t* nxt = c->d_acc1;
-    const dim3 grid((unsigned)((B + kWavesPerBlock - 1) / kWavesPerBlock)), block(kThreads);
     // MKACC_DBG_LDS=<bytes> (diagnosis, tools/dbg/determ2.py): extra dynamic LDS per
     // workgroup; 10240 leaves one workgroup per CU, the co-residency reference
     const char* dl = std::getenv("MKACC_DBG_LDS");
     const size_t lds = kStepLdsBytes + (dl ? std::strtoul(dl, nullptr, 0) : 0);
-    const bool lat = use_lat(c, B);
-    for (uint32_t u = 0; u < k; ++u) {
-        for (uint32_t i = 0; i < n; ++i) {
-            const bool first = (u == 0 && i == 0);
-            StepArgs a;
-            a.acc_in = cur;
-            a.acc_out = nxt;
-            a.cvals = c->d_cvals + ((size_t)u * n + i) * B;
-            a.key1 = key_step(c, u, i, 0);
-            a.key2 = c->nk == 2 ? key_step(c, u, i, 1) : a.key1;
-            a.keys = key_step(c, 0, n, 0);
-            a.pkey = c->d_pkey;
-            a.tw_fwd = c->d_twf;
-            a.tw_inv = c->d_twi;
-            a.img = c->d_img;
-            a.B = (uint32_t)B;
-            a.k = k;
-            a.index = u;
-            a.m = c->mod;
-            a.sd = c->sd;
-            a.dscr = c->d_dscr;
-            a.tab3 = c->d_tab3;
-            // a null kernel must never reach hipLaunchKernelGGL (mkacc_create checks the set)
-            if (lat) {
-                const void* fn = lat_fn((int)c->dg, c->method_class, first);
-                if (!fn) return nullptr;
-                launch_ptr(fn, dim3((unsigned)B), dim3(64 * k), lat_lds_bytes(k), c->stream, a);
-            } else {
-                const void* fn = step_fn((int)c->dg, c->method_class, first, !first && use_dscr(c), c->step_ver);
-                if (!fn) return nullptr;
-                if (c->step_ver == 3)   // one 2-wave workgroup per gate
-                    launch_ptr(fn, dim3((unsigned)B), dim3(128), s3::kLdsBytes + (lds - kStepLdsBytes), c->stream, a);
-                else if (c->step_ver == 2)
-                    launch_ptr(fn, dim3((unsigned)((B + kS2Waves - 1) / kS2Waves)), dim3(64 * kS2Waves),
-                               kStep2LdsBytes + (lds - kStepLdsBytes), c->stream, a);
-                else
-                    launch_ptr(fn, grid, block, lds, c->stream, a);
-            }
-            std::swap(cur, nxt);
-        }
+    const size_t unit = (size_t)c->cus * 4;
+    const size_t ns = std::min<size_t>((size_t)c->nstreams, B / unit);
+    if (ns < 2) {
+        StepChain ch(c, B, 0, B, c->stream);
+        for (uint32_t u = 0; u < k; ++u)
+            for (uint32_t i = 0; i < n; ++i)
+                if (!ch.step(u, i, lds)) return nullptr;
+        return ch.result();
     }
-    return cur;
+    // slices of whole units, the remainder in the last one
+    const size_t per = (B / unit / ns) * unit;
+    if (hipEventRecord(c->ev_fork, c->stream) != hipSuccess) return nullptr;
+    std::vector<StepChain> ch;
+    ch.reserve(ns);
+    for (size_t j = 0; j < ns; ++j) {
+        hipStream_t st = j == 0 ? c->stream : c->xs[j - 1];
+        if (j > 0 && hipStreamWaitEvent(st, c->ev_fork, 0) != hipSuccess) return nullptr;
+        ch.emplace_back(c, B, j * per, j + 1 < ns ? per : B - j * per, st);
+    }
+    for (uint32_t u = 0; u < k; ++u)
+        for (uint32_t i = 0; i < n; ++i)
+            for (auto& h : ch)
+                if (!h.step(u, i, lds)) return nullptr;
+    for (size_t j = 1; j < ns; ++j)
+        if (hipEventRecord(c->ev_join[j - 1], c->xs[j - 1]) != hipSuccess ||
+            hipStreamWaitEvent(c->stream, c->ev_join[j - 1], 0) != hipSuccess)
+            return nullptr;
+    return ch[0].result();
 }
 
 void launch_prep_c(mkacc_ctx* c, const uint32_t* d_ct, size_t B) {
@@ -680,6 +736,21 @@ int prim_launch(mkacc_ctx* c, const uint32_t* in, uint32_t* out, size_t count, s
 
 // ---- 64-bit word path (mkacc_wide.hpp) --------------------------------------------
 
+// MKACC_STREAMS=1..4 (default 2): the streams of the batch slices (launch_steps,
+// wide_launch_batch)
+hipError_t create_slice_streams(mkacc_ctx* c) {
+    const char* e = std::getenv("MKACC_STREAMS");
+    const int ns = e && e[0] >= '1' && e[0] <= '4' && !e[1] ? e[0] - '0' : 2;
+    hipError_t r = hipSuccess;
+    if (ns > 1 && (r = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming)) != hipSuccess) return r;
+    for (int j = 0; j + 1 < ns; ++j) {
+        if ((r = hipStreamCreateWithFlags(&c->xs[j], hipStreamNonBlocking)) != hipSuccess) return r;
+        if ((r = hipEventCreateWithFlags(&c->ev_join[j], hipEventDisableTiming)) != hipSuccess) return r;
+    }
+    c->nstreams = ns;
+    return r;
+}
+
 int wide_setup(mkacc_ctx* c) {
     using u128 = unsigned __int128;
     const uint64_t Q = c->p.Q;
@@ -916,15 +987,26 @@ int wide_launch_batch(mkacc_ctx* c, const uint32_t* d_ct, const uint64_t* d_in, 
         hipLaunchKernelGGL(widereg2::to_c16_kernel, g, dim3(256), 0, c->stream, d_in, cur, words, c->wfm, c->p.Q,
                            c->d_bad);
         auto dk = [](const uint64_t* p) { return reinterpret_cast<const double*>(p); };
-        // four 2-wave workgroups per CU, looping over the batch
-        const size_t wgs = std::min<size_t>(B, (size_t)c->cus * 4);
+        // four 2-wave workgroups per CU, each looping over its slice of the batch; a
+        // batch of at least two units of cus x 4 gates is cut into slices on streams of
+        // their own, as launch_steps does for the 27-bit kernels
+        const size_t unit = (size_t)c->cus * 4;
+        const size_t ns = std::max<size_t>(1, std::min<size_t>((size_t)c->nstreams, B / unit));
+        const size_t per = ns > 1 ? (B / unit / ns) * unit : B;
+        if (ns > 1) {
+            HIP_TRY(hipEventRecord(c->ev_fork, c->stream));
+            for (size_t j = 1; j < ns; ++j) HIP_TRY(hipStreamWaitEvent(c->xs[j - 1], c->ev_fork, 0));
+        }
         for (uint32_t u = 0; u < k; ++u)
-            for (uint32_t i = 0; i < n; ++i) {
+            for (uint32_t i = 0; i < n; ++i)
+            for (size_t j = 0; j < ns; ++j) {
+                const size_t g0 = j * per, Bh = j + 1 < ns ? per : B - g0;
+                const size_t ao = g0 * k * kN;
                 const bool first = (u == 0 && i == 0);
                 widereg2::StepArgs a;
-                a.acc_in = cur;
-                a.acc_out = nxt;
-                a.cvals = c->d_wcvals + ((size_t)u * n + i) * B;
+                a.acc_in = cur + ao;
+                a.acc_out = nxt + ao;
+                a.cvals = c->d_wcvals + ((size_t)u * n + i) * B + g0;
                 a.key1 = dk(key(u, i, 0));
                 a.key2 = dk(c->nk == 2 ? key(u, i, 1) : key(u, i, 0));
                 a.keys = dk(key(0, n, 0));
@@ -933,7 +1015,7 @@ int wide_launch_batch(mkacc_ctx* c, const uint32_t* d_ct, const uint64_t* d_in, 
                 a.psi = c->d_fpsi;
                 a.twf = c->d_ftwf;
                 a.tis = c->d_rtis;
-                a.B = (uint32_t)B;
+                a.B = (uint32_t)Bh;
                 a.k = k;
                 a.index = u;
                 a.dg = c->dg;
@@ -941,10 +1023,15 @@ int wide_launch_batch(mkacc_ctx* c, const uint32_t* d_ct, const uint64_t* d_in, 
                 a.Cm = c->wfCm;
                 a.m = c->wfm;
                 a.sd = c->wsd;
-                launch_ptr(mkacc_tu::widereg2_step(c->method_class, first), dim3((unsigned)wgs), dim3(128),
-                           widereg2::kLdsBytes, c->stream, a);
-                std::swap(cur, nxt);
+                launch_ptr(mkacc_tu::widereg2_step(c->method_class, first),
+                           dim3((unsigned)std::min<size_t>(Bh, unit)), dim3(128), widereg2::kLdsBytes,
+                           j == 0 ? c->stream : c->xs[j - 1], a);
+                if (j + 1 == ns) std::swap(cur, nxt);
             }
+        for (size_t j = 1; j < ns; ++j) {
+            HIP_TRY(hipEventRecord(c->ev_join[j - 1], c->xs[j - 1]));
+            HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_join[j - 1], 0));
+        }
         hipLaunchKernelGGL(widereg2::from_c16_kernel, g, dim3(256), 0, c->stream, cur, d_out, words, c->wfm);
         HIP_TRY(hipGetLastError());
         return MKACC_OK;
@@ -1262,6 +1349,7 @@ int mkacc_create(const mkacc_params* pin, int device, mkacc_ctx** out) {
     if (wide) {
         HIP_TRY(hipSetDevice(device));
         HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        HIP_TRY(create_slice_streams(c.get()));
         HIP_TRY(hipMalloc(&c->d_bad, 8));   // [0] batch inputs, [1] device key upload
         HIP_TRY(hipMemset(c->d_bad, 0, 8));
         const int rc = wide_setup(c.get());
@@ -1302,6 +1390,7 @@ int mkacc_create(const mkacc_params* pin, int device, mkacc_ctx** out) {
 
     HIP_TRY(hipSetDevice(device));
     HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIP_TRY(create_slice_streams(c.get()));
     HIP_TRY(hipMalloc(&c->d_bad, 8));   // [0] batch inputs, [1] device key upload
     HIP_TRY(hipMemset(c->d_bad, 0, 8));
     // forward NTT table in the reference's order (transformnat-impl.h:705-760),
@@ -1408,6 +1497,11 @@ void mkacc_destroy(mkacc_ctx* c) {
                     (void*)c->d_wacc1, (void*)c->d_wcvals, (void*)c->d_wct, (void*)c->d_wio, (void*)c->d_bad})
         if (p) (void)hipFree(p);
     if (c->stream) (void)hipStreamDestroy(c->stream);
+    for (int j = 0; j < mkacc_ctx::kMaxStreams - 1; ++j) {
+        if (c->xs[j]) (void)hipStreamDestroy(c->xs[j]);
+        if (c->ev_join[j]) (void)hipEventDestroy(c->ev_join[j]);
+    }
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     delete c;
 }
 

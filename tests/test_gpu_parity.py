@@ -251,3 +251,29 @@ def test_evalacc_many_gates_every_wave_slot(mk, oracle, lat, monkeypatch):
         got = eng.eval_batch(ct.astype(np.uint32), acc.astype(np.uint32))
         bad = [g for g in range(B) if not np.array_equal(got[g], exp[g])]
         assert not bad, f"gates differing from the oracle: {bad[:16]}"
+
+
+@pytest.mark.parametrize("streams", ["2", "3", "4"])
+@pytest.mark.parametrize("step", ["1", "2"])
+def test_two_stream_batch_split(mk, oracle, step, streams, monkeypatch):
+    """MKACC_STREAMS=2..4 cuts a batch of two or more units of resident gates into
+    slices whose step launches run on streams of their own: the output equals the
+    one-stream run word for word, and a spread sample across the slices equals the
+    oracle.  B = 4100 (units of 1024 gates at 256 CUs): 2048 + 2052, 1024 + 1024 +
+    2052, 1024 x 3 + 1028."""
+    monkeypatch.setenv("MKACC_STEP", step)
+    monkeypatch.setenv("MKACC_LAT", "0")
+    k, n, q, baseG, B = 2, 3, 45181, 1 << 9, 4100
+    orc, evk, pkey, ct, acc = make_case(oracle, oracle.XZW, k, n, q, baseG, B, seed=91 + int(step))
+    params = mk.make_params(mk.MKNTRU, k, n, 2048, Q_MK, q, baseG)
+    outs = {}
+    for ns in ("1", streams):
+        monkeypatch.setenv("MKACC_STREAMS", ns)
+        eng = mk.MKAccumulatorEngine(params)
+        eng.upload_keys(evk.astype(np.uint32), pkey.astype(np.uint32))
+        outs[ns] = eng.eval_batch(ct.astype(np.uint32), acc.astype(np.uint32))
+        del eng
+    assert np.array_equal(outs["1"], outs[streams])
+    pick = [0, 1, 1023, 1024, 2047, 2048, 3071, 3072, 4099]
+    exp = orc.evalacc_batch(evk, pkey, ct[pick], acc[pick], 8)
+    assert np.array_equal(outs[streams][pick], exp.astype(np.uint32))
