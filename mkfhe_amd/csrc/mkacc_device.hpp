@@ -59,8 +59,10 @@ __device__ __forceinline__ u32x2 bload2(__amdgpu_buffer_rsrc_t r, uint32_t voff,
 // the NEXT group's values for part of the wave (lanes 12-15 of each row), the
 // wrong-result "race" of round 1.  The s_nop sits between scheduling barriers
 // so nothing is moved into the gap.  tools/isa_audit.py checks every build.
+// AUX: cache-policy bits of the store (0 = default policy)
+template <int AUX = 0>
 __device__ __forceinline__ void bstore4(u32x4 v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-    __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, soff, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, soff, AUX);
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_nop 1");
     __builtin_amdgcn_sched_barrier(0);

@@ -232,8 +232,17 @@ template <int DG>
 #endif
 struct Prefetch { static constexpr int value = DG <= 3 ? MKACC_PF3 : 0; };
 // accumulator loads: each gate's own rows, written by the previous step launch
+// (A/B switches: cache-policy bits of mk_step_kernel's accumulator loads / stores and of
+// its d_i scratch loads / stores; 0 = the default policy)
+#ifndef MKACC_ACC_AUX
+#define MKACC_ACC_AUX 0
+#endif
+#ifndef MKACC_DS_AUX
+#define MKACC_DS_AUX 0
+#endif
+template <int AUX = 0>
 __device__ __forceinline__ u32x4 aload4(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-    return __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
+    return __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, AUX);
 }
 // key-block loads (shared by every gate of the launch, streamed from L2)
 __device__ __forceinline__ u32x4 kload4(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
@@ -295,13 +304,13 @@ struct DigitMac {
     __device__ __forceinline__ void issue(KeyGroup& t, int gq) const {
         const uint32_t go = gq * 1024u;
         if (DS == 2)
-            t.k1 = aload4(sr.rds, sr.vo, doff + go);   // d_i of the first party pass
+            t.k1 = aload4<MKACC_DS_AUX>(sr.rds, sr.vo, doff + go);   // d_i of the first party pass
         else
             t.k1 = kload4(sr.rk1, sr.vo, koff + go);
         t.pk = kload4(sr.rpk, sr.vo, poff + go);
         if (METHOD == XZW && DS != 2) t.k2 = kload4(sr.rk2, sr.vo, koff + go);
         if (FIRST) t.ks = kload4(sr.rks, sr.vo, koff + go);
-        if (kAcc) t.acc = aload4(sr.rin, sr.vo, aoff + go);
+        if (kAcc) t.acc = aload4<MKACC_ACC_AUX>(sr.rin, sr.vo, aoff + go);
         if (kMonoPf) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) t.mono[e] = sr.mn.at(sr.psi, 4 * gq + e);
@@ -327,7 +336,7 @@ struct DigitMac {
                 uj[r] = mad64(g[r], deff, base);
                 sv[r] = mad64(g[r], t.pk[e], sv[r]);
             }
-            if (DS == 1) bstore4(dv, sr.rds, sr.vo, doff + gq * 1024u);
+            if (DS == 1) bstore4<MKACC_DS_AUX>(dv, sr.rds, sr.vo, doff + gq * 1024u);
             sched_fence();
         }
     }
@@ -428,7 +437,7 @@ __device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_
     uint32_t x[kRegs];
 #pragma unroll
     for (int gq = 0; gq < 8; ++gq) {
-        const u32x4 t = aload4(s.rin, s.vo, u * polyB + gq * 1024u);
+        const u32x4 t = aload4<MKACC_ACC_AUX>(s.rin, s.vo, u * polyB + gq * 1024u);
         x[4 * gq] = t.x; x[4 * gq + 1] = t.y; x[4 * gq + 2] = t.z; x[4 * gq + 3] = t.w;
     }
     if (!FIRST) {
@@ -485,7 +494,7 @@ __device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_
 #pragma unroll
     for (int gq = 0; gq < 8; ++gq) {
         u32x4 t;
-        if constexpr (!Bd::kAccInSum && !FIRST) t = aload4(s.rin, s.vo, u * polyB + gq * 1024u);
+        if constexpr (!Bd::kAccInSum && !FIRST) t = aload4<MKACC_ACC_AUX>(s.rin, s.vo, u * polyB + gq * 1024u);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const int r = 4 * gq + e;
@@ -496,7 +505,7 @@ __device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_
             }
             t[e] = v;
         }
-        bstore4(t, s.rout, s.vo, u * polyB + gq * 1024u);
+        bstore4<MKACC_ACC_AUX>(t, s.rout, s.vo, u * polyB + gq * 1024u);
     }
 }
 
@@ -673,7 +682,7 @@ __device__ __forceinline__ void f_part(const StepCtx& s, uint32_t index, uint64_
         // acc[index] joins the f-part sum (Bounds: < 4 Q^2 with the folded party sum)
 #pragma unroll
         for (int gq = 0; gq < 8; ++gq) {
-            const u32x4 t = aload4(s.rin, s.vo, index * polyB + gq * 1024u);
+            const u32x4 t = aload4<MKACC_ACC_AUX>(s.rin, s.vo, index * polyB + gq * 1024u);
 #pragma unroll
             for (int e = 0; e < 4; ++e) w[4 * gq + e] = mad64(t[e], s.m.r32, w[4 * gq + e]);
         }
@@ -733,7 +742,7 @@ __device__ __forceinline__ void f_part(const StepCtx& s, uint32_t index, uint64_
             }
             t[e] = v;
         }
-        bstore4(t, s.rout, s.vo, ioff + gq * 1024u);
+        bstore4<MKACC_ACC_AUX>(t, s.rout, s.vo, ioff + gq * 1024u);
     }
 }
 
