@@ -113,6 +113,9 @@ def parse(argv=None):
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: every usable host core")
     ap.add_argument("--check-gates", type=int, default=0,
                     help="gates per rank recomputed by the oracle (0: one per host core at N=1, 2 per rank at N>1)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="N=1: oracle CPU work (threads x wall seconds) of the cpu_baseline sample; more gates of "
+                         "the timed batch are recomputed (and parity-checked) until it is reached")
     ap.add_argument("--q-bits", type=int, default=0, choices=[0, 50],
                     help="50: config 5 stress -- the paramset's shape with the 50-bit Q = 1125899906826241 and "
                          "B_g = 2^10 in 64-bit words (EvalAcc on the 64-bit word path)")
@@ -347,30 +350,50 @@ def run_rank(args, env: dict, make_engine, make_checker, torch_device: str, back
     G = max(1, min(G, B))
     idx = np.unique(np.round(np.linspace(0, B - 1, G)).astype(np.int64))
     G = len(idx)
-    idx_d = torch.as_tensor(idx, device=torch_device)
     threads = args.cpu_threads or (cpu["usable"] if world == 1 else max(1, min(G, cpu["usable"] // world)))
     chk = make_checker(p, lwe)
     keys_h = keys.cpu().numpy().view(np.uint64 if word == 8 else np.uint32)
     evk_h = keys_h[:evk_n].astype(np.uint64).reshape(eng.evk_shape)
     pkey_h = keys_h[evk_n:].astype(np.uint64).reshape(eng.pkey_shape)
     del keys
-    t_c = time.perf_counter()
     if stage == "gate":
-        sub = {key: (v[idx] if key != "nand" else v) for key, v in h.items()}
         ksk_h = ksk_d.cpu().numpy().view(np.uint32)   # the checker's host copy, after the timed region
         del ksk_d
         ksk64 = ((ksk_h[:na].astype(np.uint64), ksk_h[na:].astype(np.uint64)) if lwe else ksk_h)
-        exp_a, exp_b = chk.gates((evk_h, pkey_h), ksk64, sub, threads, (qKS, baseKS, n_out))
-        dt_c = time.perf_counter() - t_c
-        got_a = d_oa[idx_d].cpu().numpy().view(np.uint32).astype(np.uint64)
-        bad = np.any((got_a != exp_a.reshape(got_a.shape)).reshape(G, -1), axis=1)
-        if lwe:
-            bad |= d_ob[idx_d].cpu().numpy().view(np.uint32).astype(np.uint64) != exp_b
-    else:
-        exp = chk.evalacc(evk_h, pkey_h, ct_h[idx].astype(np.uint64), acc_h[idx].astype(np.uint64), threads)
-        dt_c = time.perf_counter() - t_c
-        got = d_out[idx_d].cpu().numpy().view(np.uint64 if word == 8 else np.uint32).astype(np.uint64)
-        bad = np.any((got != exp).reshape(G, -1), axis=1)
+
+    def check(idx):
+        """oracle recomputation of gates idx of the timed batch: (mismatch per gate, wall s)"""
+        idx_d = torch.as_tensor(idx, device=torch_device)
+        n = len(idx)
+        t_c = time.perf_counter()
+        if stage == "gate":
+            sub = {key: (v[idx] if key != "nand" else v) for key, v in h.items()}
+            exp_a, exp_b = chk.gates((evk_h, pkey_h), ksk64, sub, threads, (qKS, baseKS, n_out))
+            dt = time.perf_counter() - t_c
+            got_a = d_oa[idx_d].cpu().numpy().view(np.uint32).astype(np.uint64)
+            bad = np.any((got_a != exp_a.reshape(got_a.shape)).reshape(n, -1), axis=1)
+            if lwe:
+                bad |= d_ob[idx_d].cpu().numpy().view(np.uint32).astype(np.uint64) != exp_b
+        else:
+            exp = chk.evalacc(evk_h, pkey_h, ct_h[idx].astype(np.uint64), acc_h[idx].astype(np.uint64), threads)
+            dt = time.perf_counter() - t_c
+            got = d_out[idx_d].cpu().numpy().view(np.uint64 if word == 8 else np.uint32).astype(np.uint64)
+            bad = np.any((got != exp).reshape(n, -1), axis=1)
+        return bad, dt
+
+    bad, dt_c = check(idx)
+    # the CPU baseline's sample: at N = 1 more gates of the batch (evenly spread, not yet
+    # checked) until the oracle has done about --cpu-seconds of CPU work (threads x wall);
+    # they are parity-checked too
+    if world == 1 and args.cpu_baseline and not args.check_gates and G < B and dt_c > 0:
+        per_gate_cpu = dt_c * threads / G
+        more = int(np.ceil(max(0.0, args.cpu_seconds - dt_c * threads) / per_gate_cpu / threads)) * threads
+        more = min(more, B - G, 64 * threads)
+        if more > 0:
+            rest = np.setdiff1d(np.arange(B, dtype=np.int64), idx)
+            idx2 = rest[np.unique(np.round(np.linspace(0, len(rest) - 1, more)).astype(np.int64))]
+            bad2, dt2 = check(idx2)
+            bad, dt_c, G = np.concatenate([bad, bad2]), dt_c + dt2, G + len(idx2)
     counts = torch.tensor([G, int(bad.sum())], dtype=torch.int64, device=torch_device)
     if world > 1:
         dist.all_reduce(counts, op=dist.ReduceOp.SUM)
@@ -449,7 +472,8 @@ def run_rank(args, env: dict, make_engine, make_checker, torch_device: str, back
             result["cpu_baseline"] = {
                 "value": G / dt_c, "unit": "bootstraps/s", "cores": threads, "kind": chk.kind,
                 "sample": (f"{G} {what} spread over the timed batch ({p.k}x{p.n} accumulator steps each), one per "
-                           f"thread on {threads} threads, {dt_c:.2f} s wall; the same gates are the parity check"),
+                           f"thread at a time on {threads} threads, {dt_c:.2f} s wall ({dt_c * threads:.1f} thread-s); the same gates "
+                           "are the parity check"),
                 "host": cpu,
                 "reference_1core_s_per_evalacc": ref,
                 "oracle_over_reference_1core": ORACLE_OVER_REF.get(args.paramset) if ref else None,

@@ -42,3 +42,21 @@ def test_bench_fails_on_a_wrong_gate_of_rank_1():
     assert r.returncode != 0
     assert res is not None and res["parity_checked"] == 4 and res["parity_mismatches"] == 1
     assert "parity FAILED" in r.stderr
+
+
+def test_bench_n1_cpu_baseline_sample_grows_to_cpu_seconds():
+    """N = 1: the cpu_baseline sample (and parity check) is extended with more gates of the
+    timed batch until the oracle did --cpu-seconds of CPU work (the stub is instant, so the
+    whole 64-gate batch is taken)."""
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--stub-engine", "--batch", "64",
+           "--steps", "2", "--warmup", "1", "--n-override", "4", "--cpu-threads", "4"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert res["parity_checked"] == 64 and res["parity_mismatches"] == 0
+    assert res["cpu_baseline"]["cores"] == 4 and "64 NAND gates" in res["cpu_baseline"]["sample"]
+    r2 = subprocess.run(cmd + ["--cpu-seconds", "0"], capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    res2 = json.loads([ln for ln in r2.stdout.splitlines() if ln.startswith("{")][-1])
+    assert res2["parity_checked"] < 64   # one gate per usable core, not extended
