@@ -429,9 +429,16 @@ struct StepCtx {
 //   sv  += sum_i NTT(g_i) * P[u][i]
 // Party `index` is processed last (LAST): its lazy sum stays in registers
 // (`uj`, folded) and receives the f-part of HbProd before the single store.
+// MKACC_DSCR_ALT (default 1; 0 = A/B control): d_i reload passes (DS = 2) alternate the order of digits
+// 1..DG-1 (rev: DG-1 down to 1), so a pass starts its reloads with the digit the
+// previous pass read last (shorter reuse distance of the scratch lines in L2).
+// Every digit's products are the same exact lazy sums in another order: bit-exact.
+#ifndef MKACC_DSCR_ALT
+#define MKACC_DSCR_ALT 1
+#endif
 template <int DG, int METHOD, bool FIRST, bool LAST, int DS = 0>
 __device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_t (&sv)[kRegs],
-                                           uint64_t (&uj)[kRegs]) {
+                                           uint64_t (&uj)[kRegs], bool rev = false) {
     using Bd = Bounds<DG, METHOD, FIRST>;
     const uint32_t Q = s.m.Q, polyB = kN * 4u;
     uint32_t x[kRegs];
@@ -474,9 +481,10 @@ __device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_
     }
 #pragma unroll 1
     for (int i = 1; i < DG; ++i) {
+        const int j = (MKACC_DSCR_ALT && DS == 2 && rev) ? DG - i : i;
 #pragma unroll
-        for (int r = 0; r < kRegs; ++r) x[r] = pd.get(r, i + 1, s.sd);
-        const DigitMac<DG, METHOD, FIRST, false, DS> mac(sr, i, u);
+        for (int r = 0; r < kRegs; ++r) x[r] = pd.get(r, j + 1, s.sd);
+        const DigitMac<DG, METHOD, FIRST, false, DS> mac(sr, j, u);
         KeyGroup kg[mac.kBuf];
         ntt_fwd(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, s.l, Q, s.m.m1);
         digit_range<DG>(x, Q);
@@ -659,10 +667,11 @@ __device__ __forceinline__ void step_body(const StepCtx& s, uint32_t k, uint32_t
         if (!MKACC_DSCR_WAIT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     for (uint32_t t = t0; t < k; ++t) {
-        party_pass<DG, METHOD, FIRST, false, DSCR ? 2 : 0>(s, index + t < k ? index + t : index + t - k, sv, w);
+        party_pass<DG, METHOD, FIRST, false, DSCR ? 2 : 0>(s, index + t < k ? index + t : index + t - k, sv, w,
+                                                           (t & 1u) == 0);
         grow_sv();
     }
-    party_pass<DG, METHOD, FIRST, true, DSCR ? 2 : 0>(s, index, sv, w);
+    party_pass<DG, METHOD, FIRST, true, DSCR ? 2 : 0>(s, index, sv, w, (k & 1u) == 0);
     uint32_t x[kRegs];
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) x[r] = redc(sv[r], Q, s.m.qinv);
