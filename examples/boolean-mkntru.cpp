@@ -5,7 +5,9 @@
 //
 //   g++ -std=c++17 -O2 -Iinclude examples/boolean-mkntru.cpp -Lmkfhe_amd/lib
 //       -lmkfhe_amd -lmkfhe_keys -Wl,-rpath,$PWD/mkfhe_amd/lib -o boolean-mkntru
-//   ./boolean-mkntru [STD100_MKNTRU|STD128_MKNTRU|...] [--replay]
+//   ./boolean-mkntru [STD100_MKNTRU|STD128_MKNTRU|...] [--replay] [--resample]
+//   --resample: MKBTKeyGen under RDefectPolicy::RESAMPLE (redraw a key whose DggR sample r is
+//   nonzero; the default keeps the reference's keys, defect included)
 //   --replay: record the seed-0 entropy master so a run with a wrong gate can be
 //   replayed (prints it on failure; whoever holds it holds every key of the run)
 #include <cstdio>
@@ -26,10 +28,12 @@ static BINFHE_PARAMSET parse(const char* s) {
 
 int main(int argc, char** argv) {
     const char* set = nullptr;
-    bool replay = false;
+    bool replay = false, resample = false;
     for (int i = 1; i < argc; ++i) {
         if (!strcmp(argv[i], "--replay"))
             replay = true;
+        else if (!strcmp(argv[i], "--resample"))
+            resample = true;
         else
             set = argv[i];
     }
@@ -43,7 +47,7 @@ int main(int argc, char** argv) {
     cout << "Generating sk" << endl;
     auto sk = cc.MNTRU_KeyGen();
     std::cout << "Generating the bootstrapping keys..." << std::endl;
-    cc.MKBTKeyGen(sk);
+    cc.MKBTKeyGen(sk, resample ? RDefectPolicy::RESAMPLE : RDefectPolicy::KEEP);
     if (cc.GetRDefects())   // the reference's KeyGenXZW r-defect (mk-acc-xzw.cpp:160-167), reported here
         std::cout << "warning: " << cc.GetRDefects()
                   << " bootstrapping key(s) drew a nonzero DggR sample r; gates using them may decrypt wrong "

@@ -166,12 +166,14 @@ __device__ __forceinline__ uint32_t mul_shoup_lazy(uint32_t x, uint2 w, uint32_t
 // (digit_range), effective key words from key_eff < kD Q, and the previous
 // accumulator joins the party sum as acc * (2^32 mod Q) < 2 Q^2 when it fits
 // (kAccInSum), otherwise it is added after the reduction.
-template <int DG, int METHOD, bool FIRST>
+// CANON: the party sum's d-words are canonical (< Q): the d_i scratch reloads with
+// MKACC_DS_CANON (party_pass).
+template <int DG, int METHOD, bool FIRST, bool CANON = false>
 struct Bounds {
     static constexpr int kG = DG > 4 ? 2 : 4;
     static constexpr int kD = DG * kG * 3 + 2 <= 32 ? 3 : (DG * kG * 2 <= 32 ? 2 : 1);
     // the d-words the party sums actually see: XZW_B steps after the first use ev1 itself
-    static constexpr int kDSum = (METHOD == XZW_B && !FIRST) ? 1 : kD;
+    static constexpr int kDSum = ((METHOD == XZW_B && !FIRST) || CANON) ? 1 : kD;
     static constexpr bool kAccInSum = !FIRST && DG * kG * kDSum + 2 <= 32;
     static_assert(DG * kG * kDSum + (kAccInSum ? 2 : 0) <= 32, "party sum bound");
     // sumV gains DG * kG per party (pkey canonical); fold64 leaves < 2
@@ -275,9 +277,17 @@ struct StepRes {
 // party of the step, so the first party pass computes it and stores it to the
 // gate's HBM scratch (DS = 1) and the later passes load it (DS = 2) instead of
 // the ev1'/ev2 words and the psi^e - 1 gathers; DS = 0 computes it per party.
-template <int DG, int METHOD, bool FIRST, bool START, int DS = 0>
+// MKACC_DS_CANON (default 2; 0 = A/B control) >= 1: the first pass stores the d_i scratch canonical (< Q), so the
+// reload passes other than the index party's (CANON) fit the previous accumulator into
+// the party sum (Bounds::kAccInSum at dg = 4): acc_u is read again at digit 0, shortly
+// after the rotation read, instead of after the last digit.  >= 2: the first pass sums
+// the canonical words too (CANON there as well).
+#ifndef MKACC_DS_CANON
+#define MKACC_DS_CANON 2
+#endif
+template <int DG, int METHOD, bool FIRST, bool START, int DS = 0, bool CANON = false>
 struct DigitMac {
-    using Bd = Bounds<DG, METHOD, FIRST>;
+    using Bd = Bounds<DG, METHOD, FIRST, CANON>;
     static_assert(DS == 0 || (METHOD == XZW && !FIRST), "d_i scratch: XZW steps after the first");
     static constexpr bool kAcc = START && Bd::kAccInSum;
     // MKACC_MONO_PF=0 (A/B): gather X^(N-c) - 1 at use instead of with the key group
@@ -331,9 +341,10 @@ struct DigitMac {
                     DS == 2 ? t.k1[e]
                     : kMonoPf ? from3q<Bd::kD>(t.k1[e] + mul_shoup_lazy(t.k2[e], t.mono[e], Q), Q)   // = key_eff
                               : key_eff<METHOD, FIRST, Bd::kD>(t.k1[e], t.k2[e], t.ks[e], sr.psi, sr.mp, sr.mn, r, Q);
-                dv[e] = deff;
+                const uint32_t dc = (DS == 1 && MKACC_DS_CANON) ? from3q<1>(deff, Q) : deff;
+                dv[e] = dc;
                 const uint64_t base = kAcc ? mad64(t.acc[e], sr.m.r32, 0) : (START ? 0ull : uj[r]);
-                uj[r] = mad64(g[r], deff, base);
+                uj[r] = mad64(g[r], (DS == 1 && CANON) ? dc : deff, base);
                 sv[r] = mad64(g[r], t.pk[e], sv[r]);
             }
             if (DS == 1) bstore4<MKACC_DS_AUX>(dv, sr.rds, sr.vo, doff + gq * 1024u);
@@ -439,7 +450,8 @@ struct StepCtx {
 template <int DG, int METHOD, bool FIRST, bool LAST, int DS = 0>
 __device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_t (&sv)[kRegs],
                                            uint64_t (&uj)[kRegs], bool rev = false) {
-    using Bd = Bounds<DG, METHOD, FIRST>;
+    constexpr bool kCanon = !LAST && ((MKACC_DS_CANON >= 1 && DS == 2) || (MKACC_DS_CANON >= 2 && DS == 1));
+    using Bd = Bounds<DG, METHOD, FIRST, kCanon>;
     const uint32_t Q = s.m.Q, polyB = kN * 4u;
     uint32_t x[kRegs];
 #pragma unroll
@@ -468,7 +480,7 @@ __device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_
     }
     const StepRes sr = s.res();
     {
-        const DigitMac<DG, METHOD, FIRST, true, DS> mac(sr, 0, u);
+        const DigitMac<DG, METHOD, FIRST, true, DS, kCanon> mac(sr, 0, u);
         KeyGroup kg[mac.kBuf];
         ntt_fwd(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, s.l, Q, s.m.m1);
         digit_range<DG>(x, Q);
@@ -484,7 +496,7 @@ __device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_
         const int j = (MKACC_DSCR_ALT && DS == 2 && rev) ? DG - i : i;
 #pragma unroll
         for (int r = 0; r < kRegs; ++r) x[r] = pd.get(r, j + 1, s.sd);
-        const DigitMac<DG, METHOD, FIRST, false, DS> mac(sr, j, u);
+        const DigitMac<DG, METHOD, FIRST, false, DS, kCanon> mac(sr, j, u);
         KeyGroup kg[mac.kBuf];
         ntt_fwd(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, s.l, Q, s.m.m1);
         digit_range<DG>(x, Q);

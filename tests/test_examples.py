@@ -39,5 +39,12 @@ def test_example_builds(name):
 def test_example_runs(name, ps):
     r = subprocess.run([_build(name), ps], capture_output=True, text=True, timeout=300)
     print(r.stdout)
+    if r.returncode != 0 and "drew a nonzero DggR sample" in r.stdout:
+        # the reference's key-generation defect (mk-acc-xzw.cpp:160-167), reproduced bit-faithfully
+        # and reported by the example: fresh keys of this run are defective (a few per thousand
+        # key sets), not the engine.  The truth table is then checked on resampled keys.
+        r = subprocess.run([_build(name), ps, "--resample"], capture_output=True, text=True, timeout=300)
+        print(r.stdout)
+        assert "drew a nonzero DggR sample" not in r.stdout
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.count("Result of encrypted computation") == 4
