@@ -281,7 +281,8 @@ struct StepRes {
 // reload passes other than the index party's (CANON) fit the previous accumulator into
 // the party sum (Bounds::kAccInSum at dg = 4): acc_u is read again at digit 0, shortly
 // after the rotation read, instead of after the last digit.  >= 2: the first pass sums
-// the canonical words too (CANON there as well).
+// the canonical words too (CANON there as well).  >= 3 (A/B): the index party's pass
+// as well, whose sum then carries acc[index] into the f-part (f_part ACC_DONE).
 #ifndef MKACC_DS_CANON
 #define MKACC_DS_CANON 2
 #endif
@@ -450,7 +451,8 @@ struct StepCtx {
 template <int DG, int METHOD, bool FIRST, bool LAST, int DS = 0>
 __device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_t (&sv)[kRegs],
                                            uint64_t (&uj)[kRegs], bool rev = false) {
-    constexpr bool kCanon = !LAST && ((MKACC_DS_CANON >= 1 && DS == 2) || (MKACC_DS_CANON >= 2 && DS == 1));
+    constexpr bool kCanon = (!LAST || MKACC_DS_CANON >= 3) &&
+                            ((MKACC_DS_CANON >= 1 && DS == 2) || (MKACC_DS_CANON >= 2 && DS == 1));
     using Bd = Bounds<DG, METHOD, FIRST, kCanon>;
     const uint32_t Q = s.m.Q, polyB = kN * 4u;
     uint32_t x[kRegs];
@@ -531,7 +533,7 @@ __device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_
 
 template <int DG, int METHOD, bool FIRST, bool DSCR>
 __device__ __forceinline__ void step_body(const StepCtx& s, uint32_t k, uint32_t index);
-template <int DG, int METHOD, bool FIRST>
+template <int DG, int METHOD, bool FIRST, bool ACC_DONE = false>
 __device__ __forceinline__ void f_part(const StepCtx& s, uint32_t index, uint64_t (&w)[kRegs], uint32_t (&x)[kRegs]);
 
 // DSCR: d_i computed once per step and gate (first party pass) and reloaded from
@@ -687,19 +689,20 @@ __device__ __forceinline__ void step_body(const StepCtx& s, uint32_t k, uint32_t
     uint32_t x[kRegs];
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) x[r] = redc(sv[r], Q, s.m.qinv);
-    f_part<DG, METHOD, FIRST>(s, index, w, x);
+    f_part<DG, METHOD, FIRST, MKACC_DS_CANON >= 3 && DSCR && Bounds<DG, METHOD, FIRST, true>::kAccInSum>(s, index, w, x);
 }
 
 // Second half of HbProd for party `index` (mk-acc-xzw.cpp:272-289) and the
 // final store of acc[index]: w = its folded party sum (party_pass LAST),
 // x = sumV in [0, 2Q).  iNTT(sumV) -> SDD -> NTT -> acc[index] += <., f>.
-template <int DG, int METHOD, bool FIRST>
+// ACC_DONE: the index party's sum already holds acc[index] (party_pass LAST with CANON)
+template <int DG, int METHOD, bool FIRST, bool ACC_DONE>
 __device__ __forceinline__ void f_part(const StepCtx& s, uint32_t index, uint64_t (&w)[kRegs], uint32_t (&x)[kRegs]) {
     using Bd = Bounds<DG, METHOD, FIRST>;
     const uint32_t Q = s.m.Q;
     const uint32_t l = s.l;
     const uint32_t polyB = kN * 4u;
-    if constexpr (!Bd::kAccInSum && !FIRST) {
+    if constexpr (!Bd::kAccInSum && !FIRST && !ACC_DONE) {
         // acc[index] joins the f-part sum (Bounds: < 4 Q^2 with the folded party sum)
 #pragma unroll
         for (int gq = 0; gq < 8; ++gq) {
