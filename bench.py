@@ -57,16 +57,23 @@ Q50 = 1125899906826241               # config 5 stress modulus (SURVEY.md s0 ite
 REF_CPU_S_PER_EVALACC = {            # reference EvalAcc, 1 core of the survey container
     "STD100_MKNTRU": 0.274, "STD128_MKNTRU": 0.475, "STD100_MKNTRU_LWE": 0.215,
     "STD100_MKNTRU_LWE_2": 0.721, "STD128_MKNTRU_3": 6.750, "STD100_MKNTRU_3": 2.872}
-# oracle / reference single-thread EvalAcc time (tools/oracle_calib.py,
-# profiles/r3/ and profiles/r4/oracle_calibration.json).  A CROSS-MACHINE estimate: the
-# oracle was timed on this repo's Intel Xeon (AVX-512) container, the reference by the
-# survey on an 8-vCPU AMD EPYC container; the reference cannot be rebuilt here to time
-# both on one CPU.  Repeat runs of the oracle side vary by ~15 %.
-ORACLE_OVER_REF = {"STD128_MKNTRU": 0.566, "STD100_MKNTRU": 0.575, "STD100_MKNTRU_LWE_2": 0.460,
-                   "STD100_MKNTRU_3": 0.447, "STD128_MKNTRU_3": 0.432}
-CALIBRATION = {"same_machine": False, "oracle_cpu": "Intel Xeon (AVX-512), this repo's build container",
-               "reference_cpu": "8-vCPU AMD EPYC, the survey's probe container (SURVEY.md s6)",
-               "record": "profiles/r4/oracle_calibration.json"}
+# oracle / reference single-thread EvalAcc time, read from the calibration record
+# (tools/oracle_calib.py -> profiles/r4/oracle_calibration.json).  A
+# CROSS-MACHINE estimate: the oracle was timed on this repo's Intel Xeon (AVX-512)
+# container, the reference by the survey on an 8-vCPU AMD EPYC container; the reference
+# cannot be rebuilt here to time both on one CPU.
+CALIBRATION_RECORD = "profiles/r4/oracle_calibration.json"
+
+
+def oracle_over_ref() -> dict:
+    rec = json.load(open(os.path.join(ROOT, CALIBRATION_RECORD)))
+    return {k: v["oracle_over_reference"] for k, v in rec.items() if isinstance(v, dict) and "oracle_over_reference" in v}
+
+
+def calibration() -> dict:
+    rec = json.load(open(os.path.join(ROOT, CALIBRATION_RECORD)))
+    return {"same_machine": rec.get("same_machine", False), "oracle_cpu": rec.get("oracle_cpu"),
+            "reference_cpu": rec.get("reference_cpu"), "record": CALIBRATION_RECORD}
 
 
 def algorithmic_counts(k: int, n: int, dg: int, nk: int, N: int = 2048, B: int = 1, word: int = 4):
@@ -87,18 +94,33 @@ def algorithmic_counts(k: int, n: int, dg: int, nk: int, N: int = 2048, B: int =
     return mulmods, bytes_
 
 
-def measured_traffic(paramset: str, kernel: str):
+def library_kernel_ids() -> dict:
+    """{demangled kernel: isa id} of the engine library this process runs
+    (mkfhe_amd/build.py writes it next to the library, tools/kernel_isa.py)."""
+    from mkfhe_amd import _lib
+    f = _lib.LIB_PATH[:-3] + ".kernel_isa.json"
+    return json.load(open(f)) if os.path.exists(f) else {}
+
+
+def measured_traffic(paramset: str, kernel: str, algorithmic: float) -> dict:
     """Per-launch HBM bytes of the step kernel from the committed PMC record
     (profiles/traffic_<paramset>.json, written by tools/pmc_summary.py from
-    separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes), or None -- also
-    when the record was taken of another step kernel than the one benched."""
+    separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes).  `bytes` is None
+    unless the record was taken of this very kernel: same name, and the same
+    machine code (isa id) as the kernel in the library being benched."""
     f = os.path.join(ROOT, "profiles", f"traffic_{paramset}.json")
     if not os.path.exists(f):
-        return None
+        return {"bytes": None, "why": f"no record profiles/traffic_{paramset}.json"}
     rec = json.load(open(f))
-    if rec.get("kernel", "mk_step_kernel") != kernel:
-        return None
-    return rec["traffic_bytes"]
+    if rec.get("kernel") != kernel:
+        return {"bytes": None, "why": f"record is of {rec.get('kernel')}, benched kernel is {kernel}"}
+    sym, isa = rec.get("kernel_symbol"), rec.get("kernel_isa")
+    have = library_kernel_ids().get(sym) if sym else None
+    if not isa or have != isa:
+        return {"bytes": None, "why": f"record's kernel isa id {isa} differs from the library's {have} ({sym})"}
+    t = rec["traffic_bytes"]
+    return {"bytes": t, "over_algorithmic": t / algorithmic, "kernel_symbol": sym, "kernel_isa": isa,
+            "record": f"profiles/traffic_{paramset}.json", "pmc_source": rec.get("source")}
 
 
 def parse(argv=None):
@@ -419,6 +441,8 @@ def run_rank(args, env: dict, make_engine, make_checker, torch_device: str, back
             cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
             ev = os.environ.get("MKACC_STREAMS", "")
             slices = max(1, min(int(ev) if ev in ("1", "2", "3", "4") else 2, B // (cus * 4)))
+        traffic = (measured_traffic(args.paramset + ("_q50" if args.q_bits == 50 else ""), kname, by)
+                   if not args.n_override else {"bytes": None, "why": "--n-override"})
         peak_mm, peak_src = ((PEAK_FP64_MULMOD_TPS, "exact FP64 product, profiles/r2/ubench_wide.txt") if wide_fp else
                              (PEAK_INT64_MULMOD_TPS, "64-bit Shoup product, profiles/r2/ubench_wide.txt") if wide else
                              (PEAK_SHOUP_MULMOD_TPS, "27-bit Shoup product, profiles/round1_ubench_intops.txt"))
@@ -449,8 +473,8 @@ def run_rank(args, env: dict, make_engine, make_checker, torch_device: str, back
                        "reference's KATs, the EvalAcc composition is 'parity unpinned' beyond them (DESIGN.md s3)"),
             "roofline": {"bound": "hbm", "achieved": by / pl / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": by / pl / 1e9 / PEAK_HBM_GBS,
-                         "traffic": (measured_traffic(args.paramset + ("_q50" if args.q_bits == 50 else ""), kname)
-                                     if not args.n_override else None),
+                         "traffic": traffic["bytes"],
+                         "traffic_record": traffic,
                          "kernel": kname,
                          "per_launch_us": pl * 1e6,
                          "bytes_per_launch": by,
@@ -469,6 +493,7 @@ def run_rank(args, env: dict, make_engine, make_checker, torch_device: str, back
             what = ("NAND gates (head + EvalAcc + extraction/ModSwitch/key switch)" if stage == "gate"
                     else "EvalAccs")
             ref = REF_CPU_S_PER_EVALACC.get(args.paramset) if not (wide or args.n_override) else None
+            o_r = oracle_over_ref()
             result["cpu_baseline"] = {
                 "value": G / dt_c, "unit": "bootstraps/s", "cores": threads, "kind": chk.kind,
                 "sample": (f"{G} {what} spread over the timed batch ({p.k}x{p.n} accumulator steps each), one per "
@@ -476,13 +501,13 @@ def run_rank(args, env: dict, make_engine, make_checker, torch_device: str, back
                            "are the parity check"),
                 "host": cpu,
                 "reference_1core_s_per_evalacc": ref,
-                "oracle_over_reference_1core": ORACLE_OVER_REF.get(args.paramset) if ref else None,
+                "oracle_over_reference_1core": o_r.get(args.paramset) if ref else None,
                 # the reference's throughput on the same cores, scaled by the 1-core time ratio:
-                # an estimate (the ratio compares two different CPUs, CALIBRATION); only
+                # an estimate (the ratio compares two different CPUs, calibration()); only
                 # "value" above is measured on this box
-                "reference_equivalent_estimate": (G / dt_c * ORACLE_OVER_REF[args.paramset]
-                                                  if ref and args.paramset in ORACLE_OVER_REF else None),
-                "calibration": CALIBRATION if ref else None,
+                "reference_equivalent_estimate": (G / dt_c * o_r[args.paramset]
+                                                  if ref and args.paramset in o_r else None),
+                "calibration": calibration() if ref else None,
                 "reference_source": "SURVEY.md s6: the reference's own EvalAcc, 1 thread of the survey container",
             }
     if world > 1:

@@ -25,9 +25,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(_HERE)
 SOURCES = [os.path.join(_HERE, "csrc", f) for f in ("mkacc_engine.hip", "mkacc_steps.hip")]
 HEADERS = [os.path.join(_HERE, "csrc", f) for f in ("mkacc_kernels.hpp", "mkacc_step2.hpp", "mkacc_device.hpp", "mkacc_host_math.hpp",
-                                                    "mkacc_gate.hpp", "mkacc_wide.hpp", "mkacc_widefp.hpp", "mkacc_widereg.hpp",
-                                                    "mkacc_widereg2.hpp", "mkacc_layout2.hpp",
-                                                    "mkacc_step3.hpp")] + [
+                                                    "mkacc_gate.hpp", "mkacc_wide.hpp", "mkacc_fp64.hpp",
+                                                    "mkacc_widereg2.hpp", "mkacc_layout2.hpp")] + [
     os.path.join(ROOT, "include", "mkfhe_amd.h")]
 OUT = os.path.join(_HERE, "lib", "libmkfhe_amd.so")
 KEYS_SOURCES = [os.path.join(_HERE, "csrc", "mkkeys.cpp")]
@@ -97,15 +96,17 @@ STEP2_SCHED = {3: ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"]}
 # Translation units of the engine library, compiled in parallel and linked into
 # one .so: the host unit (C ABI, batch / gate / primitive kernels) and the step
 # kernel units of mkacc_steps.hip (one per digit count and kernel kind, and the
-# two 64-bit word paths), which the host unit launches through mkacc_tu.
+# two 64-bit word paths), which the host unit launches through mkacc_tu.  Only the
+# kernels the engine selects are built: mk_step2_kernel at dg <= 3, mk_step_kernel
+# at dg >= 4, mk_lat_kernel for small batches, the FP64 register-resident kernel
+# below 2^50 and the integer 64-bit kernel above (round 5 retired the variants that
+# lost their A/B runs; DESIGN.md s7 keeps their records).
 UNITS = [("engine", "mkacc_engine.hip", [])] + [
-    (f"step_dg{d}", "mkacc_steps.hip", [f"-DMKACC_TU_DG={d}", "-DMKACC_TU_PART=0"]) for d in (2, 3, 4, 5)] + [
+    (f"step_dg{d}", "mkacc_steps.hip", [f"-DMKACC_TU_DG={d}", "-DMKACC_TU_PART=0"]) for d in (4, 5)] + [
     (f"lat_dg{d}", "mkacc_steps.hip", [f"-DMKACC_TU_DG={d}", "-DMKACC_TU_PART=1"]) for d in (2, 3, 4)] + [
     (f"step2_dg{d}", "mkacc_steps.hip", [f"-DMKACC_TU_DG={d}", "-DMKACC_TU_PART=2"] + STEP2_SCHED.get(d, []))
-    for d in (2, 3, 4)] + [
-    (f"step3_dg{d}", "mkacc_steps.hip", [f"-DMKACC_TU_DG={d}", "-DMKACC_TU_PART=3"]) for d in (2, 3, 4)] + [
-    ("wide", "mkacc_steps.hip", ["-DMKACC_TU_WIDE=1"]), ("widefp", "mkacc_steps.hip", ["-DMKACC_TU_WIDE=2"]),
-    ("widereg", "mkacc_steps.hip", ["-DMKACC_TU_WIDE=3"])]
+    for d in (2, 3)] + [
+    ("wide", "mkacc_steps.hip", ["-DMKACC_TU_WIDE=1"]), ("widereg2", "mkacc_steps.hip", ["-DMKACC_TU_WIDE=2"])]
 
 
 def _jobs() -> int:
@@ -162,6 +163,26 @@ def compile_engine(out: str, flags: list[str], report: str, verbose: bool = Fals
     if verbose:
         print(" ".join(link), flush=True)
     subprocess.check_call(link)
+    os.replace(out + ".tmp", out)
+    write_kernel_ids(out)
+    return out
+
+
+def kernel_ids_path(lib: str) -> str:
+    """The per-kernel machine-code identity file written next to a library."""
+    return lib[:-3] + ".kernel_isa.json"
+
+
+def write_kernel_ids(lib: str) -> str:
+    """{demangled kernel: isa id} of the library (tools/kernel_isa.py): the traffic
+    records under profiles/ name the id of the kernel they measured, and bench.py
+    reports a record only for a library whose kernel has the same machine code."""
+    import json
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import kernel_isa
+    out = kernel_ids_path(lib)
+    with open(out + ".tmp", "w") as f:
+        json.dump(kernel_isa.kernel_ids(lib), f, indent=1)
     os.replace(out + ".tmp", out)
     return out
 

@@ -59,10 +59,8 @@ __device__ __forceinline__ u32x2 bload2(__amdgpu_buffer_rsrc_t r, uint32_t voff,
 // the NEXT group's values for part of the wave (lanes 12-15 of each row), the
 // wrong-result "race" of round 1.  The s_nop sits between scheduling barriers
 // so nothing is moved into the gap.  tools/isa_audit.py checks every build.
-// AUX: cache-policy bits of the store (0 = default policy)
-template <int AUX = 0>
 __device__ __forceinline__ void bstore4(u32x4 v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-    __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, soff, AUX);
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, soff, 0);
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_nop 1");
     __builtin_amdgcn_sched_barrier(0);
@@ -109,15 +107,12 @@ __device__ __forceinline__ uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {
 // the same).  SB: b is wave-uniform (SGPR operand).  Carry-out goes to VCC.
 // gfx950 needs a wait state between a VALU that writes an SGPR (this carry-out)
 // and a VALU that reads any SGPR: with a wave-uniform b in an SGPR, hipcc puts an
-// s_nop 0 between back-to-back multiply-adds.  MKACC_PIN_VB=1 takes b from a VGPR
-// (the compiler keeps a VGPR copy of the loop-invariant constant).
-#ifndef MKACC_PIN_VB
-#define MKACC_PIN_VB 0
-#endif
+// s_nop 0 between back-to-back multiply-adds (the s_nop is not what the wave waits
+// on).
 template <bool SB>
 __device__ __forceinline__ uint64_t mad64_pin(uint32_t a, uint32_t b, uint64_t c) {
     uint64_t r;
-    if constexpr (SB && !MKACC_PIN_VB)
+    if constexpr (SB)
         asm("v_mad_u64_u32 %0, vcc, %1, %2, %3" : "=v"(r) : "v"(a), "s"(b), "v"(c) : "vcc");
     else
         asm("v_mad_u64_u32 %0, vcc, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c) : "vcc");
@@ -126,7 +121,7 @@ __device__ __forceinline__ uint64_t mad64_pin(uint32_t a, uint32_t b, uint64_t c
 template <bool SB>
 __device__ __forceinline__ uint64_t mul64_pin(uint32_t a, uint32_t b) {
     uint64_t r;
-    if constexpr (SB && !MKACC_PIN_VB)
+    if constexpr (SB)
         asm("v_mad_u64_u32 %0, vcc, %1, %2, 0" : "=v"(r) : "v"(a), "s"(b) : "vcc");
     else
         asm("v_mad_u64_u32 %0, vcc, %1, %2, 0" : "=v"(r) : "v"(a), "v"(b) : "vcc");

@@ -53,19 +53,19 @@ int fail(int code, const std::string& msg) {
 
 #include "mkacc_gate.hpp"
 #include "mkacc_wide.hpp"
-#include "mkacc_widefp.hpp"
-#include "mkacc_widereg.hpp"
+#include "mkacc_fp64.hpp"
 #include "mkacc_widereg2.hpp"
 
 namespace {
 
 // Device key upload for the 64-bit word path: reference layout -> [k][n+1][nk][dg][2][N]
 // (EVAL order), each word in Montgomery form K * 2^64 mod Q (r, rp: 2^64 mod Q and its
-// Shoup companion), or for the FP64 variant (fp) the bits of the balanced double.
+// Shoup companion), or for the FP64 kernel (fp) the bits of the balanced double in the
+// C16 layout.
 template <typename W>
 __global__ void wide_key_layout_kernel(const W* __restrict__ src, uint64_t* __restrict__ dst, size_t npolys,
                                        uint32_t nk, uint32_t n1, uint32_t dg2, uint64_t Q, uint64_t r, uint64_t rp,
-                                       bool fp, uint32_t lay, uint32_t* __restrict__ bad) {
+                                       bool fp, uint32_t* __restrict__ bad) {
     const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= npolys * kN) return;
     size_t p = idx / kN;
@@ -77,8 +77,8 @@ __global__ void wide_key_layout_kernel(const W* __restrict__ src, uint64_t* __re
     const size_t dpoly = ((u * n1 + i) * nk + jj) * dg2 + dp;
     const uint64_t x = (uint64_t)src[idx];
     if (x >= Q) *bad = 1u;
-    // register-resident FP64 kernels: C8 (one wave per gate) or C16 (two) layout
-    const uint32_t jd = lay == 1 ? widereg::c8_index(j) : lay == 2 ? widereg2::c16_index(j) : j;
+    // the register-resident FP64 kernel reads its words in the C16 layout
+    const uint32_t jd = fp ? widereg2::c16_index(j) : j;
     if (fp) {
         const double d = (double)(x < Q ? x : 0) - (x > (Q >> 1) && x < Q ? (double)Q : 0.0);
         dst[dpoly * kN + jd] = (uint64_t)__double_as_longlong(d);
@@ -92,44 +92,22 @@ __global__ void wide_key_layout_kernel(const W* __restrict__ src, uint64_t* __re
 // produced the segfault / all-wrong records of ab_l1, lat_l1 and ab_d1,
 // DESIGN.md s2; a null kernel is now refused at mkacc_create and launch.)
 // Batch step kernel generation: 2 = mk_step2_kernel (mkacc_step2.hpp, digit NTTs
-// first, one key stream per pass; built for dg <= 3), 1 = mk_step_kernel (every
-// digit count).  Default 2 where built (STD128_MKNTRU 163.8 -> 158.5 us per
-// launch, STD100_MKNTRU 132.6 -> 126.2, STD100_MKNTRU_LWE_2 187.4 -> 183.7).  At
-// dg = 4 the 4 x 32 digit-NTT registers leave no room for the key prefetch
-// (STD128_MKNTRU_3: 1,704 us with 4-slot groups and no prefetch, 2,593 us with
-// 1-slot groups, against 1,194 us for mk_step_kernel with its d_i scratch;
-// DESIGN.md s2), so it is not built there.  MKACC_STEP=1 selects
-// mk_step_kernel; read once per context (mkacc_ctx::step_ver), which sizes its
-// workspace for that kernel.
-int step_version(int dg) {
-    const char* e = std::getenv("MKACC_STEP");
-    if (dg > 4) return 1;
-    if (e && e[0] == '3') return 3;                 // mk_step3_kernel (two waves per gate)
-    if (dg == 4) return e && e[0] == '2' ? 2 : 1;   // A/B: mk_step2_kernel at one wave per SIMD
-    if (e && e[0] == '1') return 1;
-    return 2;
-}
+// first, one key stream per pass) at dg <= 3, 1 = mk_step_kernel (with its d_i
+// scratch from k >= 4) at dg >= 4.  (STD128_MKNTRU 163.8 -> 158.5 us per launch,
+// STD100_MKNTRU 132.6 -> 126.2, STD100_MKNTRU_LWE_2 187.4 -> 183.7 for the step2
+// form; at dg = 4 the 4 x 32 digit-NTT registers leave no room for the key prefetch
+// and every step2 form measured slower than mk_step_kernel)
+int step_version(int dg) { return dg <= 3 ? 2 : 1; }
 
 const void* step_fn(int dg, int method, bool first, bool dscr, int ver) {
-    if (ver == 3) {
-        switch (dg) {
-            case 2: return mkacc_tu::step3_dg2(method, first);
-            case 3: return mkacc_tu::step3_dg3(method, first);
-            case 4: return mkacc_tu::step3_dg4(method, first);
-            default: return nullptr;
-        }
-    }
     if (ver == 2) {
         switch (dg) {
             case 2: return mkacc_tu::step2_dg2(method, first);
             case 3: return mkacc_tu::step2_dg3(method, first);
-            case 4: return mkacc_tu::step2_dg4(method, first);
             default: return nullptr;
         }
     }
     switch (dg) {
-        case 2: return mkacc_tu::step_dg2(method, first, dscr);
-        case 3: return mkacc_tu::step_dg3(method, first, dscr);
         case 4: return mkacc_tu::step_dg4(method, first, dscr);
         case 5: return mkacc_tu::step_dg5(method, first, dscr);
         default: return nullptr;
@@ -209,7 +187,6 @@ struct mkacc_ctx {
     int cus = 256;                // compute units of the device (mk_lat_kernel residency)
     int method_class = XZW;   // XZW or XZW_B
     int step_ver = 1;         // batch step kernel generation (step_version)
-    uint2* d_tab3 = nullptr;  // mk_step3_kernel per-lane twiddle table (lay2::kTabE pairs)
     uint32_t dg = 0, nk = 0;
     Mod mod{};
     SddConsts sd{};
@@ -262,19 +239,14 @@ struct mkacc_ctx {
     ulonglong2* d_wpsi = nullptr;  // psi^e, e < 2N
     uint64_t* d_wkeys = nullptr;   // [k][n+1][nk][dg][2][N] EVAL (FP64 variant: balanced doubles)
     uint64_t* d_wpkey = nullptr;   // [k][dg][N]
-    // FP64 variant of the wide path (mkacc_widefp.hpp), Q < 2^50
+    // FP64 register-resident kernel of the wide path (mkacc_widereg2.hpp), Q < 2^50,
+    // balanced doubles in the C16 layout
     bool wfp = false;
-    widefp::FMod wfm{};
-    double wfninv = 0, wfC = 0;
-    double wfcL = 0, wfCm = 0;     // widereg offset-word constants (mkacc_widereg.hpp offset_word)
-    bool wfreg = false;            // FP64 register-resident kernel (mkacc_widereg.hpp), C8 layouts
-    bool wfreg2 = false;           // ... with two waves per gate (mkacc_widereg2.hpp), C16 layouts
-    double* d_r2tab = nullptr;     // its per-lane twiddle table (widereg2::kTabD doubles)
-    uint32_t wlay() const { return wfreg2 ? 2u : (wfreg ? 1u : 0u); }
-    double* d_rimg = nullptr;      // its LDS image (widereg::kImgD doubles)
-    double* d_rtis = nullptr;      // its inverse pass-1 table [32]
-    double* d_ftwf = nullptr;      // forward / inverse twiddles and psi^e, balanced
-    double* d_ftwi = nullptr;
+    fp64::FMod wfm{};
+    double wfcL = 0, wfCm = 0;     // offset-word constants (fp64::offset_word)
+    double* d_r2tab = nullptr;     // per-lane twiddle table (widereg2::kTabD doubles)
+    double* d_rtis = nullptr;      // inverse pass-1 table [32]
+    double* d_ftwf = nullptr;      // forward twiddles (reference order) and psi^e, balanced
     double* d_fpsi = nullptr;
     size_t wws_B = 0, wio_B = 0;
     uint64_t* d_wacc0 = nullptr;
@@ -323,17 +295,8 @@ bool use_lat(const mkacc_ctx* c, size_t B) {
 }
 
 // Per-gate scratch words of the batch step kernel: mk_step_kernel DSCR keeps the
-// step's d_i ([dg][N]); mk_step2_kernel keeps sumV between the party passes ([N],
-// Step2Cfg::kSvMem).
-size_t step_scratch_words(const mkacc_ctx* c) {
-    if (use_dscr(c)) return (size_t)c->dg * kN;
-    // mk_step2_kernel at dg = 4 in two halves parks its ev2 partial sums there
-    if (c->step_ver == 2 && c->dg == 4 && s2_halves<4>()) return kN;
-#if defined(MKACC_S2_SVMEM) && MKACC_S2_SVMEM
-    if (c->step_ver == 2) return kN;   // A/B build only: the default kernel keeps sumV in registers
-#endif
-    return 0;
-}
+// step's d_i ([dg][N]).
+size_t step_scratch_words(const mkacc_ctx* c) { return use_dscr(c) ? (size_t)c->dg * kN : 0; }
 
 int ensure_ws(mkacc_ctx* c, size_t B) {
     if (B <= c->ws_B) return MKACC_OK;
@@ -388,7 +351,6 @@ struct StepChain {
         a.m = c->mod;
         a.sd = c->sd;
         a.dscr = c->d_dscr ? c->d_dscr + g0 * step_scratch_words(c) : nullptr;
-        a.tab3 = c->d_tab3;
         // a null kernel must never reach hipLaunchKernelGGL (mkacc_create checks the set)
         if (lat) {
             const void* fn = lat_fn((int)c->dg, c->method_class, first);
@@ -397,9 +359,7 @@ struct StepChain {
         } else {
             const void* fn = step_fn((int)c->dg, c->method_class, first, !first && use_dscr(c), c->step_ver);
             if (!fn) return false;
-            if (c->step_ver == 3)   // one 2-wave workgroup per gate
-                launch_ptr(fn, dim3((unsigned)Bh), dim3(128), s3::kLdsBytes + (lds - kStepLdsBytes), st, a);
-            else if (c->step_ver == 2)
+            if (c->step_ver == 2)
                 launch_ptr(fn, dim3((unsigned)((Bh + kS2Waves - 1) / kS2Waves)), dim3(64 * kS2Waves),
                            kStep2LdsBytes + (lds - kStepLdsBytes), st, a);
             else
@@ -683,9 +643,9 @@ int upload_keys_device_impl(mkacc_ctx* c, const W* d_evk, const W* d_pkey) {
         if (!c->d_wkeys) HIP_TRY(hipMalloc(&c->d_wkeys, ep * kN * 8));
         if (!c->d_wpkey) HIP_TRY(hipMalloc(&c->d_wpkey, pp * kN * 8));
         hipLaunchKernelGGL(wide_key_layout_kernel<W>, grid(ep), dim3(tpb), 0, c->stream, d_evk, c->d_wkeys, ep, nk,
-                           n1, dg * 2, Q, R, Rp, c->wfp, c->wlay(), kbad);
+                           n1, dg * 2, Q, R, Rp, c->wfp, kbad);
         hipLaunchKernelGGL(wide_key_layout_kernel<W>, grid(pp), dim3(tpb), 0, c->stream, d_pkey, c->d_wpkey, pp, 1u,
-                           1u, dg, Q, R, Rp, c->wfp, c->wlay(), kbad);
+                           1u, dg, Q, R, Rp, c->wfp, kbad);
     } else {
         if (!c->d_keys) HIP_TRY(hipMalloc(&c->d_keys, ep * kN * 4));
         if (!c->d_pkey) HIP_TRY(hipMalloc(&c->d_pkey, pp * kN * 4));
@@ -786,114 +746,75 @@ int wide_setup(mkacc_ctx* c) {
     HIP_TRY(hipMemcpy(c->d_wtwf, tf.data(), kN * sizeof(ulonglong2), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->d_wtwi, ti.data(), kN * sizeof(ulonglong2), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->d_wpsi, pw.data(), 2 * kN * sizeof(ulonglong2), hipMemcpyHostToDevice));
-    // FP64 variant (mkacc_widefp.hpp): exact while every value stays below 8 Q <= 2^53
-    // and the SDD offset word below 2^53; MKACC_WIDE_FP=0 keeps the integer kernels
+    // FP64 register-resident kernel (mkacc_widereg2.hpp): exact while every value stays
+    // below 8 Q <= 2^53; the offset word's 2^52 form (fp64::offset_word) needs
+    // C + L >= 0 and C + (Q - 1) / 2 < 2^52.  MKACC_WIDE_FP=0 keeps the integer kernels.
     const char* fe = std::getenv("MKACC_WIDE_FP");
-    c->wfp = Q < (1ull << 50) && b * c->p.digitsG <= 52 && !(fe && fe[0] == '0');
+    const uint64_t cL = (Q + 1) / 2;
+    c->wfp = Q < (1ull << 50) && b * c->p.digitsG <= 52 && C >= cL && C + (Q >> 1) < (1ull << 52) &&
+             !(fe && fe[0] == '0');
     if (c->wfp) {
         const double Qd = (double)Q;
-        c->wfm = widefp::FMod{Qd, 1.0 / Qd, (double)(Q >> 1)};
+        c->wfm = fp64::FMod{Qd, 1.0 / Qd, (double)(Q >> 1)};
         auto bal = [Q](uint64_t x) { return x > (Q >> 1) ? (double)x - (double)Q : (double)x; };
-        c->wfninv = bal(c->wninv);
-        c->wfC = (double)C;
-        std::vector<double> ftf(kN), fti(kN), fpw(2 * kN);
-        for (uint32_t i = 0; i < (uint32_t)kN; ++i) {
-            ftf[i] = bal(tf[i].x);
-            fti[i] = bal(ti[i].x);
-        }
-        for (uint32_t i = 0; i < 2u * kN; ++i) fpw[i] = bal(pw[i].x);
-        HIP_TRY(hipMalloc(&c->d_ftwf, kN * sizeof(double)));
-        HIP_TRY(hipMalloc(&c->d_ftwi, kN * sizeof(double)));
-        HIP_TRY(hipMalloc(&c->d_fpsi, 2 * kN * sizeof(double)));
-        HIP_TRY(hipMemcpy(c->d_ftwf, ftf.data(), kN * sizeof(double), hipMemcpyHostToDevice));
-        HIP_TRY(hipMemcpy(c->d_ftwi, fti.data(), kN * sizeof(double), hipMemcpyHostToDevice));
-        HIP_TRY(hipMemcpy(c->d_fpsi, fpw.data(), 2 * kN * sizeof(double), hipMemcpyHostToDevice));
-        // register-resident kernel (mkacc_widereg.hpp, default; MKACC_WFP_REG=0 keeps
-        // widefp::step_kernel): per-lane twiddle image in the 27-bit kernels' twl layout
-        const char* re = std::getenv("MKACC_WFP_REG");
-        // offset_word's 2^52 form needs C + L >= 0 and C + (Q - 1) / 2 < 2^52
-        const uint64_t cL = (Q + 1) / 2;
-        c->wfreg = !(re && re[0] == '0') && C >= cL && C + (Q >> 1) < (1ull << 52);
         c->wfcL = (double)cL;
         c->wfCm = (double)((1ull << 52) + (C - std::min(C, cL)));
-        if (c->wfreg) {
-            std::vector<double> img(widereg::kImgD), tis(32, 0.0);
-            double* F = img.data() + widereg::kImgFwd;
-            for (int st = 5; st <= 9; ++st) {
-                const int NP = 1 << (st - 5);
-                for (int lhi = 0; lhi < 32; ++lhi)
-                    for (int m = 0; m < NP; ++m) F[twl_off(st) + 32 * m + lhi] = ftf[(1 << st) + lhi * NP + m];
+        std::vector<double> ftf(kN), fpw(2 * kN), tis(32, 0.0);
+        for (uint32_t i = 0; i < (uint32_t)kN; ++i) ftf[i] = bal(tf[i].x);
+        for (uint32_t i = 0; i < 2u * kN; ++i) fpw[i] = bal(pw[i].x);
+        // psi^-e for e in [0, 2N) in natural order
+        std::vector<uint64_t> pwi(2 * kN);
+        {
+            uint64_t ei = 1;
+            for (uint32_t i = 0; i < 2u * kN; ++i) {
+                pwi[i] = ei;
+                ei = mulmod(ei, psii, Q);
             }
-            for (int ln = 0; ln < 64; ++ln)
-                for (int m = 0; m < 16; ++m) F[kTwlC + 64 * m + ln] = ftf[1024 + 16 * ln + m];
-            // psi^-e for e in [0, 2N): ti holds psi^-i at brv(i), pwi in natural order
-            std::vector<uint64_t> pwi(2 * kN);
-            {
-                uint64_t ei = 1;
-                for (uint32_t i = 0; i < 2u * kN; ++i) {
-                    pwi[i] = ei;
-                    ei = mulmod(ei, psii, Q);
-                }
-            }
-            double* I = img.data() + widereg::kImgInv;
-            for (int b = 5; b <= 9; ++b)
-                for (int m = 0; m < (1 << (b - 5)); ++m)
-                    for (int l31 = 0; l31 < 32; ++l31) I[twl_off(b) + 32 * m + l31] = bal(pwi[(size_t)(l31 | (m << 5)) << (11 - b)]);
-            for (int m = 0; m < 16; ++m)
-                for (int ln = 0; ln < 64; ++ln) I[kTwlC + 64 * m + ln] = bal(pwi[(size_t)((m << 6) | ln) << 1]);
-            // the twist psi^-i with the reference's N^-1 folded in
-            double* T = img.data() + widereg::kImgTwist;
-            for (int r = 0; r < 32; ++r)
-                for (int ln = 0; ln < 64; ++ln) T[64 * r + ln] = bal(mulmod(pwi[(r << 6) | ln], c->wninv, Q));
-            double* P = img.data() + widereg::kImgPsi;
-            for (uint32_t e = 0; e < 2u * kN; ++e) P[e] = fpw[e];
-            for (int b = 0; b < 5; ++b)
-                for (int t = 0; t < (1 << b); ++t) tis[(1 << b) + t] = bal(pwi[(size_t)t << (11 - b)]);
-            // two waves per gate (mkacc_widereg2.hpp, default; MKACC_WREG2=0 keeps one): its
-            // per-lane twiddle table, value k of sub-table T for (w, l) at
-            // ((kTG0[T] + k / 2) * 128 + w * 64 + l) * 2 + k % 2 (index maps checked against
-            // the oracle by tools/widereg2_model.py)
-            const char* r2 = std::getenv("MKACC_WREG2");
-            c->wfreg2 = !(r2 && r2[0] == '0');
-            if (c->wfreg2) {
-                using namespace lay2;
-                std::vector<double> tab(kTabE, 0.0);
-                auto put = [&](int T, uint32_t w, uint32_t l, int k, double v) { tab[tab_index(T, w, l, k)] = v; };
-                auto lg = [](int v) { int b = 0; while ((2 << b) <= v) ++b; return b; };   // floor(log2 v)
-                for (uint32_t w = 0; w < 2; ++w)
-                    for (uint32_t l = 0; l < 64; ++l) {
-                        const uint32_t l3 = (l >> 3) & 1u, l4 = (l >> 4) & 1u, l5 = (l >> 5) & 1u;
-                        auto pb = [&](uint32_t r) { return (r << 3) | (l & 7u) | (l3 << 7) | (l4 << 8) | (l5 << 9) | (w << 10); };
-                        auto pd = [&](uint32_t r) { return (r << 4) | (l & 15u) | (l4 << 8) | (l5 << 9) | (w << 10); };
-                        for (int k = 0; k < 7; ++k) {          // forward B2, stages 4..6
-                            const int st = 4 + lg(k + 1), m = k - ((1 << (st - 4)) - 1);
-                            put(TFB, w, l, k, ftf[(1u << st) + (pb((uint32_t)m << (8 - st)) >> (11 - st))]);
-                        }
-                        for (int k = 0; k < 15; ++k) {         // forward C2, stages 7..10
-                            const int st = 7 + lg(k + 1), m = k - ((1 << (st - 7)) - 1);
-                            put(TFC, w, l, k, ftf[(1u << st) + (pos_c(w, l, (uint32_t)m << (11 - st)) >> (11 - st))]);
-                        }
-                        for (int k = 0; k < 15; ++k) {         // inverse D2, bits 4..7
-                            const int b = 4 + lg(k + 1), H = 1 << (b - 4);
-                            const uint32_t t = pd((uint32_t)(k - (H - 1))) & ((1u << b) - 1u);
-                            put(TID, w, l, k, bal(pwi[(size_t)t << (11 - b)]));
-                        }
-                        for (int k = 0; k < 14; ++k) {         // inverse A2, bits 8..10
-                            const int b = k < 2 ? 8 : (k < 6 ? 9 : 10), H = 1 << (b - 7);
-                            const uint32_t t = pos_a(w, l, (uint32_t)(k - (H - 2))) & ((1u << b) - 1u);
-                            put(TIA, w, l, k, bal(pwi[(size_t)t << (11 - b)]));
-                        }
-                        for (int k = 0; k < 16; ++k)           // twist psi^-p N^-1
-                            put(TTW, w, l, k, bal(mulmod(pwi[pos_a(w, l, (uint32_t)k)], c->wninv, Q)));
-                    }
-                HIP_TRY(hipMalloc(&c->d_r2tab, tab.size() * sizeof(double)));
-                HIP_TRY(hipMemcpy(c->d_r2tab, tab.data(), tab.size() * sizeof(double), hipMemcpyHostToDevice));
-            }
-            HIP_TRY(hipMalloc(&c->d_rimg, img.size() * sizeof(double)));
-            HIP_TRY(hipMalloc(&c->d_rtis, tis.size() * sizeof(double)));
-            HIP_TRY(hipMemcpy(c->d_rimg, img.data(), img.size() * sizeof(double), hipMemcpyHostToDevice));
-            HIP_TRY(hipMemcpy(c->d_rtis, tis.data(), tis.size() * sizeof(double), hipMemcpyHostToDevice));
         }
+        // inverse pass 1: bit b, t < 2^b -> psi^-(t 2^(11-b)) (the kernel reads b < 4)
+        for (int b = 0; b < 5; ++b)
+            for (int t = 0; t < (1 << b); ++t) tis[(1 << b) + t] = bal(pwi[(size_t)t << (11 - b)]);
+        // per-lane twiddle table: value k of sub-table T for (w, l) at
+        // ((kTG0[T] + k / 2) * 128 + w * 64 + l) * 2 + k % 2 (index maps checked against
+        // the oracle by tools/widereg2_model.py)
+        using namespace lay2;
+        std::vector<double> tab(kTabE, 0.0);
+        auto put = [&](int T, uint32_t w, uint32_t l, int k, double v) { tab[tab_index(T, w, l, k)] = v; };
+        auto lg = [](int v) { int b = 0; while ((2 << b) <= v) ++b; return b; };   // floor(log2 v)
+        for (uint32_t w = 0; w < 2; ++w)
+            for (uint32_t l = 0; l < 64; ++l) {
+                const uint32_t l3 = (l >> 3) & 1u, l4 = (l >> 4) & 1u, l5 = (l >> 5) & 1u;
+                auto pb = [&](uint32_t r) { return (r << 3) | (l & 7u) | (l3 << 7) | (l4 << 8) | (l5 << 9) | (w << 10); };
+                auto pd = [&](uint32_t r) { return (r << 4) | (l & 15u) | (l4 << 8) | (l5 << 9) | (w << 10); };
+                for (int k = 0; k < 7; ++k) {          // forward B2, stages 4..6
+                    const int st = 4 + lg(k + 1), m = k - ((1 << (st - 4)) - 1);
+                    put(TFB, w, l, k, ftf[(1u << st) + (pb((uint32_t)m << (8 - st)) >> (11 - st))]);
+                }
+                for (int k = 0; k < 15; ++k) {         // forward C2, stages 7..10
+                    const int st = 7 + lg(k + 1), m = k - ((1 << (st - 7)) - 1);
+                    put(TFC, w, l, k, ftf[(1u << st) + (pos_c(w, l, (uint32_t)m << (11 - st)) >> (11 - st))]);
+                }
+                for (int k = 0; k < 15; ++k) {         // inverse D2, bits 4..7
+                    const int b = 4 + lg(k + 1), H = 1 << (b - 4);
+                    const uint32_t t = pd((uint32_t)(k - (H - 1))) & ((1u << b) - 1u);
+                    put(TID, w, l, k, bal(pwi[(size_t)t << (11 - b)]));
+                }
+                for (int k = 0; k < 14; ++k) {         // inverse A2, bits 8..10
+                    const int b = k < 2 ? 8 : (k < 6 ? 9 : 10), H = 1 << (b - 7);
+                    const uint32_t t = pos_a(w, l, (uint32_t)(k - (H - 2))) & ((1u << b) - 1u);
+                    put(TIA, w, l, k, bal(pwi[(size_t)t << (11 - b)]));
+                }
+                for (int k = 0; k < 16; ++k)           // twist psi^-p N^-1
+                    put(TTW, w, l, k, bal(mulmod(pwi[pos_a(w, l, (uint32_t)k)], c->wninv, Q)));
+            }
+        HIP_TRY(hipMalloc(&c->d_ftwf, kN * sizeof(double)));
+        HIP_TRY(hipMalloc(&c->d_fpsi, 2 * kN * sizeof(double)));
+        HIP_TRY(hipMalloc(&c->d_rtis, tis.size() * sizeof(double)));
+        HIP_TRY(hipMalloc(&c->d_r2tab, tab.size() * sizeof(double)));
+        HIP_TRY(hipMemcpy(c->d_ftwf, ftf.data(), kN * sizeof(double), hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(c->d_fpsi, fpw.data(), 2 * kN * sizeof(double), hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(c->d_rtis, tis.data(), tis.size() * sizeof(double), hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(c->d_r2tab, tab.data(), tab.size() * sizeof(double), hipMemcpyHostToDevice));
     }
     return MKACC_OK;
 }
@@ -905,7 +826,7 @@ int wide_upload_keys(mkacc_ctx* c, const W* evk, const W* pkey) {
     if (!evk || !pkey) return fail(MKACC_E_ARG, "null key pointer");
     const uint64_t Q = c->p.Q;
     const uint64_t R = (uint64_t)(((unsigned __int128)1 << 64) % Q);
-    const bool fp = c->wfp;   // FP64 variant: the bits of the balanced double
+    const bool fp = c->wfp;   // FP64 kernel: the bits of the balanced double
     auto mont = [Q, R, fp](uint64_t x) {
         if (fp) {
             const double d = x > (Q >> 1) ? (double)x - (double)Q : (double)x;
@@ -917,10 +838,10 @@ int wide_upload_keys(mkacc_ctx* c, const W* evk, const W* pkey) {
     };
     const uint32_t k = c->p.k, n = c->p.n, nk = c->nk, dg = c->dg;
     const size_t blk = (size_t)dg * 2 * kN;
-    // the register-resident FP64 kernel reads every polynomial in the C8 layout
-    auto pos = [lay = c->wlay()](size_t s) {
+    // the register-resident FP64 kernel reads every polynomial in the C16 layout
+    auto pos = [fp](size_t s) {
         const uint32_t j = (uint32_t)(s & (kN - 1));
-        return (s & ~(size_t)(kN - 1)) | (lay == 1 ? widereg::c8_index(j) : lay == 2 ? widereg2::c16_index(j) : j);
+        return (s & ~(size_t)(kN - 1)) | (fp ? widereg2::c16_index(j) : j);
     };
     std::vector<uint64_t> host((size_t)k * (n + 1) * nk * blk);
     for (uint32_t u = 0; u < k; ++u)
@@ -979,7 +900,7 @@ int wide_launch_batch(mkacc_ctx* c, const uint32_t* d_ct, const uint64_t* d_in, 
     auto key = [&](uint32_t u, uint32_t i, uint32_t j) {
         return c->d_wkeys + (((size_t)u * (n + 1) + i) * c->nk + j) * blk;
     };
-    if (c->wfreg2) {   // two waves per gate: balanced doubles in the C16 layout
+    if (c->wfp) {   // FP64, two waves per gate: balanced doubles in the C16 layout
         const size_t words = B * (size_t)k * kN;
         const dim3 g((unsigned)((words + 255) / 256));
         double* cur = reinterpret_cast<double*>(c->d_wacc0);
@@ -1033,83 +954,6 @@ int wide_launch_batch(mkacc_ctx* c, const uint32_t* d_ct, const uint64_t* d_in, 
             HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_join[j - 1], 0));
         }
         hipLaunchKernelGGL(widereg2::from_c16_kernel, g, dim3(256), 0, c->stream, cur, d_out, words, c->wfm);
-        HIP_TRY(hipGetLastError());
-        return MKACC_OK;
-    }
-    if (c->wfreg) {   // register-resident FP64 kernel: balanced doubles in the C8 layout
-        const size_t words = B * (size_t)k * kN;
-        const dim3 g((unsigned)((words + 255) / 256));
-        double* cur = reinterpret_cast<double*>(c->d_wacc0);
-        double* nxt = reinterpret_cast<double*>(c->d_wacc1);
-        hipLaunchKernelGGL(widereg::to_c8_kernel, g, dim3(256), 0, c->stream, d_in, cur, words, c->wfm, c->p.Q,
-                           c->d_bad);
-        auto dk = [](const uint64_t* p) { return reinterpret_cast<const double*>(p); };
-        // one workgroup of four gates per CU, looping over the batch
-        const size_t wgs = std::min<size_t>((B + widereg::kWaves - 1) / widereg::kWaves, (size_t)c->cus);
-        for (uint32_t u = 0; u < k; ++u)
-            for (uint32_t i = 0; i < n; ++i) {
-                const bool first = (u == 0 && i == 0);
-                widereg::StepArgs a;
-                a.acc_in = cur;
-                a.acc_out = nxt;
-                a.cvals = c->d_wcvals + ((size_t)u * n + i) * B;
-                a.key1 = dk(key(u, i, 0));
-                a.key2 = dk(c->nk == 2 ? key(u, i, 1) : key(u, i, 0));
-                a.keys = dk(key(0, n, 0));
-                a.pkey = dk(c->d_wpkey);
-                a.img = c->d_rimg;
-                a.twf = c->d_ftwf;
-                a.tis = c->d_rtis;
-                a.B = (uint32_t)B;
-                a.k = k;
-                a.index = u;
-                a.dg = c->dg;
-                a.cL = c->wfcL;
-                a.Cm = c->wfCm;
-                a.m = c->wfm;
-                a.sd = c->wsd;
-                launch_ptr(mkacc_tu::widereg_step(c->method_class, first), dim3((unsigned)wgs),
-                           dim3(64 * widereg::kWaves), widereg::kLdsBytes, c->stream, a);
-                std::swap(cur, nxt);
-            }
-        hipLaunchKernelGGL(widereg::from_c8_kernel, g, dim3(256), 0, c->stream, cur, d_out, words, c->wfm);
-        HIP_TRY(hipGetLastError());
-        return MKACC_OK;
-    }
-    if (c->wfp) {   // FP64 variant: balanced doubles between the prologue and the epilogue
-        const size_t words = B * (size_t)k * kN;
-        const dim3 g((unsigned)((words + 255) / 256));
-        double* cur = reinterpret_cast<double*>(c->d_wacc0);
-        double* nxt = reinterpret_cast<double*>(c->d_wacc1);
-        hipLaunchKernelGGL(widefp::to_balanced_kernel, g, dim3(256), 0, c->stream, d_in, cur, words, c->wfm,
-                           c->p.Q, c->d_bad);
-        auto dk = [](const uint64_t* p) { return reinterpret_cast<const double*>(p); };
-        for (uint32_t u = 0; u < k; ++u)
-            for (uint32_t i = 0; i < n; ++i) {
-                const bool first = (u == 0 && i == 0);
-                widefp::StepArgs a;
-                a.acc_in = cur;
-                a.acc_out = nxt;
-                a.cvals = c->d_wcvals + ((size_t)u * n + i) * B;
-                a.key1 = dk(key(u, i, 0));
-                a.key2 = dk(c->nk == 2 ? key(u, i, 1) : key(u, i, 0));
-                a.keys = dk(key(0, n, 0));
-                a.pkey = dk(c->d_wpkey);
-                a.twf = c->d_ftwf;
-                a.twi = c->d_ftwi;
-                a.psi = c->d_fpsi;
-                a.k = k;
-                a.index = u;
-                a.dg = c->dg;
-                a.ninv = c->wfninv;
-                a.C = c->wfC;
-                a.m = c->wfm;
-                a.sd = c->wsd;
-                launch_ptr(mkacc_tu::widefp_step(c->method_class, first), dim3((unsigned)B), dim3(widefp::kThreads), 0,
-                           c->stream, a);
-                std::swap(cur, nxt);
-            }
-        hipLaunchKernelGGL(widefp::to_canonical_kernel, g, dim3(256), 0, c->stream, cur, d_out, words, c->wfm);
         HIP_TRY(hipGetLastError());
         return MKACC_OK;
     }
@@ -1184,25 +1028,12 @@ int wide_prim(mkacc_ctx* c, const uint64_t* in, uint64_t* out, size_t count, int
     HIP_TRY(hipMalloc(&din, count * kN * 8));
     HIP_TRY(hipMalloc(&dout, count * kN * 8 * out_mul));
     HIP_TRY(hipMemcpyAsync(din, in, count * kN * 8, hipMemcpyHostToDevice, c->stream));
-    const unsigned rgrid = (unsigned)((count + widereg::kWaves - 1) / widereg::kWaves);
-    if (which == 0 && c->wfreg2)
+    if (which == 0 && c->wfp)
         hipLaunchKernelGGL(widereg2::ntt_fwd_kernel, dim3((unsigned)count), dim3(128), widereg2::kLdsBytes, c->stream,
                            din, dout, c->d_r2tab, c->d_ftwf, c->wfm);
-    else if (which == 1 && c->wfreg2)
+    else if (which == 1 && c->wfp)
         hipLaunchKernelGGL(widereg2::ntt_inv_kernel, dim3((unsigned)count), dim3(128), widereg2::kLdsBytes, c->stream,
                            din, dout, c->d_r2tab, c->d_rtis, c->wfm);
-    else if (which == 0 && c->wfreg)
-        hipLaunchKernelGGL(widereg::ntt_fwd_kernel, dim3(rgrid), dim3(64 * widereg::kWaves), widereg::kLdsBytes,
-                           c->stream, din, dout, (uint32_t)count, c->d_rimg, c->d_ftwf, c->wfm);
-    else if (which == 1 && c->wfreg)
-        hipLaunchKernelGGL(widereg::ntt_inv_kernel, dim3(rgrid), dim3(64 * widereg::kWaves), widereg::kLdsBytes,
-                           c->stream, din, dout, (uint32_t)count, c->d_rimg, c->d_rtis, c->wfm);
-    else if (which == 0 && c->wfp)
-        hipLaunchKernelGGL(widefp::ntt_fwd_kernel, dim3((unsigned)count), dim3(widefp::kThreads), 0, c->stream, din,
-                           dout, c->d_ftwf, c->wfm);
-    else if (which == 1 && c->wfp)
-        hipLaunchKernelGGL(widefp::ntt_inv_kernel, dim3((unsigned)count), dim3(widefp::kThreads), 0, c->stream, din,
-                           dout, c->d_ftwi, c->wfm, c->wfninv);
     else if (which == 0)
         hipLaunchKernelGGL(wide::ntt_fwd_kernel, dim3((unsigned)count), dim3(wide::kThreads), 0, c->stream, din, dout,
                            c->d_wtwf, Q);
@@ -1445,37 +1276,6 @@ int mkacc_create(const mkacc_params* pin, int device, mkacc_ctx** out) {
             img[kPsm1Off + psi_pos(e)] = pair((pw[e] + Q - 1) % Q);
         }
     }
-    // mk_step3_kernel's per-lane twiddle pairs (mkacc_layout2.hpp tables, EVAL layout LC4;
-    // index maps checked against the oracle by tools/widereg2_model.py)
-    std::vector<uint2> t3(lay2::kTabE, make_uint2(0, 0));
-    {
-        using namespace lay2;
-        auto lg = [](int v) { int b = 0; while ((2 << b) <= v) ++b; return b; };   // floor(log2 v)
-        for (uint32_t w = 0; w < 2; ++w)
-            for (uint32_t l = 0; l < 64; ++l) {
-                for (int k = 0; k < 7; ++k) {          // forward LB, stages 4..6
-                    const int st = 4 + lg(k + 1), m = k - ((1 << (st - 4)) - 1);
-                    t3[tab_index(TFB, w, l, k)] = htf[(1u << st) + (pos_b(w, l, (uint32_t)m << (8 - st)) >> (11 - st))];
-                }
-                for (int k = 0; k < 15; ++k) {         // forward LC4, stages 7..10
-                    const int st = 7 + lg(k + 1), m = k - ((1 << (st - 7)) - 1);
-                    t3[tab_index(TFC, w, l, k)] = htf[(1u << st) + (pos_c4(w, l, (uint32_t)m << (11 - st)) >> (11 - st))];
-                }
-                for (int k = 0; k < 15; ++k) {         // inverse LD, bits 4..7
-                    const int b = 4 + lg(k + 1), H = 1 << (b - 4);
-                    const uint32_t t = pos_d(w, l, (uint32_t)(k - (H - 1))) & ((1u << b) - 1u);
-                    t3[tab_index(TID, w, l, k)] = npair(pwi[(size_t)t << (11 - b)]);
-                }
-                for (int k = 0; k < 14; ++k) {         // inverse LA, bits 8..10
-                    const int b = k < 2 ? 8 : (k < 6 ? 9 : 10), H = 1 << (b - 7);
-                    const uint32_t t = pos_a(w, l, (uint32_t)(k - (H - 2))) & ((1u << b) - 1u);
-                    t3[tab_index(TIA, w, l, k)] = npair(pwi[(size_t)t << (11 - b)]);
-                }
-                for (int k = 0; k < 16; ++k) t3[tab_index(TTW, w, l, k)] = pair(pwi[pos_a(w, l, (uint32_t)k)]);
-            }
-    }
-    HIP_TRY(hipMalloc(&c->d_tab3, t3.size() * sizeof(uint2)));
-    HIP_TRY(hipMemcpy(c->d_tab3, t3.data(), t3.size() * sizeof(uint2), hipMemcpyHostToDevice));
     HIP_TRY(hipMalloc(&c->d_img, img.size() * sizeof(uint2)));
     HIP_TRY(hipMemcpy(c->d_twf, htf.data(), htf.size() * sizeof(uint2), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->d_twi, hti.data(), hti.size() * sizeof(uint2), hipMemcpyHostToDevice));
@@ -1492,7 +1292,8 @@ void mkacc_destroy(mkacc_ctx* c) {
                     (void*)c->d_acc0, (void*)c->d_acc1, (void*)c->d_cvals, (void*)c->d_dscr, (void*)c->d_ct,
                     (void*)c->d_io, (void*)c->d_ksk, (void*)c->d_lweA, (void*)c->d_lweB, (void*)c->d_tv,
                     (void*)c->d_digits, (void*)c->d_bh, (void*)c->d_gin, (void*)c->d_gout, (void*)c->d_wtwf,
-                    (void*)c->d_wtwi, (void*)c->d_wpsi, (void*)c->d_ftwf, (void*)c->d_ftwi, (void*)c->d_fpsi, (void*)c->d_rimg, (void*)c->d_rtis, (void*)c->d_r2tab, (void*)c->d_tab3,
+                    (void*)c->d_wtwi, (void*)c->d_wpsi, (void*)c->d_ftwf, (void*)c->d_fpsi, (void*)c->d_rtis,
+                    (void*)c->d_r2tab,
                     (void*)c->d_wkeys, (void*)c->d_wpkey, (void*)c->d_wacc0,
                     (void*)c->d_wacc1, (void*)c->d_wcvals, (void*)c->d_wct, (void*)c->d_wio, (void*)c->d_bad})
         if (p) (void)hipFree(p);
@@ -1542,11 +1343,9 @@ int mkacc_upload_keys_device(mkacc_ctx* c, const void* d_evk, const void* d_pkey
 const char* mkacc_step_kernel_name(const mkacc_ctx* c, size_t B) {
     if (!c) return "";
     if (c->wide)
-        return c->wfreg2  ? "widereg2::step_kernel"
-               : c->wfreg ? "widereg::step_kernel"
-                          : (c->wfp ? "widefp::step_kernel" : "wide::step_kernel");
+        return c->wfp ? "widereg2::step_kernel" : "wide::step_kernel";
     if (use_lat(c, B)) return "mk_lat_kernel";
-    return c->step_ver == 3 ? "mk_step3_kernel" : (c->step_ver == 2 ? "mk_step2_kernel" : "mk_step_kernel");
+    return c->step_ver == 2 ? "mk_step2_kernel" : "mk_step_kernel";
 }
 int mkacc_is_wide(const mkacc_ctx* c) { return c && c->wide ? (c->wfp ? 2 : 1) : 0; }
 

@@ -46,12 +46,10 @@ constexpr int kLdsTabWords = 2 * (1024 + kPsiPairs);
 constexpr size_t kStepLdsBytes = (size_t)(kLdsTabWords + kWavesPerBlock * kLdsWords) * 4;
 static_assert(kLdsTabWords % 4 == 0, "LDS tables are copied with dwordx4");
 static_assert(2 * kStepLdsBytes <= 160 * 1024, "two workgroups per CU");
-// mk_step2_kernel workgroup: kS2Waves gates sharing one LDS table image (4: two
-// workgroups per CU; 8: one, the table copied once per CU)
-#ifndef MKACC_S2_WAVES
-#define MKACC_S2_WAVES 4
-#endif
-constexpr int kS2Waves = MKACC_S2_WAVES;
+// mk_step2_kernel workgroup: kS2Waves gates sharing one LDS table image, two
+// workgroups per CU (one 8-wave workgroup with one table copy per CU measured 2 %
+// slower, profiles/r3/ab_step2.txt)
+constexpr int kS2Waves = 4;
 constexpr size_t kStep2LdsBytes = (size_t)(kLdsTabWords + kS2Waves * kLdsWords) * 4;
 static_assert((8 / kS2Waves) * kStep2LdsBytes <= 160 * 1024, "8 waves per CU");
 
@@ -65,13 +63,7 @@ static_assert((8 / kS2Waves) * kStep2LdsBytes <= 160 * 1024, "8 waves per CU");
 // most distinct dwords per bank, 2 = conflict-free) this averages 3.83 LDS
 // cycles per gather against 4.28 for the earlier e ^ ((e >> 5) & 31), which
 // also cost 6 VALU of address arithmetic per gather instead of 2.
-// MKACC_PSI_HI=1 (A/B): the earlier e ^ ((e >> 5) & 31), gathered with 4 VALU
-#ifndef MKACC_PSI_HI
-#define MKACC_PSI_HI 0
-#endif
-__host__ __device__ __forceinline__ uint32_t psi_pos(uint32_t e) {
-    return MKACC_PSI_HI ? e ^ ((e >> 5) & 31u) : e ^ ((e >> 5) & 3u);
-}
+__host__ __device__ __forceinline__ uint32_t psi_pos(uint32_t e) { return e ^ ((e >> 5) & 3u); }
 
 enum { XZW = 0, XZW_B = 1 };
 
@@ -94,7 +86,6 @@ struct StepArgs {
     const uint2* tw_fwd;       // [N] reference forward table (pass A, scalar reads)
     const uint2* tw_inv;       // [32] inverse pass-1 table (ntt_inv)
     uint32_t* dscr;            // [B][dg][N] C4 scratch of the step's d_i (mk_step_kernel DSCR) or null
-    const uint2* tab3;         // mk_step3_kernel: per-lane twiddle pairs (mkacc_layout2.hpp tables)
     uint32_t B, k, index;
     Mod m;
     SddConsts sd;
@@ -145,14 +136,13 @@ struct Mono {
         uint32_t a;
         asm volatile("v_add_u32 %0, %1, %2" : "=v"(a) : "s"(cs * (1024u * kBr5[r])), "v"(w));
         a &= 0x7fffu;
-        if (MKACC_PSI_HI) a ^= (a >> 5) & 0xf8u;   // 8 psi_pos(e) from 8 e
         return *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(psi) + a);
     }
 };
 __device__ __forceinline__ Mono make_mono(uint32_t c, uint32_t l) {
     const uint32_t o = ((__brev(l) >> 26) << 1) | 1u;   // 2 brv6(l) + 1
     const uint32_t co = __umul24(c, o) & (2u * kN - 1u);
-    return Mono{(MKACC_PSI_HI ? co : psi_pos(co)) << 3, c};
+    return Mono{psi_pos(co) << 3, c};
 }
 
 // Lazy Shoup product x*w in [0, 2Q) (x < 2^32)
@@ -166,8 +156,7 @@ __device__ __forceinline__ uint32_t mul_shoup_lazy(uint32_t x, uint2 w, uint32_t
 // (digit_range), effective key words from key_eff < kD Q, and the previous
 // accumulator joins the party sum as acc * (2^32 mod Q) < 2 Q^2 when it fits
 // (kAccInSum), otherwise it is added after the reduction.
-// CANON: the party sum's d-words are canonical (< Q): the d_i scratch reloads with
-// MKACC_DS_CANON (party_pass).
+// CANON: the party sum's d-words are canonical (< Q): the d_i scratch (party_pass).
 template <int DG, int METHOD, bool FIRST, bool CANON = false>
 struct Bounds {
     static constexpr int kG = DG > 4 ? 2 : 4;
@@ -229,22 +218,13 @@ __device__ __forceinline__ void digit_range(uint32_t (&x)[R], uint32_t Q) {
 // Key words of one 4-register group of a MAC: software-pipelined kPrefetch
 // groups ahead so the L2 latency of the step's key block overlaps the arithmetic.
 template <int DG>
-#ifndef MKACC_PF3
-#define MKACC_PF3 1
-#endif
-struct Prefetch { static constexpr int value = DG <= 3 ? MKACC_PF3 : 0; };
+struct Prefetch { static constexpr int value = DG <= 3 ? 1 : 0; };
 // accumulator loads: each gate's own rows, written by the previous step launch
-// (A/B switches: cache-policy bits of mk_step_kernel's accumulator loads / stores and of
-// its d_i scratch loads / stores; 0 = the default policy)
-#ifndef MKACC_ACC_AUX
-#define MKACC_ACC_AUX 0
-#endif
-#ifndef MKACC_DS_AUX
-#define MKACC_DS_AUX 0
-#endif
-template <int AUX = 0>
+// (default cache policy: non-temporal accumulator accesses cost 6 % and
+// non-temporal d_i scratch accesses 16 % per config-4 step,
+// profiles/r4/ab_c4_cpol.txt)
 __device__ __forceinline__ u32x4 aload4(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-    return __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, AUX);
+    return __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
 }
 // key-block loads (shared by every gate of the launch, streamed from L2)
 __device__ __forceinline__ u32x4 kload4(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
@@ -277,35 +257,22 @@ struct StepRes {
 // party of the step, so the first party pass computes it and stores it to the
 // gate's HBM scratch (DS = 1) and the later passes load it (DS = 2) instead of
 // the ev1'/ev2 words and the psi^e - 1 gathers; DS = 0 computes it per party.
-// MKACC_DS_CANON (default 2; 0 = A/B control) >= 1: the first pass stores the d_i scratch canonical (< Q), so the
-// reload passes other than the index party's (CANON) fit the previous accumulator into
-// the party sum (Bounds::kAccInSum at dg = 4): acc_u is read again at digit 0, shortly
-// after the rotation read, instead of after the last digit.  >= 2: the first pass sums
-// the canonical words too (CANON there as well).  >= 3 (A/B): the index party's pass
-// as well, whose sum then carries acc[index] into the f-part (f_part ACC_DONE).
-#ifndef MKACC_DS_CANON
-#define MKACC_DS_CANON 2
-#endif
+// The first pass stores the d_i scratch canonical (< Q), so the passes other than the
+// index party's (CANON) fit the previous accumulator into the party sum
+// (Bounds::kAccInSum at dg = 4): acc_u is read again at digit 0, shortly after the
+// rotation read, instead of after the last digit (+3.4 % at config 4,
+// profiles/r4/ab_c4_canon.txt; the index party's pass too measured the same, run v36).
 template <int DG, int METHOD, bool FIRST, bool START, int DS = 0, bool CANON = false>
 struct DigitMac {
     using Bd = Bounds<DG, METHOD, FIRST, CANON>;
     static_assert(DS == 0 || (METHOD == XZW && !FIRST), "d_i scratch: XZW steps after the first");
     static constexpr bool kAcc = START && Bd::kAccInSum;
-    // MKACC_MONO_PF=0 (A/B): gather X^(N-c) - 1 at use instead of with the key group
-#ifndef MKACC_MONO_PF
-#define MKACC_MONO_PF 1
-#endif
-    static constexpr bool kMonoPf = MKACC_MONO_PF && METHOD == XZW && !FIRST && DS != 2;
+    // X^(N-c) - 1 gathered with the key group
+    static constexpr bool kMonoPf = METHOD == XZW && !FIRST && DS != 2;
     // a d_i reload comes from HBM and frees the k2 / psi registers: prefetched
     // 3 groups ahead at DG <= 3, 2 at DG >= 4 (3 spill 10 VGPRs there); 1 group measured
     // 1-4% slower (profiles/r2/ab_dscr.txt)
-#ifndef MKACC_DSCR_PF
-#define MKACC_DSCR_PF 0
-#endif
-#ifndef MKACC_DSCR_WAIT
-#define MKACC_DSCR_WAIT 0
-#endif
-    static constexpr int kPrefetch = DS == 2 ? (MKACC_DSCR_PF ? MKACC_DSCR_PF : (DG <= 3 ? 3 : 2)) : Prefetch<DG>::value;
+    static constexpr int kPrefetch = DS == 2 ? (DG <= 3 ? 3 : 2) : Prefetch<DG>::value;
     static constexpr int kBuf = kPrefetch + 1;
     const StepRes& sr;
     uint32_t koff, poff, aoff, doff;
@@ -315,13 +282,13 @@ struct DigitMac {
     __device__ __forceinline__ void issue(KeyGroup& t, int gq) const {
         const uint32_t go = gq * 1024u;
         if (DS == 2)
-            t.k1 = aload4<MKACC_DS_AUX>(sr.rds, sr.vo, doff + go);   // d_i of the first party pass
+            t.k1 = aload4(sr.rds, sr.vo, doff + go);   // d_i of the first party pass
         else
             t.k1 = kload4(sr.rk1, sr.vo, koff + go);
         t.pk = kload4(sr.rpk, sr.vo, poff + go);
         if (METHOD == XZW && DS != 2) t.k2 = kload4(sr.rk2, sr.vo, koff + go);
         if (FIRST) t.ks = kload4(sr.rks, sr.vo, koff + go);
-        if (kAcc) t.acc = aload4<MKACC_ACC_AUX>(sr.rin, sr.vo, aoff + go);
+        if (kAcc) t.acc = aload4(sr.rin, sr.vo, aoff + go);
         if (kMonoPf) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) t.mono[e] = sr.mn.at(sr.psi, 4 * gq + e);
@@ -342,13 +309,13 @@ struct DigitMac {
                     DS == 2 ? t.k1[e]
                     : kMonoPf ? from3q<Bd::kD>(t.k1[e] + mul_shoup_lazy(t.k2[e], t.mono[e], Q), Q)   // = key_eff
                               : key_eff<METHOD, FIRST, Bd::kD>(t.k1[e], t.k2[e], t.ks[e], sr.psi, sr.mp, sr.mn, r, Q);
-                const uint32_t dc = (DS == 1 && MKACC_DS_CANON) ? from3q<1>(deff, Q) : deff;
+                const uint32_t dc = DS == 1 ? from3q<1>(deff, Q) : deff;
                 dv[e] = dc;
                 const uint64_t base = kAcc ? mad64(t.acc[e], sr.m.r32, 0) : (START ? 0ull : uj[r]);
                 uj[r] = mad64(g[r], (DS == 1 && CANON) ? dc : deff, base);
                 sv[r] = mad64(g[r], t.pk[e], sv[r]);
             }
-            if (DS == 1) bstore4<MKACC_DS_AUX>(dv, sr.rds, sr.vo, doff + gq * 1024u);
+            if (DS == 1) bstore4(dv, sr.rds, sr.vo, doff + gq * 1024u);
             sched_fence();
         }
     }
@@ -441,24 +408,20 @@ struct StepCtx {
 //   sv  += sum_i NTT(g_i) * P[u][i]
 // Party `index` is processed last (LAST): its lazy sum stays in registers
 // (`uj`, folded) and receives the f-part of HbProd before the single store.
-// MKACC_DSCR_ALT (default 1; 0 = A/B control): d_i reload passes (DS = 2) alternate the order of digits
-// 1..DG-1 (rev: DG-1 down to 1), so a pass starts its reloads with the digit the
-// previous pass read last (shorter reuse distance of the scratch lines in L2).
+// d_i reload passes (DS = 2) alternate the order of digits 1..DG-1 (rev: DG-1 down
+// to 1), so a pass starts its reloads with the digit the previous pass read last
+// (shorter reuse distance of the scratch lines in L2; +0.3 %, profiles/r4/ab_c4_alt.txt).
 // Every digit's products are the same exact lazy sums in another order: bit-exact.
-#ifndef MKACC_DSCR_ALT
-#define MKACC_DSCR_ALT 1
-#endif
 template <int DG, int METHOD, bool FIRST, bool LAST, int DS = 0>
 __device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_t (&sv)[kRegs],
                                            uint64_t (&uj)[kRegs], bool rev = false) {
-    constexpr bool kCanon = (!LAST || MKACC_DS_CANON >= 3) &&
-                            ((MKACC_DS_CANON >= 1 && DS == 2) || (MKACC_DS_CANON >= 2 && DS == 1));
+    constexpr bool kCanon = !LAST && DS != 0;
     using Bd = Bounds<DG, METHOD, FIRST, kCanon>;
     const uint32_t Q = s.m.Q, polyB = kN * 4u;
     uint32_t x[kRegs];
 #pragma unroll
     for (int gq = 0; gq < 8; ++gq) {
-        const u32x4 t = aload4<MKACC_ACC_AUX>(s.rin, s.vo, u * polyB + gq * 1024u);
+        const u32x4 t = aload4(s.rin, s.vo, u * polyB + gq * 1024u);
         x[4 * gq] = t.x; x[4 * gq + 1] = t.y; x[4 * gq + 2] = t.z; x[4 * gq + 3] = t.w;
     }
     if (!FIRST) {
@@ -486,16 +449,13 @@ __device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_
         KeyGroup kg[mac.kBuf];
         ntt_fwd(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, s.l, Q, s.m.m1);
         digit_range<DG>(x, Q);
-        // MKACC_DSCR_WAIT=1: the d_i scratch stores of the first pass are waited for
-        // here, just before the first reload, instead of right after that pass
-        if (DS == 2 && MKACC_DSCR_WAIT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
         for (int j = 0; j < mac.kPrefetch; ++j) mac.issue(kg[j], j);
         mac.run(x, uj, sv, kg);
     }
 #pragma unroll 1
     for (int i = 1; i < DG; ++i) {
-        const int j = (MKACC_DSCR_ALT && DS == 2 && rev) ? DG - i : i;
+        const int j = (DS == 2 && rev) ? DG - i : i;
 #pragma unroll
         for (int r = 0; r < kRegs; ++r) x[r] = pd.get(r, j + 1, s.sd);
         const DigitMac<DG, METHOD, FIRST, false, DS, kCanon> mac(sr, j, u);
@@ -516,7 +476,7 @@ __device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_
 #pragma unroll
     for (int gq = 0; gq < 8; ++gq) {
         u32x4 t;
-        if constexpr (!Bd::kAccInSum && !FIRST) t = aload4<MKACC_ACC_AUX>(s.rin, s.vo, u * polyB + gq * 1024u);
+        if constexpr (!Bd::kAccInSum && !FIRST) t = aload4(s.rin, s.vo, u * polyB + gq * 1024u);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const int r = 4 * gq + e;
@@ -527,13 +487,13 @@ __device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_
             }
             t[e] = v;
         }
-        bstore4<MKACC_ACC_AUX>(t, s.rout, s.vo, u * polyB + gq * 1024u);
+        bstore4(t, s.rout, s.vo, u * polyB + gq * 1024u);
     }
 }
 
 template <int DG, int METHOD, bool FIRST, bool DSCR>
 __device__ __forceinline__ void step_body(const StepCtx& s, uint32_t k, uint32_t index);
-template <int DG, int METHOD, bool FIRST, bool ACC_DONE = false>
+template <int DG, int METHOD, bool FIRST>
 __device__ __forceinline__ void f_part(const StepCtx& s, uint32_t index, uint64_t (&w)[kRegs], uint32_t (&x)[kRegs]);
 
 // DSCR: d_i computed once per step and gate (first party pass) and reloaded from
@@ -678,7 +638,7 @@ __device__ __forceinline__ void step_body(const StepCtx& s, uint32_t k, uint32_t
         grow_sv();
         t0 = 2;
         // the scratch stores complete before the later passes read them back
-        if (!MKACC_DSCR_WAIT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     for (uint32_t t = t0; t < k; ++t) {
         party_pass<DG, METHOD, FIRST, false, DSCR ? 2 : 0>(s, index + t < k ? index + t : index + t - k, sv, w,
@@ -689,24 +649,23 @@ __device__ __forceinline__ void step_body(const StepCtx& s, uint32_t k, uint32_t
     uint32_t x[kRegs];
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) x[r] = redc(sv[r], Q, s.m.qinv);
-    f_part<DG, METHOD, FIRST, MKACC_DS_CANON >= 3 && DSCR && Bounds<DG, METHOD, FIRST, true>::kAccInSum>(s, index, w, x);
+    f_part<DG, METHOD, FIRST>(s, index, w, x);
 }
 
 // Second half of HbProd for party `index` (mk-acc-xzw.cpp:272-289) and the
 // final store of acc[index]: w = its folded party sum (party_pass LAST),
 // x = sumV in [0, 2Q).  iNTT(sumV) -> SDD -> NTT -> acc[index] += <., f>.
-// ACC_DONE: the index party's sum already holds acc[index] (party_pass LAST with CANON)
-template <int DG, int METHOD, bool FIRST, bool ACC_DONE>
+template <int DG, int METHOD, bool FIRST>
 __device__ __forceinline__ void f_part(const StepCtx& s, uint32_t index, uint64_t (&w)[kRegs], uint32_t (&x)[kRegs]) {
     using Bd = Bounds<DG, METHOD, FIRST>;
     const uint32_t Q = s.m.Q;
     const uint32_t l = s.l;
     const uint32_t polyB = kN * 4u;
-    if constexpr (!Bd::kAccInSum && !FIRST && !ACC_DONE) {
+    if constexpr (!Bd::kAccInSum && !FIRST) {
         // acc[index] joins the f-part sum (Bounds: < 4 Q^2 with the folded party sum)
 #pragma unroll
         for (int gq = 0; gq < 8; ++gq) {
-            const u32x4 t = aload4<MKACC_ACC_AUX>(s.rin, s.vo, index * polyB + gq * 1024u);
+            const u32x4 t = aload4(s.rin, s.vo, index * polyB + gq * 1024u);
 #pragma unroll
             for (int e = 0; e < 4; ++e) w[4 * gq + e] = mad64(t[e], s.m.r32, w[4 * gq + e]);
         }
@@ -766,7 +725,7 @@ __device__ __forceinline__ void f_part(const StepCtx& s, uint32_t index, uint64_
             }
             t[e] = v;
         }
-        bstore4<MKACC_ACC_AUX>(t, s.rout, s.vo, ioff + gq * 1024u);
+        bstore4(t, s.rout, s.vo, ioff + gq * 1024u);
     }
 }
 
@@ -907,7 +866,6 @@ StepFn pick_step(int method, bool first, bool dscr) {
 
 #include "mkacc_step2.hpp"
 #include "mkacc_layout2.hpp"
-#include "mkacc_step3.hpp"
 
 template <int DG>
 StepFn pick_step2(int method, bool first) {
@@ -929,21 +887,13 @@ StepFn pick_lat(int method, bool first) {
 namespace mkacc_tu {
 using KernelPtr = const void*;
 #define MKACC_TU_API __attribute__((visibility("hidden")))
-MKACC_TU_API KernelPtr step_dg2(int method, bool first, bool dscr);
-MKACC_TU_API KernelPtr step_dg3(int method, bool first, bool dscr);
-MKACC_TU_API KernelPtr step_dg4(int method, bool first, bool dscr);
+MKACC_TU_API KernelPtr step_dg4(int method, bool first, bool dscr);   // mk_step_kernel (dg >= 4)
 MKACC_TU_API KernelPtr step_dg5(int method, bool first, bool dscr);
-MKACC_TU_API KernelPtr step2_dg2(int method, bool first);   // mk_step2_kernel (mkacc_step2.hpp)
+MKACC_TU_API KernelPtr step2_dg2(int method, bool first);   // mk_step2_kernel (mkacc_step2.hpp, dg <= 3)
 MKACC_TU_API KernelPtr step2_dg3(int method, bool first);
-MKACC_TU_API KernelPtr step2_dg4(int method, bool first);
-MKACC_TU_API KernelPtr step3_dg2(int method, bool first);   // mk_step3_kernel (mkacc_step3.hpp)
-MKACC_TU_API KernelPtr step3_dg3(int method, bool first);
-MKACC_TU_API KernelPtr step3_dg4(int method, bool first);
 MKACC_TU_API KernelPtr lat_dg2(int method, bool first);
 MKACC_TU_API KernelPtr lat_dg3(int method, bool first);
 MKACC_TU_API KernelPtr lat_dg4(int method, bool first);
 MKACC_TU_API KernelPtr wide_step(int method, bool first);     // mkacc_wide.hpp (integer 64-bit words)
-MKACC_TU_API KernelPtr widefp_step(int method, bool first);   // mkacc_widefp.hpp (FP64, Q < 2^50)
-MKACC_TU_API KernelPtr widereg_step(int method, bool first);  // mkacc_widereg.hpp (FP64, register-resident)
-MKACC_TU_API KernelPtr widereg2_step(int method, bool first);  // mkacc_widereg2.hpp (FP64, two waves per gate)
+MKACC_TU_API KernelPtr widereg2_step(int method, bool first);  // mkacc_widereg2.hpp (FP64, Q < 2^50)
 }  // namespace mkacc_tu

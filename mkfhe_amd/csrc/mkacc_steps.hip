@@ -1,41 +1,29 @@
 // mkacc_steps.hip -- kernel translation units of the engine library.  The
 // build (mkfhe_amd/build.py) compiles this file once per unit, in parallel:
-//   -DMKACC_TU_DG=d -DMKACC_TU_PART=0   mk_step_kernel instantiations of digit count d
-//   -DMKACC_TU_DG=d -DMKACC_TU_PART=1   mk_lat_kernel instantiations of digit count d
-//   -DMKACC_TU_DG=d -DMKACC_TU_PART=2   mk_step2_kernel instantiations of digit count d
-//   -DMKACC_TU_WIDE=1 / 2 / 3          64-bit word step kernels (integer / FP64 / FP64 register-resident)
+//   -DMKACC_TU_DG=d -DMKACC_TU_PART=0   mk_step_kernel instantiations of digit count d (4, 5)
+//   -DMKACC_TU_DG=d -DMKACC_TU_PART=1   mk_lat_kernel instantiations of digit count d (2..4)
+//   -DMKACC_TU_DG=d -DMKACC_TU_PART=2   mk_step2_kernel instantiations of digit count d (2, 3)
+//   -DMKACC_TU_WIDE=1 / 2               64-bit word step kernels (integer / FP64 register-resident)
 // and the host unit (mkacc_engine.hip) launches them through mkacc_tu.
 #include "mkacc_kernels.hpp"
 
 #if defined(MKACC_TU_WIDE)
 #include "mkacc_wide.hpp"
-#include "mkacc_widefp.hpp"
-#if MKACC_TU_WIDE == 3
-#include "mkacc_widereg.hpp"
+#if MKACC_TU_WIDE == 2
+#include "mkacc_fp64.hpp"
 #include "mkacc_widereg2.hpp"
 #endif
 namespace mkacc_tu {
-#if MKACC_TU_WIDE == 3
-KernelPtr widereg_step(int method, bool first) {
-    if (method == XZW)
-        return first ? (KernelPtr)widereg::step_kernel<XZW, true> : (KernelPtr)widereg::step_kernel<XZW, false>;
-    return first ? (KernelPtr)widereg::step_kernel<XZW_B, true> : (KernelPtr)widereg::step_kernel<XZW_B, false>;
-}
+#if MKACC_TU_WIDE == 2
 KernelPtr widereg2_step(int method, bool first) {
     if (method == XZW)
         return first ? (KernelPtr)widereg2::step_kernel<XZW, true> : (KernelPtr)widereg2::step_kernel<XZW, false>;
     return first ? (KernelPtr)widereg2::step_kernel<XZW_B, true> : (KernelPtr)widereg2::step_kernel<XZW_B, false>;
 }
-#elif MKACC_TU_WIDE == 1
+#else
 KernelPtr wide_step(int method, bool first) {
     if (method == XZW) return first ? (KernelPtr)wide::step_kernel<XZW, true> : (KernelPtr)wide::step_kernel<XZW, false>;
     return first ? (KernelPtr)wide::step_kernel<XZW_B, true> : (KernelPtr)wide::step_kernel<XZW_B, false>;
-}
-#else
-KernelPtr widefp_step(int method, bool first) {
-    if (method == XZW)
-        return first ? (KernelPtr)widefp::step_kernel<XZW, true> : (KernelPtr)widefp::step_kernel<XZW, false>;
-    return first ? (KernelPtr)widefp::step_kernel<XZW_B, true> : (KernelPtr)widefp::step_kernel<XZW_B, false>;
 }
 #endif
 }  // namespace mkacc_tu
@@ -52,13 +40,9 @@ KernelPtr MKACC_CAT(step_dg, MKACC_TU_DG)(int method, bool first, bool dscr) {
 KernelPtr MKACC_CAT(lat_dg, MKACC_TU_DG)(int method, bool first) {
     return (KernelPtr)pick_lat<MKACC_TU_DG>(method, first);
 }
-#elif MKACC_TU_PART == 2
+#else
 KernelPtr MKACC_CAT(step2_dg, MKACC_TU_DG)(int method, bool first) {
     return (KernelPtr)pick_step2<MKACC_TU_DG>(method, first);
-}
-#else
-KernelPtr MKACC_CAT(step3_dg, MKACC_TU_DG)(int method, bool first) {
-    return (KernelPtr)pick_step3<MKACC_TU_DG>(method, first);
 }
 #endif
 }  // namespace mkacc_tu

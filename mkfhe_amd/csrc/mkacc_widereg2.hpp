@@ -1,15 +1,15 @@
 // mkacc_widereg2.hpp -- config-5 FP64 step kernel with TWO waves per gate
-// (Q < 2^50; SURVEY.md s8 config 5 stress).  Included after mkacc_widereg.hpp,
+// (Q < 2^50; SURVEY.md s8 config 5 stress).  Included after mkacc_fp64.hpp,
 // whose exact FP64 product, bound plans and butterfly it uses.
 //
-// widereg::step_kernel keeps a whole gate in one wave: 32 doubles per lane for
-// each of the offset words, the digit NTT, uj, sumV and X^-c fill the 512-entry
-// register file, so it runs ONE wave per SIMD, and a single FP64 instruction
-// stream reaches only ~70-78 % of the issue rate even with 16 independent
-// products in flight (tools/ubench_dp_ilp.hip, profiles/r4/ubench_dp_ilp.txt;
-// two waves per SIMD: 83-91 %).  Here a gate is split over two waves of one
-// 128-thread workgroup, 16 doubles per lane each, so the per-wave state halves
-// and two waves share a SIMD.
+// One wave per gate (round 4's widereg::step_kernel, retired in round 5; git
+// history) needs 32 doubles per lane for each of the offset words, the digit NTT,
+// uj, sumV and X^-c -- the whole 512-entry register file, ONE wave per SIMD, and a
+// single FP64 instruction stream reaches only ~70-78 % of the issue rate even
+// with 16 independent products in flight (tools/ubench_dp_ilp.hip,
+// profiles/r4/ubench_dp_ilp.txt; two waves per SIMD: 83-91 %).  Here a gate is
+// split over two waves of one 128-thread workgroup, 16 doubles per lane each, so
+// the per-wave state halves and two waves share a SIMD.
 //
 // A transform is still three register passes and two LDS transposes: one across
 // the gate's two waves (s_barrier of the 2-wave workgroup, two ping-pong buffers),
@@ -35,15 +35,15 @@ namespace {
 
 namespace widereg2 {
 
-using widefp::FMod;
-using widefp::mm;
-using widefp::red;
-using widereg::bfly;
-using widereg::FPlan;
-using widereg::kLim;
-using widereg::kRedB;
-using widereg::tbound;
-using widereg::make_plan;
+using fp64::FMod;
+using fp64::mm;
+using fp64::red;
+using fp64::bfly;
+using fp64::FPlan;
+using fp64::kLim;
+using fp64::kRedB;
+using fp64::tbound;
+using fp64::make_plan;
 
 using lay2::kR;
 using lay2::Lane;
@@ -57,17 +57,12 @@ using lay2::tload;
 using lay2::transpose;
 using lay2::transpose_local;
 using Bufs = lay2::Bufs<double>;
-// 1: the LB -> LC and LC -> LD transposes stay inside each wave (no barrier); 0 (A/B):
-// every transpose crosses the 2-wave barrier
-#ifndef MKACC_WREG2_LOCAL
-#define MKACC_WREG2_LOCAL 1
-#endif
+// the LB -> LC and LC -> LD transposes stay inside each wave (no barrier; every
+// transpose crossing the barrier measured 351-352 against 349-350 us per config-5
+// launch, profiles/r4/ab_c5_widereg2.txt)
 template <int SRC, int DST>
 __device__ __forceinline__ void transpose2(double (&x)[kR], Bufs& b, uint32_t l, uint32_t w) {
-    if constexpr (MKACC_WREG2_LOCAL)
-        transpose_local<SRC, DST>(x, b.cur(), l, w);
-    else
-        transpose<SRC, DST>(x, b.cross(), l, w);
+    transpose_local<SRC, DST>(x, b.cur(), l, w);
 }
 using lay2::TFB;
 using lay2::TFC;
@@ -141,8 +136,8 @@ constexpr InvPlan1 make_inv1(int x0, int thr) {
 constexpr InvPlan1 kInv1 = make_inv1(1140, 1200);
 constexpr FPlan kInv23 = make_plan(kInv1.out, 4, 11);
 static_assert(kInv23.out <= 8000, "inverse bounds (the twist product needs |x| <= 8 Q)");
-using widereg::kFwd;
-using widereg::kFwdDig;
+using fp64::kFwd;
+using fp64::kFwdDig;
 
 typedef const __attribute__((address_space(4))) double const_f64;
 __device__ __forceinline__ const_f64* opaque_c(const double* p) {
@@ -297,7 +292,7 @@ struct StepArgs {
     const double* twf;        // forward table, reference order (pass A2 reads [1, 16))
     const double* tis;        // inverse pass-1 table [(1 << b) + t]
     uint32_t B, k, index, dg;
-    double cL, Cm;            // widereg::offset_word constants
+    double cL, Cm;            // fp64::offset_word constants
     FMod m;
     wide::Sdd64 sd;
 };
@@ -306,10 +301,7 @@ struct StepArgs {
 // first kPf issued before the digit's NTT).  1: spill-free at 2 waves per SIMD; 2
 // spilled 3 VGPRs and measured the same (362.3 against 362.8 us per config-5
 // launch, profiles/r4/ab_c5_widereg2.txt): the other wave on the SIMD hides the loads
-#ifndef MKACC_WREG2_PF
-#define MKACC_WREG2_PF 1
-#endif
-constexpr int kPf = MKACC_WREG2_PF;
+constexpr int kPf = 1;
 struct KGrp {
     u32x4 a1, a2, as, ap;
 };
@@ -326,7 +318,7 @@ __device__ __forceinline__ void kissue(KGrp& t, const KeySrc& k, int gq) {
     if (!F) t.ap = bload4(k.rpk, k.vo, k.po + so);
 }
 
-// One digit's MAC (widereg::mac with 16 slots): party (F = false): uj += g d_i,
+// One digit's MAC: party (F = false): uj += g d_i,
 // sv += g P[u][i]; f-part (F = true): uj += g f_i.  g reduced first (|g| <= Q/2 + 2).
 template <int METHOD, bool FIRST, bool F>
 __device__ __forceinline__ void mac(const double (&g)[kR], double (&uj)[kR], double (&sv)[kR], const double (&mn)[kR],
@@ -342,7 +334,7 @@ __device__ __forceinline__ void mac(const double (&g)[kR], double (&uj)[kR], dou
             const double k2 = METHOD == XZW ? __builtin_bit_cast(double, h ? u32x2{t.a2.z, t.a2.w} : u32x2{t.a2.x, t.a2.y}) : 0.0;
             const double kst = FIRST ? __builtin_bit_cast(double, h ? u32x2{t.as.z, t.as.w} : u32x2{t.as.x, t.as.y}) : 0.0;
             const double gr = red(g[r], m);
-            const double d = widefp::key_eff<METHOD, FIRST>(k1, k2, kst, FIRST ? mcv[r] : 0.0, METHOD == XZW ? mn[r] : 0.0, m);
+            const double d = fp64::key_eff<METHOD, FIRST>(k1, k2, kst, FIRST ? mcv[r] : 0.0, METHOD == XZW ? mn[r] : 0.0, m);
             uj[r] = __dadd_rn(uj[r], mm(gr, d, m));
             if (!F) {
                 const double pk = __builtin_bit_cast(double, h ? u32x2{t.ap.z, t.ap.w} : u32x2{t.ap.x, t.ap.y});
@@ -352,18 +344,21 @@ __device__ __forceinline__ void mac(const double (&g)[kR], double (&uj)[kR], dou
     }
 }
 
-// iNTT(x) -> offset words -> per digit: NTT, MAC (widereg::digits_pass)
+// iNTT(x) -> offset words -> per digit: NTT, MAC.  uj / sv reduced every kRedEvery
+// digits and at the end: from |.| <= Q/2 + 2, a later step's products stay below
+// 0.78 Q (d_i, |d| <= 1.13 Q) and 0.63 Q (P), so seven digits keep the sums below
+// 6 Q; the first step's d_i (<= 2.75 Q) gives 1.19 Q per product: four digits.
 template <int METHOD, bool FIRST, bool F>
 __device__ __forceinline__ void digits_pass(double (&x)[kR], double (&uj)[kR], double (&sv)[kR], const double (&mn)[kR],
                                             const double (&mcv)[kR], const StepArgs& a, Bufs& bufs,
                                             __amdgpu_buffer_rsrc_t rt, const Lane& ln, const KeySrc& ks0, uint32_t u) {
     const FMod& m = a.m;
     constexpr uint32_t polyB = kN * 8u;
-    constexpr uint32_t kRedEvery = FIRST ? 4u : 7u;   // widereg::digits_pass bounds
+    constexpr uint32_t kRedEvery = FIRST ? 4u : 7u;
     ntt_inv(x, bufs, a.tis, rt, ln, m);
     uint64_t D[kR];
 #pragma unroll
-    for (int r = 0; r < kR; ++r) D[r] = widereg::offset_word(x[r], m, a.cL, a.Cm);
+    for (int r = 0; r < kR; ++r) D[r] = fp64::offset_word(x[r], m, a.cL, a.Cm);
 #pragma unroll 1
     for (uint32_t i = 0; i < a.dg; ++i) {
         KeySrc ks = ks0;
@@ -375,7 +370,7 @@ __device__ __forceinline__ void digits_pass(double (&x)[kR], double (&uj)[kR], d
         sched_fence();
         double g[kR];
 #pragma unroll
-        for (int r = 0; r < kR; ++r) g[r] = widereg::digit_of(D[r], i + 1, a.sd);
+        for (int r = 0; r < kR; ++r) g[r] = fp64::digit_of(D[r], i + 1, a.sd);
         ntt_fwd<kFwdDig>(g, bufs, a.twf, rt, ln, m);
         mac<METHOD, FIRST, F>(g, uj, sv, mn, mcv, kq, ks, m);
         if (i % kRedEvery == kRedEvery - 1) {
@@ -394,7 +389,7 @@ __device__ __forceinline__ void digits_pass(double (&x)[kR], double (&uj)[kR], d
 }
 
 // One accumulator step of gate `gate`, this wave's half of every polynomial
-// (widereg::one_gate: HbProd, mk-acc-xzw.cpp:231-290, fused with AddToAccXZW{,0},
+// (HbProd, mk-acc-xzw.cpp:231-290, fused with AddToAccXZW{,0},
 // xzw.cpp:292-381; parties index + 1, ..., index, the index party's sum kept for
 // the f-part).
 template <int METHOD, bool FIRST>
@@ -467,11 +462,11 @@ __global__ __launch_bounds__(128, 2) void ntt_fwd_kernel(const uint64_t* __restr
     const uint64_t* src = in + (size_t)blockIdx.x * kN;
     double x[kR];
 #pragma unroll
-    for (int r = 0; r < kR; ++r) x[r] = widefp::balanced(src[pos_a(w, l, r)], m);
+    for (int r = 0; r < kR; ++r) x[r] = fp64::balanced(src[pos_a(w, l, r)], m);
     Bufs bufs{smem, 0u};
     ntt_fwd<kFwd>(x, bufs, twf, make_rsrc(tab, kTabD * 8u), ln, m);
 #pragma unroll
-    for (int r = 0; r < kR; ++r) out[(size_t)blockIdx.x * kN + pos_c(w, l, r)] = widefp::canon(x[r], m);
+    for (int r = 0; r < kR; ++r) out[(size_t)blockIdx.x * kN + pos_c(w, l, r)] = fp64::canon(x[r], m);
 }
 __global__ __launch_bounds__(128, 2) void ntt_inv_kernel(const uint64_t* __restrict__ in, uint64_t* __restrict__ out,
                                                          const double* tab, const double* tis, FMod m) {
@@ -481,14 +476,15 @@ __global__ __launch_bounds__(128, 2) void ntt_inv_kernel(const uint64_t* __restr
     const uint64_t* src = in + (size_t)blockIdx.x * kN;
     double x[kR];
 #pragma unroll
-    for (int r = 0; r < kR; ++r) x[r] = widefp::balanced(src[pos_c(w, l, r)], m);
+    for (int r = 0; r < kR; ++r) x[r] = fp64::balanced(src[pos_c(w, l, r)], m);
     Bufs bufs{smem, 0u};
     ntt_inv(x, bufs, tis, make_rsrc(tab, kTabD * 8u), ln, m);
 #pragma unroll
-    for (int r = 0; r < kR; ++r) out[(size_t)blockIdx.x * kN + pos_a(w, l, r)] = widefp::canon(x[r], m);
+    for (int r = 0; r < kR; ++r) out[(size_t)blockIdx.x * kN + pos_a(w, l, r)] = fp64::canon(x[r], m);
 }
 
-// batch prologue / epilogue with the C16 permutation (widereg::to_c8_kernel's contract)
+// batch prologue / epilogue with the C16 permutation: canonical u64 words (reference
+// EVAL order) <-> balanced doubles (C16); a word >= Q raises `bad` and reads as 0
 __global__ void to_c16_kernel(const uint64_t* __restrict__ in, double* __restrict__ out, size_t count, FMod m,
                               uint64_t Q, uint32_t* __restrict__ bad) {
     const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -499,13 +495,13 @@ __global__ void to_c16_kernel(const uint64_t* __restrict__ in, double* __restric
         x = 0;
     }
     const size_t poly = idx / kN;
-    out[poly * kN + c16_index((uint32_t)(idx % kN))] = widefp::balanced(x, m);
+    out[poly * kN + c16_index((uint32_t)(idx % kN))] = fp64::balanced(x, m);
 }
 __global__ void from_c16_kernel(const double* __restrict__ in, uint64_t* __restrict__ out, size_t count, FMod m) {
     const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= count) return;
     const size_t poly = idx / kN;
-    out[idx] = widefp::canon(in[poly * kN + c16_index((uint32_t)(idx % kN))], m);
+    out[idx] = fp64::canon(in[poly * kN + c16_index((uint32_t)(idx % kN))], m);
 }
 
 }  // namespace widereg2

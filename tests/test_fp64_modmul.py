@@ -1,5 +1,5 @@
 """Host check of the exact FP64 modular product of the 64-bit word path's FP64
-kernels (mkfhe_amd/csrc/mkacc_widefp.hpp): tools/fp64_modmul_check.c compares
+kernels (mkfhe_amd/csrc/mkacc_fp64.hpp): tools/fp64_modmul_check.c compares
 mm(a, b) = fma(-q, Q, h) + l with the __int128 value a*b - q*Q over random and
 corner operands at the operand bounds the kernels rely on (|a b| <= 4 Q^2),
 at the config-5 modulus and near 2^50 (CPU, IEEE binary64 as on the GPU)."""

@@ -78,7 +78,7 @@ CASES = [
     ("XZW", 16, 2, 45181, 1 << 5, 2),     # STD128_MKNTRU_4 shape: 16 parties, dg=5
     ("XZW_B", 16, 2, 32749, 1 << 7, 3),   # STD128_MKNTRU_LWE_4 shape: 16 parties, dg=3
     ("XZW", 8, 3, 45181, 1 << 6, 2),      # STD128_MKNTRU_3 shape (config 4): 8 parties, dg=4
-    ("XZW_B", 3, 3, 32749, 1 << 6, 3),    # dg=4, binary keys (mk_step2_kernel's unsplit halves)
+    ("XZW_B", 3, 3, 32749, 1 << 6, 3),    # dg=4, binary keys
 ]
 
 
@@ -125,28 +125,23 @@ def test_evalacc_dscr_modes(mk, oracle, case, dscr, monkeypatch):
     assert np.array_equal(got, exp.astype(np.uint32))
 
 
-@pytest.mark.parametrize("step", ["1", "2", "3"])
 @pytest.mark.parametrize("case", CASES, ids=[f"{c[0]}-k{c[1]}-logB{c[4].bit_length() - 1}" for c in CASES])
-def test_evalacc_step_kernels(mk, oracle, case, step, monkeypatch):
-    """The batch step kernels -- mk_step_kernel (1), mk_step2_kernel (2, digit
-    NTTs first, one key stream per pass) and mk_step3_kernel (3, the same with a
-    gate split over two waves); 2 and 3 are built for dg <= 4 -- give the oracle's
-    accumulators for every case shape; MKACC_STEP is read when the context is
-    created (it sizes the workspace), MKACC_LAT=0 keeps small batches off the
+def test_evalacc_step_kernels(mk, oracle, case, monkeypatch):
+    """The batch step kernel the engine selects -- mk_step2_kernel (digit NTTs
+    first, one key stream per pass) at dg <= 3, mk_step_kernel at dg >= 4 --
+    gives the oracle's accumulators for every case shape, with the monomial edge
+    cases in the first and last gate; MKACC_LAT=0 keeps small batches off the
     one-wave-per-party kernel."""
     meth, k, n, q, baseG, B = case
-    monkeypatch.setenv("MKACC_STEP", step)
     monkeypatch.setenv("MKACC_LAT", "0")
     om = oracle.XZW if meth == "XZW" else oracle.XZW_B
     em = mk.MKNTRU if meth == "XZW" else mk.MKNTRU_LWE
-    orc, evk, pkey, ct, acc = make_case(oracle, om, k, n, q, baseG, B + 3, seed=k * 17 + n + int(step))
+    orc, evk, pkey, ct, acc = make_case(oracle, om, k, n, q, baseG, B + 3, seed=k * 17 + n + 2)
     ct[0, 0, 0] = 0
     ct[-1, k - 1, n - 1] = q - 1 if om == oracle.XZW else 4096
     exp = orc.evalacc_batch(evk, pkey, ct, acc, 8)
     eng = mk.MKAccumulatorEngine(mk.make_params(em, k, n, 2048, Q_MK, q, baseG))
-    dg = eng.dg
-    names = {"1": "mk_step_kernel", "2": "mk_step2_kernel", "3": "mk_step3_kernel"}
-    assert eng.step_kernel_name(B + 3) == (names[step] if dg <= 4 else "mk_step_kernel")
+    assert eng.step_kernel_name(B + 3) == ("mk_step2_kernel" if eng.dg <= 3 else "mk_step_kernel")
     eng.upload_keys(evk.astype(np.uint32), pkey.astype(np.uint32))
     got = eng.eval_batch(ct.astype(np.uint32), acc.astype(np.uint32))
     assert np.array_equal(got, exp.astype(np.uint32))
@@ -253,23 +248,30 @@ def test_evalacc_many_gates_every_wave_slot(mk, oracle, lat, monkeypatch):
         assert not bad, f"gates differing from the oracle: {bad[:16]}"
 
 
+# (k, n, log2 B_g): the headline kernel's shape (mk_step2_kernel, dg = 3) and the
+# config-4 kernel's (mk_step_kernel with its d_i scratch, k >= 4, dg = 4)
+SPLIT_SHAPES = {"step2-k2-dg3": (2, 3, 7), "dscr-k4-dg4": (4, 2, 6)}
+
+
 @pytest.mark.parametrize("streams", ["2", "3", "4"])
-@pytest.mark.parametrize("step", ["1", "2"])
-def test_two_stream_batch_split(mk, oracle, step, streams, monkeypatch):
+@pytest.mark.parametrize("shape", list(SPLIT_SHAPES))
+def test_two_stream_batch_split(mk, oracle, shape, streams, monkeypatch):
     """MKACC_STREAMS=2..4 cuts a batch of two or more units of resident gates into
     slices whose step launches run on streams of their own: the output equals the
-    one-stream run word for word, and a spread sample across the slices equals the
-    oracle.  B = 4100 (units of 1024 gates at 256 CUs): 2048 + 2052, 1024 + 1024 +
-    2052, 1024 x 3 + 1028."""
-    monkeypatch.setenv("MKACC_STEP", step)
+    one-stream run word for word, and a spread sample across the slice boundaries
+    equals the oracle.  B = 4100 (units of 1024 gates at 256 CUs): 2048 + 2052,
+    1024 + 1024 + 2052, 1024 x 3 + 1028.  Both default batch kernels: the config-4
+    one reads its per-gate d_i scratch at the slice's gate offset."""
+    k, n, logb = SPLIT_SHAPES[shape]
     monkeypatch.setenv("MKACC_LAT", "0")
-    k, n, q, baseG, B = 2, 3, 45181, 1 << 9, 4100
-    orc, evk, pkey, ct, acc = make_case(oracle, oracle.XZW, k, n, q, baseG, B, seed=91 + int(step))
+    q, baseG, B = 45181, 1 << logb, 4100
+    orc, evk, pkey, ct, acc = make_case(oracle, oracle.XZW, k, n, q, baseG, B, seed=91 + k)
     params = mk.make_params(mk.MKNTRU, k, n, 2048, Q_MK, q, baseG)
     outs = {}
     for ns in ("1", streams):
         monkeypatch.setenv("MKACC_STREAMS", ns)
         eng = mk.MKAccumulatorEngine(params)
+        assert eng.step_kernel_name(B) == ("mk_step2_kernel" if k == 2 else "mk_step_kernel")
         eng.upload_keys(evk.astype(np.uint32), pkey.astype(np.uint32))
         outs[ns] = eng.eval_batch(ct.astype(np.uint32), acc.astype(np.uint32))
         del eng

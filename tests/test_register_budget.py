@@ -67,11 +67,9 @@ BUDGET = [
     (r"mk_step2_kernel<3, 1, true>", 256, 2),
     (r"mk_lat_kernel<\d, [01], (true|false)>", 256, 2),  # small-batch kernel, every digit count
     (r"mk_step_kernel<4, 0, false, true>", 256, 2),      # config-4 step (dg = 4, d_i scratch; spill-free since
-                                                          # the alternating reload order, MKACC_DSCR_ALT)
-    (r"widereg2::step_kernel<[01], false>", 256, 2),     # config-5 FP64 step, two waves per gate (default)
-    (r"widereg::step_kernel<[01], (true|false)>", 256, 1),  # ... one wave per gate (MKACC_WREG2=0; + AGPRs)
-    (r"widefp::step_kernel<[01], (true|false)>", 128, 4),  # config-5 FP64 step: 4 workgroups per CU
-    (r"wide::step_kernel<[01], (true|false)>", 128, 4),    # 64-bit integer step
+                                                          # the alternating reload order)
+    (r"widereg2::step_kernel<[01], false>", 256, 2),     # config-5 FP64 step, two waves per gate
+    (r"wide::step_kernel<[01], (true|false)>", 128, 4),    # 64-bit integer step (2^50 <= Q < 2^61)
     (r"extract_kernel|ks_mntru_kernel|ks_mklwe_kernel|mntru_head_kernel|mklwe_head_kernel", 256, 2),
 ]
 

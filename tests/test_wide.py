@@ -76,9 +76,8 @@ def test_wide_evalacc_bitexact(mk_gpu, oracle, method, k, n, baseG, B):
     assert np.array_equal(got, exp), int(np.count_nonzero(got != exp))
 
 
-# variant -> (MKACC_WIDE_FP, MKACC_WFP_REG, MKACC_WREG2, step kernel)
-VARIANTS = {"reg2": ("1", "1", "1", "widereg2::step_kernel"), "reg": ("1", "1", "0", "widereg::step_kernel"),
-            "lds": ("1", "0", "1", "widefp::step_kernel"), "int": ("0", "1", "1", "wide::step_kernel")}
+# variant -> (MKACC_WIDE_FP, step kernel)
+VARIANTS = {"fp64": ("1", "widereg2::step_kernel"), "int": ("0", "wide::step_kernel")}
 
 
 @pytest.mark.gpu
@@ -86,19 +85,16 @@ VARIANTS = {"reg2": ("1", "1", "1", "widereg2::step_kernel"), "reg": ("1", "1", 
 @pytest.mark.parametrize("method", ["XZW", "XZW_B"])
 def test_wide_fp64_and_integer_variants(mk_gpu, oracle, monkeypatch, method, variant):
     """Q < 2^50 runs the register-resident FP64 kernel with two waves per gate
-    (mkacc_widereg2.hpp) unless MKACC_WREG2=0 selects the one-wave form
-    (mkacc_widereg.hpp), MKACC_WFP_REG=0 the LDS-tile FP64 kernel
-    (mkacc_widefp.hpp) or MKACC_WIDE_FP=0 the integer kernels: all bit-exact.  The first step's digit
+    (mkacc_widereg2.hpp) unless MKACC_WIDE_FP=0 selects the integer kernels
+    (mkacc_wide.hpp, the path above 2^50): both bit-exact.  The first step's digit
     decomposition sees chosen coefficients (acc = NTT(coefficients)): 0, 1,
     Q-1 and the centring boundary Q>>1, (Q>>1)+1 where the FP64 path picks the
     reference's representative explicitly; keys include all-maximal and
     balanced-boundary words.  (The device-pointer key upload of this path is
     exercised by every bench.py --q-bits 50 run, whose oracle check covers it.)"""
     mk = mk_gpu
-    fp, reg, reg2, kname = VARIANTS[variant]
+    fp, kname = VARIANTS[variant]
     monkeypatch.setenv("MKACC_WIDE_FP", fp)
-    monkeypatch.setenv("MKACC_WFP_REG", reg)
-    monkeypatch.setenv("MKACC_WREG2", reg2)
     m = oracle.XZW if method == "XZW" else oracle.XZW_B
     k, n, B = 2, 3, 3
     orc, evk, pkey, ct, acc = make_case(oracle, m, k, n, 45181, 1 << 10, B, seed=50 + len(method), Q=Q50)
@@ -125,24 +121,29 @@ def test_wide_fp64_and_integer_variants(mk_gpu, oracle, monkeypatch, method, var
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("reg2", ["1", "0"])
+@pytest.mark.parametrize("streams", ["2", "3"])
 @pytest.mark.parametrize("method", ["XZW", "XZW_B"])
-def test_wide_register_kernel_loops_over_gates(mk_gpu, oracle, monkeypatch, method, reg2):
-    """The register-resident FP64 kernels loop over the batch (one wave per gate:
-    one workgroup of four gates per CU; two waves per gate: four 2-wave
-    workgroups per CU): a batch of more than 4 x 256 gates (and not a multiple
-    of four) takes the loop; every gate equals the single-gate result, and a
-    spread sample of them equals the oracle."""
+def test_wide_register_kernel_loops_and_slices(mk_gpu, oracle, monkeypatch, method, streams):
+    """The FP64 kernel's four 2-wave workgroups per CU loop over their slice of
+    the batch, and a batch of two or more units of CUs x 4 gates is cut into
+    MKACC_STREAMS slices on streams of their own (wide_launch_batch).  B = 4101
+    (not a multiple of four): the sliced run equals the one-stream run word for
+    word, a spread sample across the slice boundaries equals the oracle, and the
+    last gates equal a separate small batch."""
     mk = mk_gpu
-    monkeypatch.setenv("MKACC_WREG2", reg2)
     m = oracle.XZW if method == "XZW" else oracle.XZW_B
-    k, n, B = 2, 2, 1031
+    k, n, B = 2, 2, 4101
     orc, evk, pkey, ct, acc = make_case(oracle, m, k, n, 45181, 1 << 10, B, seed=61 + len(method), Q=Q50)
-    eng = _eng(mk, mk.MKNTRU if method == "XZW" else mk.MKNTRU_LWE, k, n, Q50, 45181, 1 << 10)
-    assert eng.step_kernel_name(B) == ("widereg2::step_kernel" if reg2 == "1" else "widereg::step_kernel")
-    eng.upload_keys(evk.astype(np.uint64), pkey.astype(np.uint64))
-    got = eng.eval_batch(ct.astype(np.uint32), acc.astype(np.uint64))
-    pick = [0, 1, 2, 3, 511, 1023, 1024, 1030]
+    outs = {}
+    for ns in ("1", streams):
+        monkeypatch.setenv("MKACC_STREAMS", ns)
+        eng = _eng(mk, mk.MKNTRU if method == "XZW" else mk.MKNTRU_LWE, k, n, Q50, 45181, 1 << 10)
+        assert eng.step_kernel_name(B) == "widereg2::step_kernel"
+        eng.upload_keys(evk.astype(np.uint64), pkey.astype(np.uint64))
+        outs[ns] = eng.eval_batch(ct.astype(np.uint32), acc.astype(np.uint64))
+    got = outs[streams]
+    assert np.array_equal(outs["1"], got)
+    pick = [0, 1, 2, 3, 1023, 1024, 2047, 2048, 3071, 3072, 4100]
     exp = orc.evalacc_batch(evk, pkey, ct[pick], acc[pick], 8)
     assert np.array_equal(got[pick], exp)
     one = eng.eval_batch(ct[-3:].astype(np.uint32), acc[-3:].astype(np.uint64))
