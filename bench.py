@@ -58,11 +58,11 @@ REF_CPU_S_PER_EVALACC = {            # reference EvalAcc, 1 core of the survey c
     "STD100_MKNTRU": 0.274, "STD128_MKNTRU": 0.475, "STD100_MKNTRU_LWE": 0.215,
     "STD100_MKNTRU_LWE_2": 0.721, "STD128_MKNTRU_3": 6.750, "STD100_MKNTRU_3": 2.872}
 # oracle / reference single-thread EvalAcc time, read from the calibration record
-# (tools/oracle_calib.py -> profiles/r4/oracle_calibration.json).  A
+# (tools/oracle_calib.py -> profiles/oracle_calibration.json).  A
 # CROSS-MACHINE estimate: the oracle was timed on this repo's Intel Xeon (AVX-512)
 # container, the reference by the survey on an 8-vCPU AMD EPYC container; the reference
 # cannot be rebuilt here to time both on one CPU.
-CALIBRATION_RECORD = "profiles/r4/oracle_calibration.json"
+CALIBRATION_RECORD = "profiles/oracle_calibration.json"
 
 
 def oracle_over_ref() -> dict:

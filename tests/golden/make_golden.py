@@ -17,10 +17,14 @@ evalacc_full.json
 evalacc_b4096.json (--big-batch)
     The bench's own shape: STD128_MKNTRU, full n, B = 4096 seeded gates in one
     batch, whole-output SHA-256 and per-gate digests.
-gates_realkeys.json
+gates_realkeys.json (--gates-only regenerates just this file)
     NAND gates with real keys (seeded NTL-free key generation,
     mkfhe_amd/keys.py), evaluated by the oracle: digest of the output
-    ciphertexts and their decryptions.
+    ciphertexts and their decryptions, at every BASELINE configuration's
+    parameter set: STD128_MKNTRU (configs 1/2), STD100_MKNTRU_LWE (the
+    boolean-mklwe example), STD100_MKNTRU_LWE_2 (config 3, MK-LWE k = 4) and
+    STD128_MKNTRU_3 (config 4, MK-NTRU k = 8).  The seeds draw no
+    r-defective key (KEEP policy): asserted here.
 """
 import hashlib
 import json
@@ -137,34 +141,41 @@ def make_evalacc():
     return out
 
 
+# paramset, method, seed
+GATE_CASES = [("STD128_MKNTRU", 0, 9100), ("STD100_MKNTRU_LWE", 2, 9200),
+              ("STD100_MKNTRU_LWE_2", 2, 9300), ("STD128_MKNTRU_3", 0, 9400)]
+
+
 def make_gates():
     from mkfhe_amd import keys as K
     out = []
     m1 = np.array([0, 0, 1, 1]); m2 = np.array([0, 1, 0, 1])
-    for ps, method in (("STD128_MKNTRU", 0), ("STD100_MKNTRU_LWE", 2)):
+    threads = min(8, os.cpu_count() or 1)
+    for ps, method, seed in GATE_CASES:
         p = K.paramset(ps, method)
         k, n, _, dg, nk, dks = K.dims(p)
-        seed = 9100 if method == 0 else 9200
         if method == 0:
             sk = K.mntru_keygen(p, seed)
             bk = K.bt_keygen(p, sk, seed=seed + 1)
+            assert bk.rdefects == 0, (ps, "r-defective key drawn: pick another seed")
             ctn = K.mntru_ctgate(p, sk, seed + 2)
             c1, c2 = K.mntru_encrypt(p, sk, m1, seed=seed + 3), K.mntru_encrypt(p, sk, m2, seed=seed + 4)
             orc = pyoracle.Oracle(pyoracle.XZW, k, n, N, p.acc.Q, p.acc.q, p.acc.baseG)
             heads = np.stack([pyoracle.mntru_head(ctn, c1[i], c2[i], p.acc.q) for i in range(4)])
             acc0 = np.broadcast_to(orc.mntru_testvector(4), (4, k, N)).copy()
-            acc = orc.evalacc_batch(bk.evk, bk.pkey, heads, acc0, 4)
+            acc = orc.evalacc_batch(bk.evk, bk.pkey, heads, acc0, threads)
             res = np.stack([orc.mntru_tail_ksk1(acc[i], bk.ksk, p.ks.qKS, p.ks.baseKS, n) for i in range(4)])
             dec = K.mntru_decrypt(p, sk, res.astype(np.uint32), mod=p.ks.qKS)
             inputs = {"ct_nand": digest(ctn), "ct1": digest(c1), "ct2": digest(c2)}
         else:
             sk = K.mklwe_keygen(p, seed)
             bk = K.bt_keygen(p, sk, seed=seed + 1)
+            assert bk.rdefects == 0, (ps, "r-defective key drawn: pick another seed")
             a1, b1 = K.mklwe_encrypt(p, sk, m1, seed=seed + 3)
             a2, b2 = K.mklwe_encrypt(p, sk, m2, seed=seed + 4)
             orc = pyoracle.Oracle(pyoracle.XZW_B, k, n, N, p.acc.Q, 2 * N, p.acc.baseG)
             cs, accs = zip(*[orc.mklwe_head(a1[i], b1[i], a2[i], b2[i], p.acc.q) for i in range(4)])
-            acc = orc.evalacc_batch(bk.evk, bk.pkey, np.stack(cs), np.stack(accs), 4)
+            acc = orc.evalacc_batch(bk.evk, bk.pkey, np.stack(cs), np.stack(accs), threads)
             A, Bk = bk.ksk_A.astype(np.uint64), bk.ksk_B.astype(np.uint64)
             outs = [orc.mklwe_tail(acc[i], A, Bk, p.ks.qKS, p.ks.baseKS, n) for i in range(4)]
             res = np.concatenate([np.stack([o[0] for o in outs]).reshape(4, -1),
@@ -211,6 +222,8 @@ def main():
         json.dump(make_big_batch(), open(os.path.join(HERE, "evalacc_b4096.json"), "w"))
         return
     json.dump(make_gates(), open(os.path.join(HERE, "gates_realkeys.json"), "w"), indent=1)
+    if "--gates-only" in sys.argv:
+        return
     json.dump(make_evalacc(), open(os.path.join(HERE, "evalacc_full.json"), "w"), indent=1)
 
 

@@ -107,3 +107,73 @@ def test_mkntru_four_parties_decrypt_correctly():
     m1, m2 = rng.integers(0, 2, 128), rng.integers(0, 2, 128)
     out = cc.EvalBinGate(NAND, cc.Encrypt(sk, m1), cc.Encrypt(sk, m2))
     assert np.array_equal(cc.DecryptGate(sk, out), 1 - (m1 & m2))
+
+
+def _mntru_oracle_gates(oracle, cc, c1, c2, idx):
+    """The CPU oracle's full MK-NTRU NAND gates (head, EvalAcc, extraction,
+    ModSwitch, KeySwitch2) of gates idx on the context's real keys."""
+    from mkfhe_amd import keys as K
+    p, bk = cc.params, cc.BTKey
+    k, n, _, dg, nk, dks = K.dims(p)
+    orc = oracle.Oracle(oracle.XZW, k, n, N, p.acc.Q, p.acc.q, p.acc.baseG)
+    heads = np.stack([oracle.mntru_head(cc.ctNAND, c1[i], c2[i], p.acc.q) for i in idx])
+    acc0 = np.broadcast_to(orc.mntru_testvector(4), (len(idx), k, N)).copy()
+    acc = orc.evalacc_batch(bk.evk, bk.pkey, heads, acc0, min(16, os.cpu_count() or 1))
+    return np.stack([orc.mntru_tail_ksk1(acc[j], bk.ksk, p.ks.qKS, p.ks.baseKS, n) for j in range(len(idx))])
+
+
+@pytest.mark.gpu
+def test_config4_eight_party_mkntru_gates_decrypt_correctly(oracle):
+    """Config 4's parameter set (STD128_MKNTRU_3: k = 8, n = 765, B_g = 2^6, dg = 4;
+    binfhecontext.cpp:131) with real seeded keys: a 320-gate batch (the batch step
+    kernel with its d_i scratch, the k = 8 extraction and KeySwitch2 of
+    mntru-pke.cpp:763-823) decrypts to NAND, and the engine's output ciphertexts
+    equal the CPU oracle's full gates bit for bit.  The seed draws no r-defective
+    key (asserted), so the truth table is deterministic."""
+    from mkfhe_amd.binfhe import NAND
+    cc = _ctx("STD128_MKNTRU_3", 0, 808)
+    sk = cc.MNTRU_KeyGen()
+    cc.MKBTKeyGen(sk)
+    assert cc.GetRDefects() == 0
+    cc.ctGateGen(sk, NAND)
+    rng = np.random.default_rng(12)
+    B = 320
+    m1, m2 = rng.integers(0, 2, B), rng.integers(0, 2, B)
+    c1, c2 = cc.Encrypt(sk, m1), cc.Encrypt(sk, m2)
+    assert cc.engine().step_kernel_name(B) == "mk_step_kernel"
+    out = cc.EvalBinGate(NAND, c1, c2)
+    assert np.array_equal(cc.DecryptGate(sk, out), 1 - (m1 & m2))
+    idx = [0, B - 1]
+    assert np.array_equal(out[idx].astype(np.uint64), _mntru_oracle_gates(oracle, cc, c1, c2, idx))
+
+
+@pytest.mark.gpu
+def test_config3_four_party_mklwe_gates_decrypt_correctly(oracle):
+    """Config 3's parameter set (STD100_MKNTRU_LWE_2: MK-LWE, k = 4, n = 500;
+    binfhecontext.cpp:142; UniEncAccumulatorXZW_B, mk-acc-xzw_B.cpp:103-132, and
+    KeySwitch, mklwe-pke.cpp:260-298) with real seeded keys: a 640-gate batch (the
+    batch step kernel) decrypts to NAND, and two gates equal the CPU oracle's
+    full gates bit for bit."""
+    from mkfhe_amd import keys as K
+    from mkfhe_amd.binfhe import NAND
+    cc = _ctx("STD100_MKNTRU_LWE_2", 2, 404)
+    sk = cc.MKLWE_KeyGen()
+    cc.MKBTKeyGen(sk)
+    assert cc.GetRDefects() == 0
+    rng = np.random.default_rng(13)
+    B = 640
+    m1, m2 = rng.integers(0, 2, B), rng.integers(0, 2, B)
+    (a1, b1), (a2, b2) = cc.Encrypt(sk, m1), cc.Encrypt(sk, m2)
+    assert cc.engine().step_kernel_name(B) == "mk_step2_kernel"
+    oa, ob = cc.EvalBinGate(NAND, (a1, b1), (a2, b2))
+    assert np.array_equal(cc.DecryptGate(sk, (oa, ob)), 1 - (m1 & m2))
+    p, bk = cc.params, cc.BTKey
+    k, n, _, dg, nk, dks = K.dims(p)
+    orc = oracle.Oracle(oracle.XZW_B, k, n, N, p.acc.Q, 2 * N, p.acc.baseG)
+    idx = [0, B - 1]
+    cs, accs = zip(*[orc.mklwe_head(a1[i], b1[i], a2[i], b2[i], p.acc.q) for i in idx])
+    acc = orc.evalacc_batch(bk.evk, bk.pkey, np.stack(cs), np.stack(accs), min(16, os.cpu_count() or 1))
+    A, Bk = bk.ksk_A.astype(np.uint64), bk.ksk_B.astype(np.uint64)
+    for j, i in enumerate(idx):
+        ea, eb = orc.mklwe_tail(acc[j], A, Bk, p.ks.qKS, p.ks.baseKS, n)
+        assert np.array_equal(oa[i].astype(np.uint64), ea) and int(ob[i]) == eb

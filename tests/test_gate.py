@@ -94,10 +94,15 @@ def test_gate_tail_mntru(mk_gpu, oracle):
         assert np.array_equal(got[b], exp.astype(np.uint32)), b
 
 
+# (k, n, log2 B_g, MKACC_LAT): config 4's shape (k = 8, dg = 4) and STD100_MKNTRU_3's
+# (k = 8, dg = 2) through both the small-batch and the batch step kernel
 @pytest.mark.gpu
-@pytest.mark.parametrize("k,n,logB", [(2, 4, 9), (2, 3, 7), (3, 2, 6)])
-def test_nand_gate_mntru(mk_gpu, oracle, k, n, logB):
+@pytest.mark.parametrize("k,n,logB,lat", [(2, 4, 9, ""), (2, 3, 7, ""), (3, 2, 6, ""), (8, 2, 6, "1"), (8, 2, 6, "0"),
+                                          (8, 2, 9, "1"), (8, 2, 9, "0")])
+def test_nand_gate_mntru(mk_gpu, oracle, k, n, logB, lat, monkeypatch):
     mk = mk_gpu
+    if lat:
+        monkeypatch.setenv("MKACC_LAT", lat)
     B = 5
     orc, eng, evk, pkey, ksk2, q, qKS, baseKS = _mntru_setup(mk, oracle, k, n, 1 << logB, B, seed=k * 10 + n)
     ct1 = oracle.fill_uniform(B * k * n, q, 31).reshape(B, k, n)
@@ -139,7 +144,7 @@ def test_gate_tail_mklwe(mk_gpu, oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("k,n", [(2, 4), (4, 2)])
+@pytest.mark.parametrize("k,n", [(2, 4), (4, 2), (8, 2)])
 def test_nand_gate_mklwe(mk_gpu, oracle, k, n):
     mk = mk_gpu
     B = 6

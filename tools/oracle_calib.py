@@ -7,7 +7,7 @@ Each paramset: real keys from the keys library (seed 1), one NAND input's head
 (XZW) or the MK-LWE head (XZW_B) with the test-vector accumulator, evalacc on 1
 thread, best of --reps.  Writes JSON {paramset: {oracle_s, reference_s, ratio}}.
 
-usage: tools/oracle_calib.py [--reps 3] [--out profiles/r4/oracle_calibration.json]
+usage: tools/oracle_calib.py [--reps 3] [--out profiles/oracle_calibration.json]
 """
 import argparse
 import json
