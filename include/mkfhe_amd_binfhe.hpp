@@ -1036,9 +1036,10 @@ private:
         checkk(mkkg_pkey(&m_kp, next_seed(), ek.crs.data(), ek.f_eval.data(), ek.pkey.data()));
         uint64_t ndef = 0;
         m_rdefects = 0;
-        checkk(mkkg_acc_keygen_ex(&m_kp, next_seed(), ek.crs.data(), ek.finv_eval.data(), lwe_sk.data(),
-                                  ek.evk.data(), static_cast<uint32_t>(policy), &ndef));
-        m_rdefects = ndef;
+        const int rc = mkkg_acc_keygen_ex(&m_kp, next_seed(), ek.crs.data(), ek.finv_eval.data(), lwe_sk.data(),
+                                          ek.evk.data(), static_cast<uint32_t>(policy), &ndef);
+        m_rdefects = ndef;   // also after a REJECT: GetRDefects() reports the rejected draw
+        checkk(rc);
         up_keys(ek.evk.data(), ek.pkey.data());
         return ek;
     }

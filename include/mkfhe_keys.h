@@ -202,7 +202,9 @@ int mkkg_ntt_inverse(const mkkg_params* p, const uint32_t* in, uint32_t* out, si
  * master: 8 words = 64 hex digits, word 0 first.
  * mkkg_entropy_replay(1): opt in.  If MKFHE_ENTROPY is set, the journal
  *   restarts at that master (MKACC_E_ARG, and no opt-in, if it is not 64 hex
- *   digits); otherwise the current master stays.  mkkg_entropy_replay(0)
+ *   digits, or if a seed-0 call has already drawn from another master: a
+ *   restarted counter would reuse earlier call keys; the same master keeps its
+ *   counter); otherwise the current master stays.  mkkg_entropy_replay(0)
  *   opts out again (the master stays, it is just no longer exported).
  * mkkg_entropy_get: the master (drawn now if no seed-0 call has drawn it yet)
  *   and the number of seed-0 calls made since it was set; MKACC_E_ARG unless

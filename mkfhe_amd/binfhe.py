@@ -98,7 +98,11 @@ class BinFHEContext:
             raise ConfigError("secret key type does not match the context method")
         seed = self._next()
         self.rdefects = 0
-        bk = K.bt_keygen(self.kp, sk, seed=seed, crs_seed=(seed ^ 0xC25) if seed else None, rdefect=rdefect)
+        try:
+            bk = K.bt_keygen(self.kp, sk, seed=seed, crs_seed=(seed ^ 0xC25) if seed else None, rdefect=rdefect)
+        except K.KeyDefectError as e:
+            self.rdefects = e.rdefects   # GetRDefects() reports the rejected draw's count
+            raise
         self.rdefects = bk.rdefects
         self._upload(bk)
 

@@ -116,6 +116,29 @@ def _jobs() -> int:
     return max(1, min(len(UNITS), os.cpu_count() or 1))
 
 
+def included_files(path: str, seen=None) -> list[str]:
+    """path and every in-tree header it reaches through #include "..." (transitively)."""
+    import re
+    seen = [] if seen is None else seen
+    path = os.path.normpath(path)
+    if path in seen or not os.path.exists(path):
+        return seen
+    seen.append(path)
+    with open(path) as f:
+        for m in re.finditer(r'^\s*#\s*include\s+"([^"]+)"', f.read(), re.M):
+            included_files(os.path.join(os.path.dirname(path), m.group(1)), seen)
+    return seen
+
+
+def unit_key(path: str, cmd: list[str]) -> str:
+    """Identity of one translation unit's compile: its sources and its command line."""
+    h = hashlib.sha256(" ".join(cmd).encode())
+    for f in included_files(path):
+        with open(f, "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read())
+    return h.hexdigest()
+
+
 def compile_engine(out: str, flags: list[str], report: str, verbose: bool = False, only=None) -> str:
     """hipcc the engine units into `out` with extra `flags` (-D switches of A/B builds).
     only: names of the units to compile with the flags; the others are linked from
@@ -131,13 +154,30 @@ def compile_engine(out: str, flags: list[str], report: str, verbose: bool = Fals
               "-I", os.path.join(ROOT, "include"), *_id_defines("MKACC", engine_ids(), flags), *flags,
               "-Rpass-analysis=kernel-resource-usage"]
 
+    ids_flags = _id_defines("MKACC", engine_ids(), flags)
+
     def unit(u):
         name, src, defs = u
         obj = os.path.join(objdir, name + ".o")
-        cmd = common + defs + ["-c", "-o", obj, os.path.join(_HERE, "csrc", src)]
+        path = os.path.join(_HERE, "csrc", src)
+        cmd = common + defs + ["-c", "-o", obj, path]
+        # a step unit whose sources (its file and the headers it reaches) and flags are
+        # unchanged keeps its object: the build-id defines only reach the host unit
+        key = unit_key(path, [c for c in cmd if c not in ids_flags] + (ids_flags if name == "engine" else []))
+        stamp = obj + ".key"
+        if os.path.exists(obj) and os.path.exists(stamp) and open(stamp).read() == key:
+            rep = obj + ".res"
+            return name, obj, subprocess.CompletedProcess(cmd, 0, "", open(rep).read() if os.path.exists(rep) else "")
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode == 0:
+            with open(obj + ".res", "w") as f:
+                f.write(r.stderr)
+            with open(stamp, "w") as f:
+                f.write(key)
+        elif os.path.exists(stamp):
+            os.remove(stamp)
         return name, obj, r
 
     # a variant always recompiles the host unit too: it carries the build

@@ -372,6 +372,24 @@ struct StepChain {
     uint32_t* result() const { return cur - ao; }   // the full-batch buffer holding the result
 };
 
+// Joins the slice streams a batch forked from the context stream back into it on
+// every exit path: later work on c->stream -- a key upload's
+// hipStreamSynchronize, a workspace free -- must stay ordered after every slice
+// launch, also when a launch helper returns early.
+struct SliceJoin {
+    mkacc_ctx* c;
+    size_t ns = 0;   // slices forked (streams xs[0 .. ns-2] wait on ev_fork)
+    bool ok = true;  // every join recorded and waited for
+    ~SliceJoin() { join(); }
+    void join() {
+        for (size_t j = 1; j < ns; ++j)
+            if (hipEventRecord(c->ev_join[j - 1], c->xs[j - 1]) != hipSuccess ||
+                hipStreamWaitEvent(c->stream, c->ev_join[j - 1], 0) != hipSuccess)
+                ok = false;
+        ns = 0;
+    }
+};
+
 // The k*n accumulator steps over a batch whose monomial exponents are in
 // d_cvals and whose C4 accumulators are in d_acc0; returns the buffer holding
 // the result (nullptr if the build has no kernel for the context's digit count).
@@ -401,22 +419,21 @@ uint32_t* launch_steps(mkacc_ctx* c, size_t B) {
     // slices of whole units, the remainder in the last one
     const size_t per = (B / unit / ns) * unit;
     if (hipEventRecord(c->ev_fork, c->stream) != hipSuccess) return nullptr;
+    SliceJoin join{c};
     std::vector<StepChain> ch;
     ch.reserve(ns);
     for (size_t j = 0; j < ns; ++j) {
         hipStream_t st = j == 0 ? c->stream : c->xs[j - 1];
         if (j > 0 && hipStreamWaitEvent(st, c->ev_fork, 0) != hipSuccess) return nullptr;
+        join.ns = j + 1;
         ch.emplace_back(c, B, j * per, j + 1 < ns ? per : B - j * per, st);
     }
     for (uint32_t u = 0; u < k; ++u)
         for (uint32_t i = 0; i < n; ++i)
             for (auto& h : ch)
                 if (!h.step(u, i, lds)) return nullptr;
-    for (size_t j = 1; j < ns; ++j)
-        if (hipEventRecord(c->ev_join[j - 1], c->xs[j - 1]) != hipSuccess ||
-            hipStreamWaitEvent(c->stream, c->ev_join[j - 1], 0) != hipSuccess)
-            return nullptr;
-    return ch[0].result();
+    join.join();
+    return join.ok ? ch[0].result() : nullptr;
 }
 
 void launch_prep_c(mkacc_ctx* c, const uint32_t* d_ct, size_t B) {
@@ -914,9 +931,13 @@ int wide_launch_batch(mkacc_ctx* c, const uint32_t* d_ct, const uint64_t* d_in, 
         const size_t unit = (size_t)c->cus * 4;
         const size_t ns = std::max<size_t>(1, std::min<size_t>((size_t)c->nstreams, B / unit));
         const size_t per = ns > 1 ? (B / unit / ns) * unit : B;
+        SliceJoin join{c};
         if (ns > 1) {
             HIP_TRY(hipEventRecord(c->ev_fork, c->stream));
-            for (size_t j = 1; j < ns; ++j) HIP_TRY(hipStreamWaitEvent(c->xs[j - 1], c->ev_fork, 0));
+            for (size_t j = 1; j < ns; ++j) {
+                HIP_TRY(hipStreamWaitEvent(c->xs[j - 1], c->ev_fork, 0));
+                join.ns = j + 1;
+            }
         }
         for (uint32_t u = 0; u < k; ++u)
             for (uint32_t i = 0; i < n; ++i)
@@ -949,10 +970,8 @@ int wide_launch_batch(mkacc_ctx* c, const uint32_t* d_ct, const uint64_t* d_in, 
                            j == 0 ? c->stream : c->xs[j - 1], a);
                 if (j + 1 == ns) std::swap(cur, nxt);
             }
-        for (size_t j = 1; j < ns; ++j) {
-            HIP_TRY(hipEventRecord(c->ev_join[j - 1], c->xs[j - 1]));
-            HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_join[j - 1], 0));
-        }
+        join.join();
+        if (!join.ok) return fail(MKACC_E_DEVICE, "joining the batch slice streams failed");
         hipLaunchKernelGGL(widereg2::from_c16_kernel, g, dim3(256), 0, c->stream, cur, d_out, words, c->wfm);
         HIP_TRY(hipGetLastError());
         return MKACC_OK;

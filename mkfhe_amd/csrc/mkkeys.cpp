@@ -533,9 +533,19 @@ int mkkg_entropy_replay(int enable) try {
         uint32_t m[8];
         if (!parse_hex256(env, m))
             return fail(MKACC_E_ARG, "MKFHE_ENTROPY must be 64 hex digits; the replay journal was not enabled");
-        std::memcpy(e.master, m, sizeof m);
-        e.calls = 0;
-        e.init = true;
+        // the imported master restarts the call counter, so it is imported only while no
+        // seed-0 call has drawn from the journal: a restart after one would make later
+        // seed-0 keys and ciphertexts reuse the call keys of earlier ones.  A repeated
+        // opt-in with the journal's own master keeps the counter.
+        if (e.init && e.calls != 0) {
+            if (std::memcmp(e.master, m, sizeof m) != 0)
+                return fail(MKACC_E_ARG, "MKFHE_ENTROPY is imported only before the first seed-0 call of the "
+                                         "process; the journal keeps its master and counter");
+        } else {
+            std::memcpy(e.master, m, sizeof m);
+            e.calls = 0;
+            e.init = true;
+        }
     } else {
         entropy_init_locked(e);
     }

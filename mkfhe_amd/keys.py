@@ -141,7 +141,8 @@ E_RDEFECT = -20
 
 class KeyDefectError(MkaccError):
     """MKBTKeyGen with rdefect="reject" drew a bootstrapping key with DggR sample r != 0
-    (the reference's KeyGenXZW defect, mk-acc-xzw.cpp:160-167)."""
+    (the reference's KeyGenXZW defect, mk-acc-xzw.cpp:160-167); .rdefects counts them."""
+    rdefects = 0
 
 
 def _check(rc: int):
@@ -262,8 +263,13 @@ def bt_keygen(p: MkkgParams, sk, seed: int = 0, crs_seed: int | None = None, rde
     evk = np.empty((k, nk, n + 1, dg, 2, N), np.uint32)
     lwe_sk = _in(sk.F_col0 if isinstance(sk, MNTRUPrivateKey) else sk.s)
     ndef = _u64()
-    _check(L.mkkg_acc_keygen_ex(ctypes.byref(p), sub(3), _p(c), _p(skNinv), _p(lwe_sk), _p(evk), RDEFECT[rdefect],
-                                ctypes.byref(ndef)))
+    rc = L.mkkg_acc_keygen_ex(ctypes.byref(p), sub(3), _p(c), _p(skNinv), _p(lwe_sk), _p(evk), RDEFECT[rdefect],
+                              ctypes.byref(ndef))
+    try:
+        _check(rc)
+    except KeyDefectError as e:
+        e.rdefects = int(ndef.value)   # the count is written before the rejection
+        raise
     key = UniEncBTKey(c, skN, skN_eval, skNinv, pkey, evk, rdefects=int(ndef.value))
     if isinstance(sk, MNTRUPrivateKey):
         key.ksk = np.empty((k, N * dks, n), np.uint32)

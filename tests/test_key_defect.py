@@ -68,8 +68,9 @@ def test_keygen_reports_rejects_or_resamples_the_defective_key(oracle):
         assert kept.rdefects == 1
         K.entropy_set(MASTER)
         sk = K.mntru_keygen(p, 0)
-        with pytest.raises(K.KeyDefectError, match="nonzero DggR"):
+        with pytest.raises(K.KeyDefectError, match="nonzero DggR") as rejected:
             K.bt_keygen(p, sk, seed=0, rdefect="reject")
+        assert rejected.value.rdefects == 1               # the count survives the rejection
         K.entropy_set(MASTER)
         dec, bk = F.example_run(K, oracle, p, orc, False, min(8, os.cpu_count() or 1), rdefect="resample")
         assert bk.rdefects == 1 and F.r_defects(oracle, p, bk) == []

@@ -131,12 +131,36 @@ def test_entropy_is_not_exported_or_overridden_without_opt_in():
                            capture_output=True, text=True, timeout=120) for _ in range(2)]
     assert all(r.returncode == 0 for r in runs), runs[0].stderr
     out = [r.stdout.split() for r in runs]
-    assert out[0][1] == "refused" and out[0][2] == "opted-in"
+    # a seed-0 key was drawn before the opt-in: importing the environment's master then
+    # would restart the call counter and reuse call keys, so it is refused
+    assert out[0][1] == "refused" and out[0][2] == "bad-env" and "before the first seed-0 call" in runs[0].stdout
     assert out[0][0] != out[1][0]            # fresh keys: the environment was not read
     bad = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env={**os.environ, "MKFHE_ENTROPY": "xyz"},
                          capture_output=True, text=True, timeout=120)
     assert bad.returncode == 0, bad.stderr
     assert "bad-env" in bad.stdout and "64 hex digits" in bad.stdout
+
+
+def test_repeated_opt_in_does_not_rewind_the_journal():
+    """entropy_replay() twice around a seed-0 keygen with MKFHE_ENTROPY
+    set.  The first opt-in (no seed-0 call yet) imports the master; the second
+    keeps the journal's counter, so the next seed-0 key is a new draw, not a
+    repeat of the first (which a restarted counter would have produced)."""
+    code = ("from mkfhe_amd import keys as K; p = K.paramset('STD100_MKNTRU', 0)\n"
+            "K.entropy_replay(); a = K.mntru_keygen(p, 0).F\n"
+            "K.entropy_replay(); print(K.entropy_get()[1]); b = K.mntru_keygen(p, 0).F\n"
+            "print(int((a != b).any())); print(int(a.sum()))\n")
+    hexkey = "0123456789abcdef" * 4
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env={**os.environ, "MKFHE_ENTROPY": hexkey},
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    calls, differ, first = r.stdout.split()
+    assert calls == "1" and differ == "1"
+    # and the first key is the imported master's first draw (replayable)
+    again = subprocess.run([sys.executable, "-c", "from mkfhe_amd import keys as K; p = K.paramset('STD100_MKNTRU', 0); "
+                            "K.entropy_replay(); print(int(K.mntru_keygen(p, 0).F.sum()))"], cwd=ROOT,
+                           env={**os.environ, "MKFHE_ENTROPY": hexkey}, capture_output=True, text=True, timeout=120)
+    assert again.returncode == 0 and again.stdout.split()[0] == first
 
 
 def test_encrypt_count_limit_is_an_error_not_a_crash():

@@ -41,7 +41,9 @@ def split_functions(text: str) -> list[tuple[str, str]]:
                 out.append((name, "\n".join(body)))
             name, body = m.group(1), []
             continue
-        if name is None or not s or s.startswith(("Disassembly", ";")):
+        # (objdump's per-file header lines -- "<tmp path>: file format elf64-amdgpu" --
+        # separate the code objects of the units and belong to no function)
+        if name is None or not s or s.startswith(("Disassembly", ";")) or "file format" in s:
             continue
         s = s.split("//")[0].strip()
         if s:
