@@ -94,6 +94,19 @@ def algorithmic_counts(k: int, n: int, dg: int, nk: int, N: int = 2048, B: int =
     return mulmods, bytes_
 
 
+def key_broadcast_bytes(k: int, n: int, N: int, dg: int, nk: int, word: int, stage: str, lwe: bool, qKS: int,
+                        baseKS: int = 32) -> int:
+    """Bytes rank 0 broadcasts once (run_rank): the bootstrapping key evk [k][nk][n+1][dg][2][N]
+    and P [k][dg][N] in `word`-byte words, and for whole gates the key-switching key as u32 --
+    MK-NTRU KSK [k][N dks][n] (KSK2's multiples j KSK are formed by the kernel,
+    mntru-pke.cpp:744-755), MK-LWE A [k][N][baseKS][dks][n] and B [k][N][baseKS][dks]."""
+    dks = int(np.ceil(np.log(qKS) / np.log(baseKS)))
+    b = (k * nk * (n + 1) * dg * 2 * N + k * dg * N) * word
+    if stage == "gate":
+        b += (k * N * baseKS * dks * (n + 1) if lwe else k * N * dks * n) * 4
+    return b
+
+
 def library_kernel_ids() -> dict:
     """{demangled kernel: isa id} of the engine library this process runs
     (mkfhe_amd/build.py writes it next to the library, tools/kernel_isa.py)."""
@@ -145,6 +158,8 @@ def parse(argv=None):
                     help="profiling aid: shorten the LWE dimension (fewer accumulator steps); not a bench config")
     ap.add_argument("--stub-engine", action="store_true",
                     help="test aid (tests/test_bench_ranks.py): CPU stand-in engine + gloo, to exercise the rank logic")
+    ap.add_argument("--stub-shapes", choices=["toy", "real"], default="toy",
+                    help="test aid: the stand-in engine's key and gate shapes (real: the parameter set's)")
     return ap.parse_args(argv)
 
 
@@ -278,6 +293,7 @@ def run_rank(args, env: dict, make_engine, make_checker, torch_device: str, back
     # dist.broadcast on NCCL only orders torch's current stream; the engine converts the
     # keys on its own stream, so the host waits for the received buffer first
     evk_n, pkey_n = int(np.prod(eng.evk_shape)), int(np.prod(eng.pkey_shape))
+    bcast = (evk_n + pkey_n) * word          # bytes rank 0 broadcasts (keys), + key-switching keys below
     keys = shard.broadcast_keys(evk_n + pkey_n, p.Q, seed=12345, device=torch_device)
     sync_dev()
     eng.upload_keys_device(keys[:evk_n], keys[evk_n:])
@@ -285,10 +301,12 @@ def run_rank(args, env: dict, make_engine, make_checker, torch_device: str, back
     if stage == "gate":
         if lwe:
             na, nb = p.k * p.N * baseKS * dks * n_out, p.k * p.N * baseKS * dks
+            bcast += (na + nb) * 4
             ksk_d = shard.broadcast_keys(na + nb, qKS, seed=23456, device=torch_device)
             sync_dev()
             eng.upload_ksk_device(qKS, baseKS, n_out, d_A=ksk_d[:na], d_B=ksk_d[na:])
         else:
+            bcast += p.k * p.N * dks * n_out * 4
             ksk_d = shard.broadcast_keys(p.k * p.N * dks * n_out, qKS, seed=23456, device=torch_device)
             sync_dev()
             eng.upload_ksk_device(qKS, baseKS, n_out, d_ksk=ksk_d)
@@ -420,6 +438,15 @@ def run_rank(args, env: dict, make_engine, make_checker, torch_device: str, back
     if world > 1:
         dist.all_reduce(counts, op=dist.ReduceOp.SUM)
     checked, mismatches = int(counts[0].item()), int(counts[1].item())
+    # what every rank did: its gates of the global batch (contiguous, B per GPU), the oracle
+    # threads of its check and what it checked (tests/test_bench_ranks.py asserts them)
+    mine = {"rank": rank, "gates": list(shard.shard_range(world * B, rank, world)), "oracle_threads": threads,
+            "checked": G, "mismatches": int(bad.sum()), "keys_received_bytes": bcast}
+    ranks = [None] * world
+    if world > 1:
+        dist.all_gather_object(ranks, mine)
+    else:
+        ranks = [mine]
 
     result = None
     if rank == 0:
@@ -467,6 +494,8 @@ def run_rank(args, env: dict, make_engine, make_checker, torch_device: str, back
                        "parallelism": f"gate-sharded x{world}"},
             "parity_checked": checked,
             "parity_mismatches": mismatches,
+            "keys_broadcast_bytes": bcast,
+            "ranks": ranks,
             "parity": (f"{G} gates of every rank's timed batch, evenly spread from the first to the last, "
                        "recomputed by the CPU oracle (oracle/, "
                        "bit-exact integer compare of every output word); the oracle's primitives are pinned by the "

@@ -24,10 +24,19 @@ def _digest(evk, pkey) -> int:
 
 
 class StubEngine:
+    """--stub-shapes toy (default): k = 2, n = 8, N = 16; real: the parameter set's own
+    k, n (or --n-override), N and digit count, so the key broadcast has its real size."""
+
     def __init__(self, args):
         lwe = "_LWE" in args.paramset
-        self.params = types.SimpleNamespace(method=2 if lwe else 0, k=2, n=8, N=16, Q=Q, q=QLWE, baseG=128,
-                                            digitsG=4, root=0)
+        if getattr(args, "stub_shapes", "toy") == "real":
+            import mkfhe_amd as mk
+            r = mk.paramset(args.paramset)
+            self.params = types.SimpleNamespace(method=2 if lwe else 0, k=r.k, n=args.n_override or r.n, N=r.N,
+                                                Q=Q, q=r.q, baseG=r.baseG, digitsG=r.digitsG, root=0)
+        else:
+            self.params = types.SimpleNamespace(method=2 if lwe else 0, k=2, n=8, N=16, Q=Q, q=QLWE, baseG=128,
+                                                digitsG=4, root=0)
         p = self.params
         self.method, self.k, self.n, self.N, self.Q, self.q = p.method, p.k, p.n, p.N, p.Q, p.q
         self.wide = False
