@@ -13,6 +13,11 @@ std::shared_ptr<UniEncAccumulator> MakeAccumulator(BINFHE_METHOD method) {
     return std::make_shared<UniEncAccumulatorAMD>(method);
 }
 
+// ... over the eight GPUs of a node: the batches shard across them
+std::shared_ptr<UniEncAccumulator> MakeNodeAccumulator(BINFHE_METHOD method) {
+    return std::make_shared<UniEncAccumulatorAMD>(method, std::vector<int>{0, 1, 2, 3, 4, 5, 6, 7});
+}
+
 // BinFHEScheme::MKKeyGen -> UniEncACCscheme->KeyGenAcc (binfhe-base-scheme.cpp:272, :334)
 UniEncACCKey KeyGenThroughSeam(const std::shared_ptr<UniEncAccumulator>& acc,
                                const std::shared_ptr<UniEncCryptoParams>& params,

@@ -16,9 +16,16 @@
 //   * EvalAccBatch -> B independent EvalAcc calls in one engine pass (extension)
 //   * EvalNANDBatch-> B whole NAND gates (head, BootstrapGateCore, extraction, ModSwitch, KeySwitch2 /
 //                    KeySwitch) on the GPU: BinFHEScheme::EvalBinGate binfhe-base-scheme.cpp:380-515 (extension)
+//   * a device list -> the batches shard over the GPUs of the node (mkacc_group_*: keys converted once and
+//                    copied device to device over xGMI, contiguous gate shards, bit-identical outputs)
 //
 // Errors follow the reference's convention (exception.h:162): an engine status
 // becomes OPENFHE_THROW(config_error / math_error, text).
+//
+// The conversions between the reference's objects and the C-ABI buffers are the
+// templates of mk-acc-amd-pack.h, instantiated here with the reference's types and
+// executed on stand-in types by tests/cpp/adapter_pack.cpp (layout checks on the
+// CPU; engine-vs-oracle on an MI355X).
 #ifndef MK_ACC_AMD_H
 #define MK_ACC_AMD_H
 
@@ -31,6 +38,7 @@
 #include "mntru-cryptoparameters.h"
 #include "mntru-keyswitchkey2.h"
 #include "mkfhe_amd.h"
+#include "mk-acc-amd-pack.h"
 
 #include <cstdint>
 #include <memory>
@@ -43,21 +51,37 @@ namespace lbcrypto {
 class UniEncAccumulatorAMD final : public UniEncAccumulator {
     // NATIVE_SIZE=32 -> uint32_t words, NATIVE_SIZE=64 -> uint64_t (mkacc_*_u64 entry points)
     using Word = NativeInteger::Integer;
-    static int EngineEval(mkacc_ctx* c, const uint32_t* ct, uint32_t* acc, size_t B) {
-        return mkacc_eval_batch(c, ct, acc, acc, B);
+    // one engine context, or (device list of two or more) a group of them
+    int EngineEval(const uint32_t* ct, uint32_t* acc, size_t B) const {
+        return m_group ? mkacc_group_eval_batch(m_group, ct, acc, acc, B) : mkacc_eval_batch(m_ctx, ct, acc, acc, B);
     }
-    static int EngineEval(mkacc_ctx* c, const uint32_t* ct, uint64_t* acc, size_t B) {
-        return mkacc_eval_batch_u64(c, ct, acc, acc, B);
+    int EngineEval(const uint32_t* ct, uint64_t* acc, size_t B) const {
+        return m_group ? mkacc_group_eval_batch_u64(m_group, ct, acc, acc, B)
+                       : mkacc_eval_batch_u64(m_ctx, ct, acc, acc, B);
     }
-    static int EngineUpload(mkacc_ctx* c, const uint32_t* evk, const uint32_t* pkey) {
-        return mkacc_upload_keys(c, evk, pkey);
+    int EngineUpload(const uint32_t* evk, const uint32_t* pkey) const {
+        return m_group ? mkacc_group_upload_keys(m_group, evk, pkey) : mkacc_upload_keys(m_ctx, evk, pkey);
     }
-    static int EngineUpload(mkacc_ctx* c, const uint64_t* evk, const uint64_t* pkey) {
-        return mkacc_upload_keys_u64(c, evk, pkey);
+    int EngineUpload(const uint64_t* evk, const uint64_t* pkey) const {
+        return m_group ? mkacc_group_upload_keys_u64(m_group, evk, pkey) : mkacc_upload_keys_u64(m_ctx, evk, pkey);
     }
+    int EngineUploadKSK2(const mkacc_ks_params& ks, const uint32_t* w) const {
+        return m_group ? mkacc_group_upload_ksk_mntru(m_group, &ks, w) : mkacc_upload_ksk_mntru(m_ctx, &ks, w);
+    }
+    int EngineUploadKSK(const mkacc_ks_params& ks, const uint32_t* wa, const uint32_t* wb) const {
+        return m_group ? mkacc_group_upload_ksk_mklwe(m_group, &ks, wa, wb) : mkacc_upload_ksk_mklwe(m_ctx, &ks, wa, wb);
+    }
+    // member 0 answers the shape queries (every member has the same parameters)
+    mkacc_ctx* Ctx0() const { return m_group ? mkacc_group_member(m_group, 0) : m_ctx; }
 
 public:
-    explicit UniEncAccumulatorAMD(BINFHE_METHOD method, int device = 0) : m_method(method), m_device(device) {
+    explicit UniEncAccumulatorAMD(BINFHE_METHOD method, int device = 0)
+        : UniEncAccumulatorAMD(method, std::vector<int>{device}) {}
+    // Two or more devices: every batch (EvalAccBatch, EvalNANDBatch) shards over them.
+    UniEncAccumulatorAMD(BINFHE_METHOD method, std::vector<int> devices)
+        : m_method(method), m_devices(std::move(devices)) {
+        if (m_devices.empty())
+            OPENFHE_THROW(config_error, "UniEncAccumulatorAMD: empty device list");
         if (method == MKNTRU)
             m_cpu = std::make_shared<UniEncAccumulatorXZW>();
         else if (method == MKNTRU_B || method == MKNTRU_LWE)
@@ -70,6 +94,8 @@ public:
     ~UniEncAccumulatorAMD() {
         if (m_ctx)
             mkacc_destroy(m_ctx);
+        if (m_group)
+            mkacc_group_destroy(m_group);
     }
 
     // ---- key generation: the reference's own code, unchanged ----------------
@@ -111,27 +137,22 @@ public:
         // XZW scales c = ct*2N/q with the ciphertext's own modulus (mk-acc-xzw.cpp:96,110); XZW_B takes
         // ct mod 2N as is (mk-acc-xzw_B.cpp:103-132), so there q only matters to the gate head.
         const uint64_t q = ct[0][0].GetModulus().ConvertToInt<uint64_t>();
-        Prepare(params, ek, n, (m_method == MKNTRU || !m_ctx) ? q : m_p.q);
+        Prepare(params, ek, n, (m_method == MKNTRU || !Ctx0()) ? q : m_p.q);
         UploadKeys(ek, Pkey);
         std::vector<uint32_t> c(B * k * n);
         std::vector<Word> a(B * k * N);
         for (size_t b = 0; b < B; ++b) {
-            if (ct[b].size() != k || acc[b] == nullptr || acc[b]->GetElements().size() != k)
-                OPENFHE_THROW(config_error, "EvalAccBatch: ciphertext/accumulator has the wrong number of parties");
+            if (acc[b] == nullptr || acc[b]->GetElements().size() != k)
+                OPENFHE_THROW(config_error, "EvalAccBatch: accumulator has the wrong number of parties");
+            mkacc_pack::pack_vectors(ct[b], k, n, c.data() + b * k * n, Fail);
             for (uint32_t u = 0; u < k; ++u) {
-                const NativeVector& cu = ct[b][u];
-                if (cu.GetLength() != n)
-                    OPENFHE_THROW(config_error, "EvalAccBatch: ragged ciphertext");
-                for (uint32_t i = 0; i < n; ++i)
-                    c[(b * k + u) * n + i] = cu[i].ConvertToInt<uint32_t>();
                 const NativePoly& p = acc[b]->GetElements()[u];
                 if (p.GetFormat() != Format::EVALUATION)
                     OPENFHE_THROW(config_error, "EvalAccBatch: accumulator must be in EVALUATION format");
-                for (uint32_t j = 0; j < N; ++j)
-                    a[(b * k + u) * N + j] = p[j].ConvertToInt<Word>();
+                mkacc_pack::pack_poly(p, N, a.data() + (b * k + u) * N, Fail);
             }
         }
-        Check(EngineEval(m_ctx, c.data(), a.data(), B));
+        Check(EngineEval(c.data(), a.data(), B));
         for (size_t b = 0; b < B; ++b) {
             auto& polys = acc[b]->GetElements();
             for (uint32_t u = 0; u < k; ++u) {
@@ -175,7 +196,8 @@ public:
             PackMNTRU(*ct1[b], a1.data() + b * k * n, k, n);
             PackMNTRU(*ct2[b], a2.data() + b * k * n, k, n);
         }
-        Check(mkacc_eval_nand_mntru(m_ctx, nand.data(), a1.data(), a2.data(), out.data(), B));
+        Check(m_group ? mkacc_group_eval_nand_mntru(m_group, nand.data(), a1.data(), a2.data(), out.data(), B)
+                      : mkacc_eval_nand_mntru(m_ctx, nand.data(), a1.data(), a2.data(), out.data(), B));
         std::vector<MNTRUCiphertext> res(B);
         for (size_t b = 0; b < B; ++b) {
             std::vector<NativeVector> c(k, NativeVector(n, ntru->GetqKS()));
@@ -218,7 +240,9 @@ public:
             b1[b] = ct1[b]->GetB().ConvertToInt<uint32_t>();
             b2[b] = ct2[b]->GetB().ConvertToInt<uint32_t>();
         }
-        Check(mkacc_eval_nand_mklwe(m_ctx, a1.data(), b1.data(), a2.data(), b2.data(), oa.data(), ob.data(), B));
+        Check(m_group ? mkacc_group_eval_nand_mklwe(m_group, a1.data(), b1.data(), a2.data(), b2.data(), oa.data(),
+                                                    ob.data(), B)
+                      : mkacc_eval_nand_mklwe(m_ctx, a1.data(), b1.data(), a2.data(), b2.data(), oa.data(), ob.data(), B));
         std::vector<MKLWECiphertext> res(B);
         for (size_t b = 0; b < B; ++b) {
             std::vector<NativeVector> a(k, NativeVector(n, lwe->GetqKS()));
@@ -249,6 +273,8 @@ public:
     }
 
 private:
+    static void Fail(const char* what) { OPENFHE_THROW(config_error, what); }
+
     static void Check(int rc) {
         if (rc == MKACC_OK)
             return;
@@ -278,16 +304,22 @@ private:
         p.baseG   = P->GetBaseG();
         p.digitsG = P->GetDigitsG();
         p.root    = P->GetPolyParams()->GetRootOfUnity().ConvertToInt<uint64_t>();
-        if (m_ctx && p.k == m_p.k && p.n == m_p.n && p.N == m_p.N && p.Q == m_p.Q && p.q == m_p.q &&
+        if (Ctx0() && p.k == m_p.k && p.n == m_p.n && p.N == m_p.N && p.Q == m_p.Q && p.q == m_p.q &&
             p.baseG == m_p.baseG && p.digitsG == m_p.digitsG && p.root == m_p.root)
             return;
         if (m_ctx)
             mkacc_destroy(m_ctx);
-        m_ctx = nullptr;
+        if (m_group)
+            mkacc_group_destroy(m_group);
+        m_ctx   = nullptr;
+        m_group = nullptr;
         m_key.reset();
         m_ksk2.reset();
         m_ksk.reset();
-        Check(mkacc_create(&p, m_device, &m_ctx));
+        if (m_devices.size() > 1)
+            Check(mkacc_group_create(&p, m_devices.data(), static_cast<uint32_t>(m_devices.size()), &m_group));
+        else
+            Check(mkacc_create(&p, m_devices[0], &m_ctx));
         m_p = p;
     }
 
@@ -297,49 +329,16 @@ private:
     void UploadKeys(ConstUniEncACCKey& ek, const std::vector<std::vector<NativePoly>>& Pkey) const {
         const uint32_t k = m_p.k, N = m_p.N, dg = m_p.digitsG - 1, n1 = m_p.n + 1;
         const uint32_t nk = m_method == MKNTRU ? 2 : 1;
-        if (Pkey.size() != k)
-            OPENFHE_THROW(config_error, "Pkey has the wrong number of parties");
-        std::vector<Word> pk(mkacc_pkey_words(m_ctx));  // [k][dg][N]
-        for (uint32_t u = 0; u < k; ++u) {
-            if (Pkey[u].size() < dg)
-                OPENFHE_THROW(config_error, "Pkey has the wrong number of digits");
-            for (uint32_t d = 0; d < dg; ++d)
-                for (uint32_t s = 0; s < N; ++s)
-                    pk[(size_t(u) * dg + d) * N + s] = Pkey[u][d][s].ConvertToInt<Word>();
-        }
+        std::vector<Word> pk(mkacc_pkey_words(Ctx0()));  // [k][dg][N]
+        mkacc_pack::pack_pkey(Pkey, k, dg, N, pk.data(), Fail);
         // Pkey arrives by value on every call, so it is compared by content; the
         // key object is held, so its address cannot be recycled while cached.
         if (m_key == ek && m_pkey == pk)
             return;
-        const auto& K = ek->GetElements();
-        if (K.size() != k)
-            OPENFHE_THROW(config_error, "bootstrapping key has the wrong number of parties");
-        std::vector<Word> evk(mkacc_evk_words(m_ctx), Word(0));
-        size_t o = 0;
-        for (uint32_t u = 0; u < k; ++u) {
-            if (K[u].size() < nk)
-                OPENFHE_THROW(config_error, "bootstrapping key has the wrong shape");
-            for (uint32_t j = 0; j < nk; ++j) {
-                if (K[u][j].size() != n1)
-                    OPENFHE_THROW(config_error, "bootstrapping key has the wrong dimension");
-                for (uint32_t i = 0; i < n1; ++i) {
-                    const auto& e = K[u][j][i];
-                    if (e == nullptr) {
-                        o += size_t(dg) * 2 * N;
-                        continue;
-                    }
-                    const auto& el = e->GetElements();
-                    if (el.size() != dg)
-                        OPENFHE_THROW(config_error, "bootstrapping key has the wrong number of digits");
-                    for (uint32_t d = 0; d < dg; ++d)
-                        for (uint32_t t = 0; t < 2; ++t, o += N)
-                            for (uint32_t s = 0; s < N; ++s)
-                                evk[o + s] = el[d][t][s].ConvertToInt<Word>();
-                }
-            }
-        }
+        std::vector<Word> evk(mkacc_evk_words(Ctx0()));
+        mkacc_pack::pack_evk(ek->GetElements(), k, nk, n1, dg, N, evk.data(), Fail);
         m_key.reset();
-        Check(EngineUpload(m_ctx, evk.data(), pk.data()));
+        Check(EngineUpload(evk.data(), pk.data()));
         m_key  = ek;
         m_pkey = std::move(pk);
     }
@@ -352,17 +351,10 @@ private:
         if (m_ksk2 == K)
             return;
         const uint32_t k = m_p.k, N = m_p.N, n = ks.n_out, dks = mkacc_ks_digits(&ks);
-        const auto& E = K->GetElements();  // [k][baseKS][N*dks][n]
         std::vector<uint32_t> w(size_t(k) * N * dks * n);
-        for (uint32_t u = 0; u < k; ++u) {
-            if (E.size() != k || E[u].size() < 2 || E[u][1].size() != size_t(N) * dks)
-                OPENFHE_THROW(config_error, "KeySwitch2 key has the wrong shape");
-            for (size_t l = 0; l < size_t(N) * dks; ++l)
-                for (uint32_t i = 0; i < n; ++i)
-                    w[(u * size_t(N) * dks + l) * n + i] = E[u][1][l][i].ConvertToInt<uint32_t>();
-        }
+        mkacc_pack::pack_ksk2(K->GetElements(), k, N, dks, n, w.data(), Fail);   // [k][baseKS][N*dks][n]
         m_ksk2.reset();
-        Check(mkacc_upload_ksk_mntru(m_ctx, &ks, w.data()));
+        Check(EngineUploadKSK2(ks, w.data()));
         m_ksk2 = K;
     }
 
@@ -373,51 +365,26 @@ private:
         if (m_ksk == K)
             return;
         const uint32_t k = m_p.k, N = m_p.N, n = ks.n_out, base = ks.baseKS, dks = mkacc_ks_digits(&ks);
-        const auto& A = K->GetElementsA();
-        const auto& Bk = K->GetElementsB();
         std::vector<uint32_t> wa(size_t(k) * N * base * dks * n), wb(size_t(k) * N * base * dks);
-        for (uint32_t u = 0; u < k; ++u)
-            for (uint32_t i = 0; i < N; ++i)
-                for (uint32_t a = 0; a < base; ++a)
-                    for (uint32_t j = 0; j < dks; ++j) {
-                        const size_t r = ((size_t(u) * N + i) * base + a) * dks + j;
-                        wb[r] = Bk[u][i][a][j].ConvertToInt<uint32_t>();
-                        for (uint32_t l = 0; l < n; ++l)
-                            wa[r * n + l] = A[u][i][a][j][l].ConvertToInt<uint32_t>();
-                    }
+        mkacc_pack::pack_lwe_ksk(K->GetElementsA(), K->GetElementsB(), k, N, base, dks, n, wa.data(), wb.data(), Fail);
         m_ksk.reset();
-        Check(mkacc_upload_ksk_mklwe(m_ctx, &ks, wa.data(), wb.data()));
+        Check(EngineUploadKSK(ks, wa.data(), wb.data()));
         m_ksk = K;
     }
 
     static void PackMNTRU(const MNTRUCiphertextImpl& ct, uint32_t* dst, uint32_t k, uint32_t n) {
-        const auto& e = ct.GetElements();
-        if (e.size() != k)
-            OPENFHE_THROW(config_error, "ciphertext has the wrong number of parties");
-        for (uint32_t u = 0; u < k; ++u) {
-            if (e[u].GetLength() != n)
-                OPENFHE_THROW(config_error, "ciphertext has the wrong dimension");
-            for (uint32_t i = 0; i < n; ++i)
-                dst[u * n + i] = e[u][i].ConvertToInt<uint32_t>();
-        }
+        mkacc_pack::pack_vectors(ct.GetElements(), k, n, dst, Fail);
     }
     static void PackMKLWE(const MKLWECiphertextImpl& ct, uint32_t* dst, uint32_t k, uint32_t n) {
-        const auto& a = ct.GetA();
-        if (a.size() != k)
-            OPENFHE_THROW(config_error, "ciphertext has the wrong number of parties");
-        for (uint32_t u = 0; u < k; ++u) {
-            if (a[u].GetLength() != n)
-                OPENFHE_THROW(config_error, "ciphertext has the wrong dimension");
-            for (uint32_t i = 0; i < n; ++i)
-                dst[u * n + i] = a[u][i].ConvertToInt<uint32_t>();
-        }
+        mkacc_pack::pack_vectors(ct.GetA(), k, n, dst, Fail);
     }
 
     BINFHE_METHOD m_method;
-    int m_device;
+    std::vector<int> m_devices;
     std::shared_ptr<UniEncAccumulator> m_cpu;  // reference XZW / XZW_B: KeyGenAcc
     mutable std::mutex m_mu;
-    mutable mkacc_ctx* m_ctx = nullptr;
+    mutable mkacc_ctx* m_ctx     = nullptr;   // one device
+    mutable mkacc_group* m_group = nullptr;   // two or more
     mutable mkacc_params m_p{};
     mutable std::shared_ptr<const UniEncACCKeyImpl> m_key;
     mutable std::vector<Word> m_pkey;

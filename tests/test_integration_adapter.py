@@ -96,6 +96,8 @@ def test_a_broken_adapter_fails_the_check(tmp_path):
     for d in ("src/core/include", "src/core/lib", None, "third-party/cereal/include", "src/binfhe/include"):
         inc += ["-isystem", cfg if d is None else os.path.join(REF, d)]
     r = subprocess.run(["g++", "-std=gnu++17", "-fsyntax-only", "-pthread", "-Wall", "-Werror", *inc,
-                        "-I", str(tmp_path), "-I", os.path.join(ROOT, "include"), str(tu)],
+                        "-I", str(tmp_path), "-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROOT, "integration"),
+                        str(tu)],
                        capture_output=True, text=True, timeout=300)
     assert r.returncode != 0 and "override" in r.stderr
+
