@@ -92,6 +92,13 @@ def build_keys(force: bool = False, verbose: bool = False) -> str:
 # strategy spills 6) and ran 154.6-155.3 us per STD128_MKNTRU launch against
 # 159.0-159.9 (profiles/r3/ab_sched.txt); the ISA audit stays clean with it.
 STEP2_SCHED = {3: ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"]}
+# Shoup products of the transforms written in C (MKACC_BFLY_C, mkacc_device.hpp):
+# no s_nop per butterfly; -1.7 to -2.1 % per headline step, +0.6 % for mk_step_kernel
+# at dg = 4 (profiles/r5/ab_hl_bfly_c.txt), so only the later-step units of
+# mk_step2_kernel take it (dg = 2: -0.3 to -0.5 % per config-3 step,
+# profiles/r5/ab_c3_bfly_c.txt; its first-step kernels, a unit of their own,
+# would spill at dg = 3).
+STEP2_BFLY = {2: ["-DMKACC_BFLY_C=1"], 3: ["-DMKACC_BFLY_C=1"]}
 
 # Translation units of the engine library, compiled in parallel and linked into
 # one .so: the host unit (C ABI, batch / gate / primitive kernels) and the step
@@ -104,7 +111,10 @@ STEP2_SCHED = {3: ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"]}
 UNITS = [("engine", "mkacc_engine.hip", [])] + [
     (f"step_dg{d}", "mkacc_steps.hip", [f"-DMKACC_TU_DG={d}", "-DMKACC_TU_PART=0"]) for d in (4, 5)] + [
     (f"lat_dg{d}", "mkacc_steps.hip", [f"-DMKACC_TU_DG={d}", "-DMKACC_TU_PART=1"]) for d in (2, 3, 4)] + [
-    (f"step2_dg{d}", "mkacc_steps.hip", [f"-DMKACC_TU_DG={d}", "-DMKACC_TU_PART=2"] + STEP2_SCHED.get(d, []))
+    (f"step2_dg{d}", "mkacc_steps.hip", [f"-DMKACC_TU_DG={d}", "-DMKACC_TU_PART=2"] + STEP2_SCHED.get(d, []) +
+     STEP2_BFLY.get(d, []))
+    for d in (2, 3)] + [
+    (f"step2f_dg{d}", "mkacc_steps.hip", [f"-DMKACC_TU_DG={d}", "-DMKACC_TU_PART=3"] + STEP2_SCHED.get(d, []))
     for d in (2, 3)] + [
     ("wide", "mkacc_steps.hip", ["-DMKACC_TU_WIDE=1"]), ("widereg2", "mkacc_steps.hip", ["-DMKACC_TU_WIDE=2"])]
 

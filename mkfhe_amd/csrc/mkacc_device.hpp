@@ -224,9 +224,21 @@ __device__ __forceinline__ void transpose(uint32_t (&x)[kRegs], uint32_t* lds, u
 // instruction.  The inverse (GS) keeps values in [0, 2Q).
 // Forward twiddle pairs hold { -w mod 2^32, floor(w 2^32 / Q) }: the negated
 // Shoup product -T = q*Q - b*w is then two pinned multiply-adds.
+// MKACC_BFLY_C (a per-unit flag, mkfhe_amd/build.py): the Shoup product's two
+// multiply-adds written in C instead of pinned asm.  hipcc cannot see what an asm
+// statement does, so it puts an s_nop 0 before every VALU that reads a register an
+// asm statement wrote (one per butterfly: the second multiply-add reads the first's
+// result, or the add/sub reads the second's); in C it emits v_mul_lo_u32 +
+// v_mad_u64_u32 for the same low word and no wait state.  Faster for the headline
+// kernel (-1.7 to -2.1 % per step, profiles/r5/ab_hl_bfly_c.txt), slower for
+// mk_step_kernel at dg = 4 (+0.6 %, more registers), so only the step2 units set it.
+#ifndef MKACC_BFLY_C
+#define MKACC_BFLY_C 0
+#endif
 template <bool SW>
 __device__ __forceinline__ uint32_t shoup_neg(uint32_t b, uint2 w, uint32_t Q) {
     const uint32_t q = __umulhi(b, w.y);
+    if constexpr (MKACC_BFLY_C) return (uint32_t)((uint64_t)q * Q + (uint64_t)(b * w.x));
     return (uint32_t)mad64_pin<true>(q, Q, mul64_pin<SW>(b, w.x));   // -T, T in [0, 2Q)
 }
 template <bool SW = false>

@@ -102,8 +102,8 @@ int step_version(int dg) { return dg <= 3 ? 2 : 1; }
 const void* step_fn(int dg, int method, bool first, bool dscr, int ver) {
     if (ver == 2) {
         switch (dg) {
-            case 2: return mkacc_tu::step2_dg2(method, first);
-            case 3: return mkacc_tu::step2_dg3(method, first);
+            case 2: return first ? mkacc_tu::step2f_dg2(method) : mkacc_tu::step2_dg2(method);
+            case 3: return first ? mkacc_tu::step2f_dg3(method) : mkacc_tu::step2_dg3(method);
             default: return nullptr;
         }
     }

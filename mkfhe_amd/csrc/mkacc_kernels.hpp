@@ -148,6 +148,7 @@ __device__ __forceinline__ Mono make_mono(uint32_t c, uint32_t l) {
 // Lazy Shoup product x*w in [0, 2Q) (x < 2^32)
 __device__ __forceinline__ uint32_t mul_shoup_lazy(uint32_t x, uint2 w, uint32_t Q) {
     const uint32_t q = __umulhi(x, w.y);
+    if constexpr (MKACC_BFLY_C) return (uint32_t)((uint64_t)q * (0u - Q) + (uint64_t)(x * w.x));
     return (uint32_t)mad64_pin<true>(q, 0u - Q, mul64_pin<false>(x, w.x));   // x*w - q*Q in [0, 2Q)
 }
 
@@ -867,10 +868,9 @@ StepFn pick_step(int method, bool first, bool dscr) {
 #include "mkacc_step2.hpp"
 #include "mkacc_layout2.hpp"
 
-template <int DG>
-StepFn pick_step2(int method, bool first) {
-    if (method == XZW) return first ? mk_step2_kernel<DG, XZW, true> : mk_step2_kernel<DG, XZW, false>;
-    return first ? mk_step2_kernel<DG, XZW_B, true> : mk_step2_kernel<DG, XZW_B, false>;
+template <int DG, bool FIRST>
+StepFn pick_step2(int method) {
+    return method == XZW ? mk_step2_kernel<DG, XZW, FIRST> : mk_step2_kernel<DG, XZW_B, FIRST>;
 }
 
 template <int DG>
@@ -889,8 +889,10 @@ using KernelPtr = const void*;
 #define MKACC_TU_API __attribute__((visibility("hidden")))
 MKACC_TU_API KernelPtr step_dg4(int method, bool first, bool dscr);   // mk_step_kernel (dg >= 4)
 MKACC_TU_API KernelPtr step_dg5(int method, bool first, bool dscr);
-MKACC_TU_API KernelPtr step2_dg2(int method, bool first);   // mk_step2_kernel (mkacc_step2.hpp, dg <= 3)
-MKACC_TU_API KernelPtr step2_dg3(int method, bool first);
+MKACC_TU_API KernelPtr step2_dg2(int method);    // mk_step2_kernel (mkacc_step2.hpp, dg <= 3), later steps
+MKACC_TU_API KernelPtr step2_dg3(int method);
+MKACC_TU_API KernelPtr step2f_dg2(int method);   // its first (KDM) step, a unit of its own (build.py STEP2_BFLY)
+MKACC_TU_API KernelPtr step2f_dg3(int method);
 MKACC_TU_API KernelPtr lat_dg2(int method, bool first);
 MKACC_TU_API KernelPtr lat_dg3(int method, bool first);
 MKACC_TU_API KernelPtr lat_dg4(int method, bool first);

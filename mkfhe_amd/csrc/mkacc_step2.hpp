@@ -188,6 +188,21 @@ __device__ __forceinline__ void mac2(const StepCtx& s, uint32_t u, const uint32_
     vcc_fence();   // the caller's branches follow the last reductions
 }
 
+// digits I .. DG - 1 (unrolled by recursion: an unroll pragma over two whole
+// transforms is dropped when the body passes the unroller's threshold, and a G[i]
+// with a run-time i puts the whole G array in scratch memory)
+template <int DG, int I>
+__device__ __forceinline__ void digit_ntts_from(const StepCtx& s, const PackedDigits<DG>& pd,
+                                                uint32_t (&G)[DG][kRegs]) {
+    if constexpr (I < DG) {
+#pragma unroll
+        for (int r = 0; r < kRegs; ++r) G[I][r] = pd.get(r, I + 1, s.sd);
+        ntt_fwd(G[I], s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, s.l, s.m.Q, s.m.m1);
+        digit_range<DG>(G[I], s.m.Q);
+        digit_ntts_from<DG, I + 1>(s, pd, G);
+    }
+}
+
 // iNTT -> SDD -> dg forward NTTs: x (layout C, [0, 2Q)) -> G[i] = NTT(digit i + 1)
 template <int DG>
 __device__ __forceinline__ void digit_ntts(const StepCtx& s, uint32_t (&x)[kRegs], uint32_t (&G)[DG][kRegs]) {
@@ -202,13 +217,7 @@ __device__ __forceinline__ void digit_ntts(const StepCtx& s, uint32_t (&x)[kRegs
     }
     ntt_fwd(G[0], s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, s.l, Q, s.m.m1);
     digit_range<DG>(G[0], Q);
-#pragma unroll
-    for (int i = 1; i < DG; ++i) {
-#pragma unroll
-        for (int r = 0; r < kRegs; ++r) G[i][r] = pd.get(r, i + 1, s.sd);
-        ntt_fwd(G[i], s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, s.l, Q, s.m.m1);
-        digit_range<DG>(G[i], Q);
-    }
+    digit_ntts_from<DG, 1>(s, pd, G);
 }
 
 // two waves per SIMD (256 VGPRs): two 4-wave workgroups per CU

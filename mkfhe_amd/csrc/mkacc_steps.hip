@@ -2,7 +2,8 @@
 // build (mkfhe_amd/build.py) compiles this file once per unit, in parallel:
 //   -DMKACC_TU_DG=d -DMKACC_TU_PART=0   mk_step_kernel instantiations of digit count d (4, 5)
 //   -DMKACC_TU_DG=d -DMKACC_TU_PART=1   mk_lat_kernel instantiations of digit count d (2..4)
-//   -DMKACC_TU_DG=d -DMKACC_TU_PART=2   mk_step2_kernel instantiations of digit count d (2, 3)
+//   -DMKACC_TU_DG=d -DMKACC_TU_PART=2   mk_step2_kernel instantiations of digit count d (2, 3), later steps
+//   -DMKACC_TU_DG=d -DMKACC_TU_PART=3   the same kernel's first (KDM) step
 //   -DMKACC_TU_WIDE=1 / 2               64-bit word step kernels (integer / FP64 register-resident)
 // and the host unit (mkacc_engine.hip) launches them through mkacc_tu.
 #include "mkacc_kernels.hpp"
@@ -40,10 +41,10 @@ KernelPtr MKACC_CAT(step_dg, MKACC_TU_DG)(int method, bool first, bool dscr) {
 KernelPtr MKACC_CAT(lat_dg, MKACC_TU_DG)(int method, bool first) {
     return (KernelPtr)pick_lat<MKACC_TU_DG>(method, first);
 }
+#elif MKACC_TU_PART == 2
+KernelPtr MKACC_CAT(step2_dg, MKACC_TU_DG)(int method) { return (KernelPtr)pick_step2<MKACC_TU_DG, false>(method); }
 #else
-KernelPtr MKACC_CAT(step2_dg, MKACC_TU_DG)(int method, bool first) {
-    return (KernelPtr)pick_step2<MKACC_TU_DG>(method, first);
-}
+KernelPtr MKACC_CAT(step2f_dg, MKACC_TU_DG)(int method) { return (KernelPtr)pick_step2<MKACC_TU_DG, true>(method); }
 #endif
 }  // namespace mkacc_tu
 
