@@ -99,6 +99,9 @@ STEP2_SCHED = {3: ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"]}
 # profiles/r5/ab_c3_bfly_c.txt; its first-step kernels, a unit of their own,
 # would spill at dg = 3).
 STEP2_BFLY = {2: ["-DMKACC_BFLY_C=1"], 3: ["-DMKACC_BFLY_C=1"]}
+# and mk_lat_kernel (small batches, few waves per SIMD to hide a wait state): a
+# 64-gate STD128_MKNTRU batch 65.7 -> 63.0 ms (profiles/r5/ab_lat_bfly_c.txt)
+LAT_BFLY = ["-DMKACC_BFLY_C=1"]
 
 # Translation units of the engine library, compiled in parallel and linked into
 # one .so: the host unit (C ABI, batch / gate / primitive kernels) and the step
@@ -110,7 +113,7 @@ STEP2_BFLY = {2: ["-DMKACC_BFLY_C=1"], 3: ["-DMKACC_BFLY_C=1"]}
 # lost their A/B runs; DESIGN.md s7 keeps their records).
 UNITS = [("engine", "mkacc_engine.hip", [])] + [
     (f"step_dg{d}", "mkacc_steps.hip", [f"-DMKACC_TU_DG={d}", "-DMKACC_TU_PART=0"]) for d in (4, 5)] + [
-    (f"lat_dg{d}", "mkacc_steps.hip", [f"-DMKACC_TU_DG={d}", "-DMKACC_TU_PART=1"]) for d in (2, 3, 4)] + [
+    (f"lat_dg{d}", "mkacc_steps.hip", [f"-DMKACC_TU_DG={d}", "-DMKACC_TU_PART=1"] + LAT_BFLY) for d in (2, 3, 4)] + [
     (f"step2_dg{d}", "mkacc_steps.hip", [f"-DMKACC_TU_DG={d}", "-DMKACC_TU_PART=2"] + STEP2_SCHED.get(d, []) +
      STEP2_BFLY.get(d, []))
     for d in (2, 3)] + [

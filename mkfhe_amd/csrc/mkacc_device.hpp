@@ -230,8 +230,9 @@ __device__ __forceinline__ void transpose(uint32_t (&x)[kRegs], uint32_t* lds, u
 // asm statement wrote (one per butterfly: the second multiply-add reads the first's
 // result, or the add/sub reads the second's); in C it emits v_mul_lo_u32 +
 // v_mad_u64_u32 for the same low word and no wait state.  Faster for the headline
-// kernel (-1.7 to -2.1 % per step, profiles/r5/ab_hl_bfly_c.txt), slower for
-// mk_step_kernel at dg = 4 (+0.6 %, more registers), so only the step2 units set it.
+// kernel (-1.7 to -2.1 % per step, profiles/r5/ab_hl_bfly_c.txt) and for
+// mk_lat_kernel (-4 %, ab_lat_bfly_c.txt), slower for mk_step_kernel at dg = 4
+// (+0.6 %, more registers): build.py sets it for the step2 and lat units.
 #ifndef MKACC_BFLY_C
 #define MKACC_BFLY_C 0
 #endif
