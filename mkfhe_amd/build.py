@@ -102,6 +102,10 @@ STEP2_BFLY = {2: ["-DMKACC_BFLY_C=1"], 3: ["-DMKACC_BFLY_C=1"]}
 # and mk_lat_kernel (small batches, few waves per SIMD to hide a wait state): a
 # 64-gate STD128_MKNTRU batch 65.7 -> 63.0 ms (profiles/r5/ab_lat_bfly_c.txt)
 LAT_BFLY = ["-DMKACC_BFLY_C=1"]
+# mk_step_kernel at dg = 4 (config 4): the forward transforms only (MKACC_BFLY_C=2);
+# in every transform it needs 8 B of scratch and is 0.6 % slower, forward-only is
+# spill-free and 1.0-1.1 % faster (profiles/r5/ab_c4_bfly_c.txt)
+STEP_BFLY = {4: ["-DMKACC_BFLY_C=2"]}
 
 # Translation units of the engine library, compiled in parallel and linked into
 # one .so: the host unit (C ABI, batch / gate / primitive kernels) and the step
@@ -112,7 +116,8 @@ LAT_BFLY = ["-DMKACC_BFLY_C=1"]
 # below 2^50 and the integer 64-bit kernel above (round 5 retired the variants that
 # lost their A/B runs; DESIGN.md s7 keeps their records).
 UNITS = [("engine", "mkacc_engine.hip", [])] + [
-    (f"step_dg{d}", "mkacc_steps.hip", [f"-DMKACC_TU_DG={d}", "-DMKACC_TU_PART=0"]) for d in (4, 5)] + [
+    (f"step_dg{d}", "mkacc_steps.hip", [f"-DMKACC_TU_DG={d}", "-DMKACC_TU_PART=0"] + STEP_BFLY.get(d, []))
+    for d in (4, 5)] + [
     (f"lat_dg{d}", "mkacc_steps.hip", [f"-DMKACC_TU_DG={d}", "-DMKACC_TU_PART=1"] + LAT_BFLY) for d in (2, 3, 4)] + [
     (f"step2_dg{d}", "mkacc_steps.hip", [f"-DMKACC_TU_DG={d}", "-DMKACC_TU_PART=2"] + STEP2_SCHED.get(d, []) +
      STEP2_BFLY.get(d, []))

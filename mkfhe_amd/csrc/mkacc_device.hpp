@@ -231,29 +231,34 @@ __device__ __forceinline__ void transpose(uint32_t (&x)[kRegs], uint32_t* lds, u
 // result, or the add/sub reads the second's); in C it emits v_mul_lo_u32 +
 // v_mad_u64_u32 for the same low word and no wait state.  Faster for the headline
 // kernel (-1.7 to -2.1 % per step, profiles/r5/ab_hl_bfly_c.txt) and for
-// mk_lat_kernel (-4 %, ab_lat_bfly_c.txt), slower for mk_step_kernel at dg = 4
-// (+0.6 %, more registers): build.py sets it for the step2 and lat units.
+// mk_lat_kernel (-4 %, ab_lat_bfly_c.txt): build.py sets 1 (every product) for the
+// step2 and lat units.  mk_step_kernel at dg = 4 needs more registers with it (8 B
+// of scratch, +0.6 %); 2 (the forward transforms only) is spill-free there and
+// 1.0-1.1 % faster (ab_c4_bfly_c.txt); 3 is the inverse only.
 #ifndef MKACC_BFLY_C
 #define MKACC_BFLY_C 0
 #endif
-template <bool SW>
+constexpr bool kFwdC = MKACC_BFLY_C == 1 || MKACC_BFLY_C == 2;
+constexpr bool kInvC = MKACC_BFLY_C == 1 || MKACC_BFLY_C == 3;
+template <bool SW, bool C>
 __device__ __forceinline__ uint32_t shoup_neg(uint32_t b, uint2 w, uint32_t Q) {
     const uint32_t q = __umulhi(b, w.y);
-    if constexpr (MKACC_BFLY_C) return (uint32_t)((uint64_t)q * Q + (uint64_t)(b * w.x));
+    if constexpr (C) return (uint32_t)((uint64_t)q * Q + (uint64_t)(b * w.x));
     return (uint32_t)mad64_pin<true>(q, Q, mul64_pin<SW>(b, w.x));   // -T, T in [0, 2Q)
 }
-template <bool SW = false>
+template <bool SW, bool C>
 __device__ __forceinline__ void ct_bfly_lazy(uint32_t& a, uint32_t& b, uint2 w, uint32_t Q) {
     const uint32_t X = a;
-    const uint32_t Tn = shoup_neg<SW>(b, w, Q);
+    const uint32_t Tn = shoup_neg<SW, C>(b, w, Q);
     a = X - Tn;                                                  // X + T
     b = X + Tn + 2u * Q;                                         // X - T + 2Q
 }
 // last stage: a in [0, 24Q) -> X in [0, 2Q) as Shoup's product by 1
 // (companion m1 = floor(2^32 / Q)); outputs in [0, 4Q)
+template <bool C>
 __device__ __forceinline__ void ct_bfly_last(uint32_t& a, uint32_t& b, uint2 w, uint32_t Q, uint32_t m1) {
     const uint32_t X = a - __umulhi(a, m1) * Q;                  // [0, 2Q)
-    const uint32_t Tn = shoup_neg<false>(b, w, Q);
+    const uint32_t Tn = shoup_neg<false, C>(b, w, Q);
     a = X - Tn;                                                  // [0, 4Q)
     b = X + Tn + 2u * Q;                                         // (0, 4Q)
 }
@@ -349,7 +354,7 @@ struct FwdAApply {
             if (r & H) continue;
             const int m = r >> (5 - S);
             if (m < M0 || m >= M0 + CNT) continue;
-            ct_bfly_lazy<true>(x[r], x[r + H], w[m - M0], Q);
+            ct_bfly_lazy<true, kFwdC>(x[r], x[r + H], w[m - M0], Q);
         }
     }
 };
@@ -387,12 +392,12 @@ struct FwdApply {
                 if (r & H) continue;
                 const int m = r >> SH;
                 if (m < M0 || m >= M0 + CNT) continue;
-                ct_bfly_lazy(x[r], x[r + H], w[m - M0], Q);
+                ct_bfly_lazy<false, kFwdC>(x[r], x[r + H], w[m - M0], Q);
             }
         } else {
             if constexpr (M0 == 0) transpose<1, 2>(x, lds, l);
 #pragma unroll
-            for (int j = 0; j < CNT; ++j) ct_bfly_last(x[2 * (M0 + j)], x[2 * (M0 + j) + 1], w[j], Q, m1);
+            for (int j = 0; j < CNT; ++j) ct_bfly_last<kFwdC>(x[2 * (M0 + j)], x[2 * (M0 + j) + 1], w[j], Q, m1);
         }
     }
 };
@@ -517,7 +522,7 @@ struct Inv1Apply {
                 x[r] = X + Y;
                 x[r + H] = X - Y + (uint32_t)kInvPlan.bound[S][r + H] * Q;
             } else {
-                ct_bfly_lazy<true>(x[r], x[r + H], w[t - M0], Q);
+                ct_bfly_lazy<true, kInvC>(x[r], x[r + H], w[t - M0], Q);
             }
         }
     }
@@ -558,12 +563,12 @@ struct InvApply {
                 if (r & H) continue;
                 const int m = r & (H - 1);
                 if (m < M0 || m >= M0 + CNT) continue;
-                ct_bfly_lazy(x[r], x[r + H], w[m - M0], Q);
+                ct_bfly_lazy<false, kInvC>(x[r], x[r + H], w[m - M0], Q);
             }
         } else if constexpr (S == 10) {
             if constexpr (M0 == 0) transpose<3, 0>(x, lds, l);
 #pragma unroll
-            for (int j = 0; j < CNT; ++j) ct_bfly_lazy(x[M0 + j], x[M0 + j + 16], w[j], Q);
+            for (int j = 0; j < CNT; ++j) ct_bfly_lazy<false, kInvC>(x[M0 + j], x[M0 + j + 16], w[j], Q);
         } else {
 #pragma unroll
             for (int j = 0; j < CNT; ++j) x[M0 + j] = mul_shoup(x[M0 + j], w[j].x, w[j].y, Q);

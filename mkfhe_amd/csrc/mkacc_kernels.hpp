@@ -148,7 +148,7 @@ __device__ __forceinline__ Mono make_mono(uint32_t c, uint32_t l) {
 // Lazy Shoup product x*w in [0, 2Q) (x < 2^32)
 __device__ __forceinline__ uint32_t mul_shoup_lazy(uint32_t x, uint2 w, uint32_t Q) {
     const uint32_t q = __umulhi(x, w.y);
-    if constexpr (MKACC_BFLY_C) return (uint32_t)((uint64_t)q * (0u - Q) + (uint64_t)(x * w.x));
+    if constexpr (MKACC_BFLY_C == 1) return (uint32_t)((uint64_t)q * (0u - Q) + (uint64_t)(x * w.x));
     return (uint32_t)mad64_pin<true>(q, 0u - Q, mul64_pin<false>(x, w.x));   // x*w - q*Q in [0, 2Q)
 }
 
