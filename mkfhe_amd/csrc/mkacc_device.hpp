@@ -234,7 +234,9 @@ __device__ __forceinline__ void transpose(uint32_t (&x)[kRegs], uint32_t* lds, u
 // mk_lat_kernel (-4 %, ab_lat_bfly_c.txt): build.py sets 1 (every product) for the
 // step2 and lat units.  mk_step_kernel at dg = 4 needs more registers with it (8 B
 // of scratch, +0.6 %); 2 (the forward transforms only) is spill-free there and
-// 1.0-1.1 % faster (ab_c4_bfly_c.txt); 3 is the inverse only.
+// 1.0-1.1 % faster (ab_c4_bfly_c.txt) -- in the MK-NTRU kernels only: the MK-LWE
+// (XZW_B) one at dg = 4 would spill 16 B (mkacc_kernels.hpp fwd_c); 3 is the
+// inverse only.
 #ifndef MKACC_BFLY_C
 #define MKACC_BFLY_C 0
 #endif
@@ -343,6 +345,7 @@ struct FwdALoad {
         for (int j = 0; j < CNT; ++j) w[j] = twc[(1 << S) + M0 + j];
     }
 };
+template <bool C>
 struct FwdAApply {
     uint32_t (&x)[kRegs];
     uint32_t Q;
@@ -354,7 +357,7 @@ struct FwdAApply {
             if (r & H) continue;
             const int m = r >> (5 - S);
             if (m < M0 || m >= M0 + CNT) continue;
-            ct_bfly_lazy<true, kFwdC>(x[r], x[r + H], w[m - M0], Q);
+            ct_bfly_lazy<true, C>(x[r], x[r + H], w[m - M0], Q);
         }
     }
 };
@@ -379,6 +382,7 @@ struct FwdLoad {
         for (int j = 0; j < CNT; ++j) w[j] = S < 10 ? twl[twl_off(S < 10 ? S : 5) + 32 * (M0 + j)] : tw10[64 * (M0 + j)];
     }
 };
+template <bool C>
 struct FwdApply {
     uint32_t (&x)[kRegs];
     uint32_t* lds;
@@ -392,12 +396,12 @@ struct FwdApply {
                 if (r & H) continue;
                 const int m = r >> SH;
                 if (m < M0 || m >= M0 + CNT) continue;
-                ct_bfly_lazy<false, kFwdC>(x[r], x[r + H], w[m - M0], Q);
+                ct_bfly_lazy<false, C>(x[r], x[r + H], w[m - M0], Q);
             }
         } else {
             if constexpr (M0 == 0) transpose<1, 2>(x, lds, l);
 #pragma unroll
-            for (int j = 0; j < CNT; ++j) ct_bfly_last<kFwdC>(x[2 * (M0 + j)], x[2 * (M0 + j) + 1], w[j], Q, m1);
+            for (int j = 0; j < CNT; ++j) ct_bfly_last<C>(x[2 * (M0 + j)], x[2 * (M0 + j) + 1], w[j], Q, m1);
         }
     }
 };
@@ -409,13 +413,14 @@ struct FwdApply {
 // Input residues in [0, 4Q); output EVAL values in [0, 4Q) (not canonical).
 //   tw10 : stage-10 twiddles (pairs (m, lane) at tw10 + 64*m + lane); twl + kTwlC
 //          or a copy of that block in LDS
+template <bool C = kFwdC>
 __device__ __forceinline__ void ntt_fwd(uint32_t (&x)[kRegs], uint32_t* lds, const uint2* tw_g, const uint2* twl,
                                         const uint2* tw10, uint32_t l, uint32_t Q, uint32_t m1) {
     // pass A: stages 0..4 (bits 10..6); twiddle index uniform across the wave
     const ConstTable twc{(const_u64*)opaque(tw_g)};
     {
         const FwdALoad ld{twc};
-        const FwdAApply ap{x, Q};
+        const FwdAApply<C> ap{x, Q};
         uint2 sa[8], sb[8];
         ld.template go<0, 0, 1>(sa);
         tw_pipe<FwdASeq, 0>(sa, sb, ld, ap);
@@ -424,7 +429,7 @@ __device__ __forceinline__ void ntt_fwd(uint32_t (&x)[kRegs], uint32_t* lds, con
     // passes B (stages 5..9, bits 5..1) and C (stage 10, bit 0), one twiddle stream
     {
         const FwdLoad ld(twl, tw10, lo);
-        const FwdApply ap{x, lds, l, Q, m1};
+        const FwdApply<C> ap{x, lds, l, Q, m1};
         uint2 wa[4], wb[4];
         ld.template go<5, 0, 1>(wa);
         transpose<0, 1>(x, lds, l);
@@ -505,6 +510,7 @@ struct Inv1Load {
         for (int j = 0; j < CNT; ++j) w[j] = twc[(1 << S) + M0 + j];
     }
 };
+template <bool C>
 struct Inv1Apply {
     uint32_t (&x)[kRegs];
     uint32_t Q;
@@ -522,7 +528,7 @@ struct Inv1Apply {
                 x[r] = X + Y;
                 x[r + H] = X - Y + (uint32_t)kInvPlan.bound[S][r + H] * Q;
             } else {
-                ct_bfly_lazy<true, kInvC>(x[r], x[r + H], w[t - M0], Q);
+                ct_bfly_lazy<true, C>(x[r], x[r + H], w[t - M0], Q);
             }
         }
     }
@@ -550,6 +556,7 @@ struct InvLoad {
                           : t64[(S == 10 ? kTwlC : kTwlPairs) + 64 * (M0 + j)];
     }
 };
+template <bool C>
 struct InvApply {
     uint32_t (&x)[kRegs];
     uint32_t* lds;
@@ -563,12 +570,12 @@ struct InvApply {
                 if (r & H) continue;
                 const int m = r & (H - 1);
                 if (m < M0 || m >= M0 + CNT) continue;
-                ct_bfly_lazy<false, kInvC>(x[r], x[r + H], w[m - M0], Q);
+                ct_bfly_lazy<false, C>(x[r], x[r + H], w[m - M0], Q);
             }
         } else if constexpr (S == 10) {
             if constexpr (M0 == 0) transpose<3, 0>(x, lds, l);
 #pragma unroll
-            for (int j = 0; j < CNT; ++j) ct_bfly_lazy<false, kInvC>(x[M0 + j], x[M0 + j + 16], w[j], Q);
+            for (int j = 0; j < CNT; ++j) ct_bfly_lazy<false, C>(x[M0 + j], x[M0 + j + 16], w[j], Q);
         } else {
 #pragma unroll
             for (int j = 0; j < CNT; ++j) x[M0 + j] = mul_shoup(x[M0 + j], w[j].x, w[j].y, Q);
@@ -577,20 +584,21 @@ struct InvApply {
 };
 
 // Input residues in [0, 2Q), layout C; output canonical coefficients, layout A.
+template <bool C = kInvC>
 __device__ __forceinline__ void ntt_inv(uint32_t (&x)[kRegs], uint32_t* lds, const uint2* tis, const uint2* twl,
                                         uint32_t l, uint32_t Q) {
     // pass 1: bits 0..4 on registers, twiddle index (r mod 2^b) wave-uniform
     const ConstTable twc{(const_u64*)opaque(tis)};
     {
         const Inv1Load ld{twc};
-        const Inv1Apply ap{x, Q};
+        const Inv1Apply<C> ap{x, Q};
         uint2 sa[8], sb[8];
         tw_pipe<Inv1Seq, 0>(sa, sb, ld, ap);
     }
     const uint32_t lo = opaque_v(l);
     {
         const InvLoad ld(twl, lo);
-        const InvApply ap{x, lds, l, Q};
+        const InvApply<C> ap{x, lds, l, Q};
         uint2 wa[4], wb[4];
         ld.template go<5, 0, 1>(wa);
         transpose<2, 3>(x, lds, l);

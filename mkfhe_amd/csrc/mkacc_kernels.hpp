@@ -145,6 +145,10 @@ __device__ __forceinline__ Mono make_mono(uint32_t c, uint32_t l) {
     return Mono{psi_pos(co) << 3, c};
 }
 
+// MKACC_BFLY_C = 2 (forward transforms in C) for the MK-NTRU step kernels only
+template <int METHOD>
+constexpr bool fwd_c = kFwdC && !(MKACC_BFLY_C == 2 && METHOD != XZW);
+
 // Lazy Shoup product x*w in [0, 2Q) (x < 2^32)
 __device__ __forceinline__ uint32_t mul_shoup_lazy(uint32_t x, uint2 w, uint32_t Q) {
     const uint32_t q = __umulhi(x, w.y);
@@ -448,7 +452,7 @@ __device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_
     {
         const DigitMac<DG, METHOD, FIRST, true, DS, kCanon> mac(sr, 0, u);
         KeyGroup kg[mac.kBuf];
-        ntt_fwd(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, s.l, Q, s.m.m1);
+        ntt_fwd<fwd_c<METHOD>>(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, s.l, Q, s.m.m1);
         digit_range<DG>(x, Q);
 #pragma unroll
         for (int j = 0; j < mac.kPrefetch; ++j) mac.issue(kg[j], j);
@@ -461,7 +465,7 @@ __device__ __forceinline__ void party_pass(const StepCtx& s, uint32_t u, uint64_
         for (int r = 0; r < kRegs; ++r) x[r] = pd.get(r, j + 1, s.sd);
         const DigitMac<DG, METHOD, FIRST, false, DS, kCanon> mac(sr, j, u);
         KeyGroup kg[mac.kBuf];
-        ntt_fwd(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, s.l, Q, s.m.m1);
+        ntt_fwd<fwd_c<METHOD>>(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, s.l, Q, s.m.m1);
         digit_range<DG>(x, Q);
 #pragma unroll
         for (int j = 0; j < mac.kPrefetch; ++j) mac.issue(kg[j], j);
@@ -695,13 +699,13 @@ __device__ __forceinline__ void f_part(const StepCtx& s, uint32_t index, uint64_
         if constexpr (kSplit) {
             const SplitMac<DG> mac(sr, i);
             KeyGroup kg[mac.kBuf];
-            ntt_fwd(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, l, Q, s.m.m1);
+            ntt_fwd<fwd_c<METHOD>>(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, l, Q, s.m.m1);
             digit_range<DG>(x, Q);
 #pragma unroll
             for (int j = 0; j < mac.kPrefetch; ++j) mac.issue(kg[j], j);
             mac.run(x, w, w2, kg);
         } else {
-            ntt_fwd(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, l, Q, s.m.m1);
+            ntt_fwd<fwd_c<METHOD>>(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, l, Q, s.m.m1);
             digit_range<DG>(x, Q);
             mac_index<DG, METHOD, FIRST>(x, i, w, s.rk1, s.rk2, s.rks, s.tb.psi, s.mp, s.mn, s.vo, Q);
         }
