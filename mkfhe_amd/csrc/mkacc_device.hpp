@@ -235,13 +235,13 @@ __device__ __forceinline__ void transpose(uint32_t (&x)[kRegs], uint32_t* lds, u
 // step2 and lat units.  mk_step_kernel at dg = 4 needs more registers with it (8 B
 // of scratch, +0.6 %); 2 (the forward transforms only) is spill-free there and
 // 1.0-1.1 % faster (ab_c4_bfly_c.txt) -- in the MK-NTRU kernels only: the MK-LWE
-// (XZW_B) one at dg = 4 would spill 16 B (mkacc_kernels.hpp fwd_c); 3 is the
-// inverse only.
+// (XZW_B) one at dg = 4 would spill 16 B (mkacc_kernels.hpp fwd_c).
 #ifndef MKACC_BFLY_C
 #define MKACC_BFLY_C 0
 #endif
 constexpr bool kFwdC = MKACC_BFLY_C == 1 || MKACC_BFLY_C == 2;
-constexpr bool kInvC = MKACC_BFLY_C == 1 || MKACC_BFLY_C == 3;
+constexpr bool kInvC = MKACC_BFLY_C == 1;
+static_assert(MKACC_BFLY_C >= 0 && MKACC_BFLY_C <= 2, "MKACC_BFLY_C: 0 (asm), 1 (C), 2 (C in the forward transforms)");
 template <bool SW, bool C>
 __device__ __forceinline__ uint32_t shoup_neg(uint32_t b, uint2 w, uint32_t Q) {
     const uint32_t q = __umulhi(b, w.y);
