@@ -77,7 +77,7 @@ def test_wide_evalacc_bitexact(mk_gpu, oracle, method, k, n, baseG, B):
 
 
 # variant -> (MKACC_WIDE_FP, step kernel)
-VARIANTS = {"fp64": ("1", "widereg2::steps_kernel"), "int": ("0", "wide::step_kernel")}
+VARIANTS = {"fp64": ("1", "widereg2::step_kernel"), "int": ("0", "wide::step_kernel")}
 
 
 @pytest.mark.gpu
@@ -138,7 +138,7 @@ def test_wide_register_kernel_loops_and_slices(mk_gpu, oracle, monkeypatch, meth
     for ns in ("1", streams):
         monkeypatch.setenv("MKACC_STREAMS", ns)
         eng = _eng(mk, mk.MKNTRU if method == "XZW" else mk.MKNTRU_LWE, k, n, Q50, 45181, 1 << 10)
-        assert eng.step_kernel_name(B) == "widereg2::steps_kernel"
+        assert eng.step_kernel_name(B) == "widereg2::step_kernel"
         eng.upload_keys(evk.astype(np.uint64), pkey.astype(np.uint64))
         outs[ns] = eng.eval_batch(ct.astype(np.uint32), acc.astype(np.uint64))
     got = outs[streams]
