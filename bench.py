@@ -463,7 +463,7 @@ def run_rank(args, env: dict, make_engine, make_checker, torch_device: str, back
         # (mkacc_engine.hip launch_steps / wide_launch_batch): one accumulator step of the
         # batch is then `slices` launches, and per_launch_us is the time of one such step
         slices = 1
-        if is_cuda and kname in ("mk_step_kernel", "mk_step2_kernel", "widereg2::step_kernel", "widereg2::steps_kernel"):
+        if is_cuda and kname in ("mk_step_kernel", "mk_step2_kernel", "mk_step3_kernel", "widereg2::step_kernel"):
             import torch
             cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
             ev = os.environ.get("MKACC_STREAMS", "")
@@ -509,12 +509,8 @@ def run_rank(args, env: dict, make_engine, make_checker, torch_device: str, back
                          "bytes_per_launch": by,
                          "slices_per_step": slices,
                          "launch_note": ("one accumulator step of the whole batch: " + (
-                             f"{slices} concurrent slices of {B // slices}+ gates on {slices} streams" if slices > 1
-                             else "one slice") + (
-                             "; every later step of a party runs in one launch per slice (widereg2::steps_kernel), "
-                             "so per_launch_us is the EvalAcc time / (k n)"
-                             if kname == "widereg2::steps_kernel" else
-                             "; rocprof lists each slice launch with its own (overlapping) duration"))},
+                             f"{slices} concurrent launches of {B // slices}+ gates on {slices} streams; rocprof lists each "
+                             "slice launch with its own (overlapping) duration" if slices > 1 else "one launch"))},
             # VALU view: algorithmic mod-muls per launch against the measured rate of the
             # product the kernel is built on (32-bit Shoup; FP64 or 64-bit Shoup on the wide path)
             "roofline_valu": {

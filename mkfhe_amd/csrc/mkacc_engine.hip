@@ -939,51 +939,37 @@ int wide_launch_batch(mkacc_ctx* c, const uint32_t* d_ct, const uint64_t* d_in, 
                 join.ns = j + 1;
             }
         }
-        // the first step (AddToAccXZW0) cur -> nxt, then every later step of a party in
-        // one launch, in place in nxt (widereg2::steps_kernel)
-        auto args = [&](size_t j, uint32_t u, uint32_t i, const double* in, double* out) {
-            const size_t g0 = j * per, Bh = j + 1 < ns ? per : B - g0;
-            const size_t ao = g0 * k * kN;
-            widereg2::StepArgs a;
-            a.acc_in = in + ao;
-            a.acc_out = out + ao;
-            a.cvals = c->d_wcvals + ((size_t)u * n + i) * B + g0;
-            a.key1 = dk(key(u, i, 0));
-            a.key2 = dk(c->nk == 2 ? key(u, i, 1) : key(u, i, 0));
-            a.keys = dk(key(0, n, 0));
-            a.pkey = dk(c->d_wpkey);
-            a.tab = c->d_r2tab;
-            a.psi = c->d_fpsi;
-            a.twf = c->d_ftwf;
-            a.tis = c->d_rtis;
-            a.B = (uint32_t)Bh;
-            a.k = k;
-            a.index = u;
-            a.dg = c->dg;
-            a.cL = c->wfcL;
-            a.Cm = c->wfCm;
-            a.m = c->wfm;
-            a.sd = c->wsd;
-            return a;
-        };
-        for (size_t j = 0; j < ns; ++j) {
-            const size_t Bh = j + 1 < ns ? per : B - j * per;
-            hipStream_t st = j == 0 ? c->stream : c->xs[j - 1];
-            launch_ptr(mkacc_tu::widereg2_step(c->method_class, true), dim3((unsigned)std::min<size_t>(Bh, unit)),
-                       dim3(128), widereg2::kLdsBytes, st, args(j, 0, 0, cur, nxt));
-            for (uint32_t u = 0; u < k; ++u) {
-                const uint32_t i0 = u == 0 ? 1u : 0u;
-                if (i0 >= n) continue;
-                widereg2::StepsArgs f;
-                f.s = args(j, u, i0, nxt, nxt);
-                f.steps = n - i0;
-                f.cstride = (uint32_t)B;
-                f.key_step = (size_t)c->nk * blk;
-                launch_ptr(mkacc_tu::widereg2_steps(c->method_class), dim3((unsigned)std::min<size_t>(Bh, unit)),
-                           dim3(128), widereg2::kLdsBytes, st, f);
+        for (uint32_t u = 0; u < k; ++u)
+            for (uint32_t i = 0; i < n; ++i)
+            for (size_t j = 0; j < ns; ++j) {
+                const size_t g0 = j * per, Bh = j + 1 < ns ? per : B - g0;
+                const size_t ao = g0 * k * kN;
+                const bool first = (u == 0 && i == 0);
+                widereg2::StepArgs a;
+                a.acc_in = cur + ao;
+                a.acc_out = nxt + ao;
+                a.cvals = c->d_wcvals + ((size_t)u * n + i) * B + g0;
+                a.key1 = dk(key(u, i, 0));
+                a.key2 = dk(c->nk == 2 ? key(u, i, 1) : key(u, i, 0));
+                a.keys = dk(key(0, n, 0));
+                a.pkey = dk(c->d_wpkey);
+                a.tab = c->d_r2tab;
+                a.psi = c->d_fpsi;
+                a.twf = c->d_ftwf;
+                a.tis = c->d_rtis;
+                a.B = (uint32_t)Bh;
+                a.k = k;
+                a.index = u;
+                a.dg = c->dg;
+                a.cL = c->wfcL;
+                a.Cm = c->wfCm;
+                a.m = c->wfm;
+                a.sd = c->wsd;
+                launch_ptr(mkacc_tu::widereg2_step(c->method_class, first),
+                           dim3((unsigned)std::min<size_t>(Bh, unit)), dim3(128), widereg2::kLdsBytes,
+                           j == 0 ? c->stream : c->xs[j - 1], a);
+                if (j + 1 == ns) std::swap(cur, nxt);
             }
-        }
-        std::swap(cur, nxt);
         join.join();
         if (!join.ok) return fail(MKACC_E_DEVICE, "joining the batch slice streams failed");
         hipLaunchKernelGGL(widereg2::from_c16_kernel, g, dim3(256), 0, c->stream, cur, d_out, words, c->wfm);
@@ -1376,8 +1362,7 @@ int mkacc_upload_keys_device(mkacc_ctx* c, const void* d_evk, const void* d_pkey
 const char* mkacc_step_kernel_name(const mkacc_ctx* c, size_t B) {
     if (!c) return "";
     if (c->wide)
-        return c->wfp ? (c->p.k * (size_t)c->p.n > 1 ? "widereg2::steps_kernel" : "widereg2::step_kernel")
-                      : "wide::step_kernel";
+        return c->wfp ? "widereg2::step_kernel" : "wide::step_kernel";
     if (use_lat(c, B)) return "mk_lat_kernel";
     return c->step_ver == 2 ? "mk_step2_kernel" : "mk_step_kernel";
 }

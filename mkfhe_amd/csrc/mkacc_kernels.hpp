@@ -902,5 +902,4 @@ MKACC_TU_API KernelPtr lat_dg3(int method, bool first);
 MKACC_TU_API KernelPtr lat_dg4(int method, bool first);
 MKACC_TU_API KernelPtr wide_step(int method, bool first);     // mkacc_wide.hpp (integer 64-bit words)
 MKACC_TU_API KernelPtr widereg2_step(int method, bool first);  // mkacc_widereg2.hpp (FP64, Q < 2^50)
-MKACC_TU_API KernelPtr widereg2_steps(int method);             // its later steps of one party, fused
 }  // namespace mkacc_tu

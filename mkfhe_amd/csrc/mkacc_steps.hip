@@ -21,9 +21,6 @@ KernelPtr widereg2_step(int method, bool first) {
         return first ? (KernelPtr)widereg2::step_kernel<XZW, true> : (KernelPtr)widereg2::step_kernel<XZW, false>;
     return first ? (KernelPtr)widereg2::step_kernel<XZW_B, true> : (KernelPtr)widereg2::step_kernel<XZW_B, false>;
 }
-KernelPtr widereg2_steps(int method) {
-    return method == XZW ? (KernelPtr)widereg2::steps_kernel<XZW> : (KernelPtr)widereg2::steps_kernel<XZW_B>;
-}
 #else
 KernelPtr wide_step(int method, bool first) {
     if (method == XZW) return first ? (KernelPtr)wide::step_kernel<XZW, true> : (KernelPtr)wide::step_kernel<XZW, false>;

@@ -452,41 +452,6 @@ __global__ __launch_bounds__(128, 2) void step_kernel(StepArgs a) {
     for (uint32_t gate = blockIdx.x; gate < a.B; gate += gridDim.x) one_gate<METHOD, FIRST>(a, gate, bufs, ln);
 }
 
-// Steps i0 .. i1 - 1 of party `index` in one launch (the later steps: FIRST is
-// the separate step_kernel launch).  Per-step launches cost the ramp and the tail
-// of every launch (the waves are alive for 82 % of a one-stream step launch,
-// profiles/r5/pmc_c5_v5.txt); here each gate runs its steps back to back in place
-// (acc_in == acc_out: every wave reads and writes only its own half of each
-// polynomial, and a party pass writes only the polynomial it read), the step's
-// stores drained before the next step's loads.  Step i's keys sit key_step
-// doubles after step i0's, its exponents cstride words after.
-struct StepsArgs {
-    StepArgs s;            // step i0; acc_in == acc_out
-    uint32_t steps;        // i1 - i0
-    uint32_t cstride;      // words between the exponents of consecutive steps (the whole batch)
-    size_t key_step;       // doubles between the key blocks of consecutive steps
-};
-template <int METHOD>
-__global__ __launch_bounds__(128, 2) void steps_kernel(StepsArgs a) {
-    extern __shared__ __attribute__((aligned(16))) double smem[];
-    const uint32_t l = threadIdx.x & 63u;
-    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const Lane ln{l, w, (w * 64u + l) * 16u};
-    Bufs bufs{smem, 0u};
-    for (uint32_t gate = blockIdx.x; gate < a.s.B; gate += gridDim.x) {
-        StepArgs s = a.s;
-#pragma unroll 1
-        for (uint32_t t = 0; t < a.steps; ++t) {
-            one_gate<METHOD, false>(s, gate, bufs, ln);
-            // this step's stores complete before the next step loads the same words
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            s.cvals += a.cstride;
-            s.key1 += a.key_step;
-            s.key2 += a.key_step;
-        }
-    }
-}
-
 // primitive kernels for parity tests: one polynomial per 2-wave workgroup, canonical
 // u64 words in the reference's order in and out
 __global__ __launch_bounds__(128, 2) void ntt_fwd_kernel(const uint64_t* __restrict__ in, uint64_t* __restrict__ out,

@@ -71,7 +71,6 @@ BUDGET = [
     (r"mk_step_kernel<4, 1, false, false>", 256, 2),     # MK-LWE at dg = 4 (STD128_MKNTRU_LWE_4): keeps the asm
                                                           # forward products (MKACC_BFLY_C=2 is MK-NTRU only)
     (r"widereg2::step_kernel<[01], false>", 256, 2),     # config-5 FP64 step, two waves per gate
-    (r"widereg2::steps_kernel<[01]>", 256, 2),            # its later steps of a party, fused
     (r"wide::step_kernel<[01], (true|false)>", 128, 4),    # 64-bit integer step (2^50 <= Q < 2^61)
     (r"extract_kernel|ks_mntru_kernel|ks_mklwe_kernel|mntru_head_kernel|mklwe_head_kernel", 256, 2),
 ]

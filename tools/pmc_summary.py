@@ -1,11 +1,7 @@
 #!/usr/bin/env python3
 """Average per-dispatch PMC values of one kernel across rocprofv3 counter CSVs.
 
-usage: pmc_summary.py DIR [KERNEL_SUBSTRING [PARAMSET [fused=KxN]]]
-
-fused=KxN: the kernel runs every later step of one party in one dispatch
-(widereg2::steps_kernel: k dispatches cover k*n - 1 steps of a pass), so the record
-is the counters summed over its dispatches divided by the steps they covered.
+usage: pmc_summary.py DIR [KERNEL_SUBSTRING [PARAMSET]]
 
 With PARAMSET, writes profiles/traffic_<PARAMSET>.json, the per-launch HBM
 traffic record bench.py reports as roofline.traffic: FETCH_SIZE and WRITE_SIZE
@@ -57,24 +53,15 @@ def main() -> int:
         sys.path.insert(0, ROOT)
         from mkfhe_amd import _lib
         ids = json.load(open(_lib.LIB_PATH[:-3] + ".kernel_isa.json"))
-        fused = next((a[6:] for a in sys.argv[4:] if a.startswith("fused=")), None)
-        if fused:
-            K, N = (int(v) for v in fused.split("x"))
-            f /= cnt["FETCH_SIZE"] / K * (K * N - 1)
-            w /= cnt["WRITE_SIZE"] / K * (K * N - 1)
-        else:
-            f /= cnt["FETCH_SIZE"]
-            w /= cnt["WRITE_SIZE"]
+        f /= cnt["FETCH_SIZE"]
+        w /= cnt["WRITE_SIZE"]
         rec = {"paramset": sys.argv[3], "kernel": pat, "kernel_symbol": sym, "kernel_isa": ids.get(sym),
                "build_info": _lib.load().build_info,
                "fetch_size_kb": f, "write_size_kb": w, "traffic_bytes": (2 * f + w) * 1024,
                "correction": "MI355X_MICROARCH.md HBM: FETCH_SIZE (KB) x2 for 16-B/lane coalesced reads on gfx950, "
                              "WRITE_SIZE (KB) x1; separate --pmc passes; per dispatch of the step kernel",
-               "launch": ("MKACC_STREAMS=1 during the passes: one dispatch is one step of the whole batch "
-                          "(tools/gpu_lib.sh pmc), the bench's bytes_per_launch") if not fused else
-                         (f"MKACC_STREAMS=1 during the passes; one dispatch runs every later step of one party "
-                          f"(k x n = {fused}): counters summed over the dispatches / the steps they covered, "
-                          "per step of the whole batch (the bench's bytes_per_launch)"),
+               "launch": "MKACC_STREAMS=1 during the passes: one dispatch is one step of the whole batch "
+                         "(tools/gpu_lib.sh pmc), the bench's bytes_per_launch",
                "source": d}
         out = os.path.join(ROOT, "profiles", f"traffic_{sys.argv[3]}.json")
         json.dump(rec, open(out, "w"), indent=1)
