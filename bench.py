@@ -160,6 +160,10 @@ def parse(argv=None):
                     help="test aid (tests/test_bench_ranks.py): CPU stand-in engine + gloo, to exercise the rank logic")
     ap.add_argument("--stub-shapes", choices=["toy", "real"], default="toy",
                     help="test aid: the stand-in engine's key and gate shapes (real: the parameter set's)")
+    ap.add_argument("--shared-gpu", action="store_true",
+                    help="rehearsal aid on a one-GPU box: every rank runs the real engine on device 0 and the "
+                         "collectives go over gloo (RCCL refuses two ranks on one device); a plumbing check of "
+                         "the N > 1 path on hardware, not a scaling measurement")
     return ap.parse_args(argv)
 
 
@@ -491,7 +495,8 @@ def run_rank(args, env: dict, make_engine, make_checker, torch_device: str, back
                                    f"(k={p.k}, n={p.n}, N={p.N}, dg={dg}"
                                    + (f", Q={p.Q} in 64-bit words, B_g=2^{p.baseG.bit_length() - 1})" if wide else ")"),
                        "paramset": args.paramset, "stage": stage, "batch_per_gpu": B, "global_batch": world * B,
-                       "parallelism": f"gate-sharded x{world}"},
+                       "parallelism": f"gate-sharded x{world}" + (" (rehearsal: every rank on one GPU, gloo)"
+                                                                   if getattr(args, "shared_gpu", False) else "")},
             "parity_checked": checked,
             "parity_mismatches": mismatches,
             "keys_broadcast_bytes": bcast,
@@ -564,7 +569,8 @@ def main(argv=None):
         import torch
         import mkfhe_amd as mk
 
-        torch.cuda.set_device(local)
+        dev = 0 if args.shared_gpu else local
+        torch.cuda.set_device(dev)
 
         def make_engine():
             p = mk.paramset(args.paramset)
@@ -572,9 +578,9 @@ def main(argv=None):
                 p.n = args.n_override
             if args.q_bits == 50:   # SURVEY.md s8 config 5 stress (s6: reference CPU 0.568 s / EvalAcc at k=2, n=560)
                 p.Q, p.baseG, p.digitsG, p.root = Q50, 1 << 10, 0, 0
-            return mk.MKAccumulatorEngine(p, device=local)
+            return mk.MKAccumulatorEngine(p, device=dev)
 
-        res = run_rank(args, env, make_engine, OracleChecker, f"cuda:{local}", "nccl")
+        res = run_rank(args, env, make_engine, OracleChecker, f"cuda:{dev}", "gloo" if args.shared_gpu else "nccl")
     if res is not None:
         print(json.dumps(res), flush=True)
 
