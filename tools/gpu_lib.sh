@@ -40,7 +40,7 @@ smoke() {
 _summary() {   # one line of a bench JSON
     python3 - "$1" <<'EOF'
 import json, sys
-d = json.load(open(sys.argv[1]))
+d = json.loads([ln for ln in open(sys.argv[1]) if ln.startswith("{")][-1])
 r, v = d["roofline"], d.get("roofline_valu", {})
 print(sys.argv[1].split("/")[-1], f"{d['value']:.1f} {d['unit']}", f"{d['ms_per_step']:.2f} ms/step",
       f"{r['per_launch_us']:.2f} us/launch", f"valu {v.get('frac', 0):.3f}", f"hbm {r['frac']:.3f}",

@@ -6,7 +6,8 @@ every half-wave hit 32 distinct bank pairs in every layout), the per-lane twiddl
 indexing of every pass, and the monomial exponent split -- the forward and
 inverse transform pair run on (wave, lane, register) arrays and must equal the
 oracle's NTT (reference order) -- for the FP64 kernel's EVAL layout and the 27-bit
-kernel's (mk_step3_kernel) -- and the two-buffer LDS schedule with a barrier only in
+kernel's two-wave layout (that kernel, mk_step3_kernel, was retired in round 5; the
+layout stays in mkacc_layout2.hpp and is still checked) -- and the two-buffer LDS schedule with a barrier only in
 the cross-wave transposes is checked race-free over a sequence of gate-steps.
 Test infrastructure: imports oracle/ only.
 usage: python3 tools/widereg2_model.py      (about a minute)"""
@@ -21,7 +22,7 @@ def A2(p): return (bit(p,6), p&63, p>>7)
 def B2(p): return (bit(p,10), (p&7)|(bit(p,7)<<3)|(bit(p,8)<<4)|(bit(p,9)<<5), (p>>3)&15)
 def C2(p): return (bit(p,10), bit(p,5)|(bit(p,6)<<1)|(bit(p,9)<<2)|(bit(p,7)<<3)|(bit(p,4)<<4)|(bit(p,8)<<5), p&15)
 def D2(p): return (bit(p,10), (p&15)|(bit(p,8)<<4)|(bit(p,9)<<5), (p>>4)&15)
-# the 27-bit kernel's EVAL layout (mk_step3_kernel): the one-wave layout C split at slot bit 4
+# the 27-bit two-wave EVAL layout (of the retired mk_step3_kernel): the one-wave layout C split at slot bit 4
 def C4(p): return (bit(p,4), p>>5, p&15)
 L={'A':A2,'B':B2,'C':C2,'D':D2,'E':C4}
 inv={}
