@@ -1,25 +1,22 @@
 // mkacc_layout2.hpp -- register / lane / LDS layouts of the TWO-waves-per-gate
-// transforms (mk_step3_kernel, 27-bit words; widereg2::step_kernel, FP64).
+// transforms (widereg2::step_kernel, FP64; round 4's 27-bit two-wave kernel and
+// its EVAL layout LC4 were retired in round 5 -- git history, 7a372b6).
 // Included inside mkacc_kernels.hpp's anonymous namespace.
 //
 // A polynomial of N = 2048 positions p (11 bits) is split over the two waves of a
 // 128-thread workgroup, 16 elements per lane.  Position p sits at (wave w, lane l,
-// register r) in one of five layouts (l written l5..l0):
-//   LA  r = p10..p7, w = p6,  l = p5..p0                  coefficients (both kernels)
+// register r) in one of four layouts (l written l5..l0):
+//   LA  r = p10..p7, w = p6,  l = p5..p0                  coefficients
 //   LB  r = p6..p3,  w = p10, l = (p9, p8, p7, p2, p1, p0)
-//   LC  r = p3..p0,  w = p10, l = (p8, p4, p7, p9, p6, p5) EVAL slots (FP64 kernel, "C16")
-//   LC4 r = p3..p0,  w = p4,  l = p10..p5                 EVAL slots (27-bit kernel): slot
-//                                                         (l << 5) | (w << 4) | r is the
-//                                                         one-wave layout C's, so the C4
-//                                                         key / accumulator words serve both
+//   LC  r = p3..p0,  w = p10, l = (p8, p4, p7, p9, p6, p5) EVAL slots ("C16")
 //   LD  r = p7..p4,  w = p10, l = (p9, p8, p3, p2, p1, p0)
-// Forward: LA stages 0-3 (wave-uniform twiddles) -> LB stages 4-6 -> LC/LC4 stages
-// 7-10; inverse: LC/LC4 bits 0-3 (wave-uniform) -> LD bits 4-7 -> LA bits 8-10.
+// Forward: LA stages 0-3 (wave-uniform twiddles) -> LB stages 4-6 -> LC stages
+// 7-10; inverse: LC bits 0-3 (wave-uniform) -> LD bits 4-7 -> LA bits 8-10.
 // The LDS element of position p is sum_k W_k p_k with
 // W = 1, 2, 4, 8, 16, 33, 66, 136, 272, 548, 1088 -- injective, additive in every
 // bit (a per-lane base plus a compile-time register offset, so one address VGPR and
 // immediate offsets), and in every layout the 32 lanes of each half-wave hit 32
-// distinct values mod 32 and (all but LC4) the 16 lanes of each quarter 16 distinct
+// distinct values mod 32 and the 16 lanes of each quarter 16 distinct
 // values mod 16: conflict-free ds_read/ds_write_b32, ds_read_b64 and the 16-lane
 // groups of ds_write_b64 / ds_read2_b64 (MI355X_MICROARCH.md s LDS; the first LC
 // map, l = (p8, p9, p7, p6, p5, p4), put p4 -- weight 16 -- in a 16-lane group:
@@ -31,7 +28,7 @@ namespace lay2 {
 
 constexpr int kR = 16;                 // elements per lane and polynomial
 constexpr int kBufE = 2175;            // LDS elements of one transpose buffer (max index 2174)
-enum { LA = 0, LB = 1, LC = 2, LD = 3, LC4 = 4 };
+enum { LA = 0, LB = 1, LC = 2, LD = 3 };
 constexpr int kW[11] = {1, 2, 4, 8, 16, 33, 66, 136, 272, 548, 1088};
 
 // register offset of register r in layout L (compile time)
@@ -41,7 +38,7 @@ __host__ __device__ constexpr int roff(int r) {
     return L == LA   ? b0 * kW[7] + b1 * kW[8] + b2 * kW[9] + b3 * kW[10]
            : L == LB ? b0 * kW[3] + b1 * kW[4] + b2 * kW[5] + b3 * kW[6]
            : L == LD ? b0 * kW[4] + b1 * kW[5] + b2 * kW[6] + b3 * kW[7]
-                     : r;   // LC, LC4: registers are p3..p0
+                     : r;   // LC: registers are p3..p0
 }
 // lane / wave base of layout L
 template <int L>
@@ -51,7 +48,6 @@ __host__ __device__ __forceinline__ uint32_t lbase(uint32_t l, uint32_t w) {
     if (L == LA) return (l & 31u) + l5 * kW[5] + w * kW[6];
     if (L == LB) return (l & 7u) + l3 * kW[7] + l4 * kW[8] + l5 * kW[9] + w * kW[10];
     if (L == LC) return l0 * kW[5] + l1 * kW[6] + l2 * kW[9] + l3 * kW[7] + l4 * kW[4] + l5 * kW[8] + w * kW[10];
-    if (L == LC4) return w * kW[4] + l0 * kW[5] + l1 * kW[6] + l2 * kW[7] + l3 * kW[8] + l4 * kW[9] + l5 * kW[10];
     return (l & 15u) + l4 * kW[8] + l5 * kW[9] + w * kW[10];
 }
 // positions of (w, l, r)
@@ -63,7 +59,6 @@ __host__ __device__ __forceinline__ uint32_t pos_c(uint32_t w, uint32_t l, uint3
     return r | (((l >> 4) & 1u) << 4) | ((l & 1u) << 5) | (((l >> 1) & 1u) << 6) | (((l >> 3) & 1u) << 7) |
            (((l >> 5) & 1u) << 8) | (((l >> 2) & 1u) << 9) | (w << 10);
 }
-__host__ __device__ __forceinline__ uint32_t pos_c4(uint32_t w, uint32_t l, uint32_t r) { return r | (w << 4) | (l << 5); }
 __host__ __device__ __forceinline__ uint32_t pos_d(uint32_t w, uint32_t l, uint32_t r) {
     return (r << 4) | (l & 15u) | (((l >> 4) & 1u) << 8) | (((l >> 5) & 1u) << 9) | (w << 10);
 }
@@ -137,7 +132,7 @@ __device__ __forceinline__ void transpose(T (&x)[kR], T* buf, uint32_t l, uint32
 // next transform's LA -> LB, which moves to the other buffer.
 template <int SRC, int DST, typename T>
 __device__ __forceinline__ void transpose_local(T (&x)[kR], T* buf, uint32_t l, uint32_t w) {
-    static_assert(SRC != LA && DST != LA && SRC != LC4 && DST != LC4, "wave-local transposes keep w = p10");
+    static_assert(SRC != LA && DST != LA, "wave-local transposes keep w = p10");
     T* ws = buf + lbase<SRC>(l, w);
 #pragma unroll
     for (int r = 0; r < kR; ++r) ws[roff<SRC>(r)] = x[r];

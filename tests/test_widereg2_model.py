@@ -1,6 +1,5 @@
 """CPU check of the two-waves-per-gate kernels' index maps
-(mkfhe_amd/csrc/mkacc_layout2.hpp, used by widereg2::step_kernel; the
-27-bit two-wave layout of the retired mk_step3_kernel is still checked): tools/widereg2_model.py runs the layouts, LDS word map (bank
+(mkfhe_amd/csrc/mkacc_layout2.hpp, used by widereg2::step_kernel): tools/widereg2_model.py runs the layouts, LDS word map (bank
 groups of every LDS instruction the transposes use), per-lane twiddle indexing
 and monomial split in exact integers against the oracle's NTT; the header's
 constants must be the model's."""

@@ -5,9 +5,7 @@ word map (injective, additive in every bit, and conflict-free: the 32 lanes of
 every half-wave hit 32 distinct bank pairs in every layout), the per-lane twiddle
 indexing of every pass, and the monomial exponent split -- the forward and
 inverse transform pair run on (wave, lane, register) arrays and must equal the
-oracle's NTT (reference order) -- for the FP64 kernel's EVAL layout and the 27-bit
-kernel's two-wave layout (that kernel, mk_step3_kernel, was retired in round 5; the
-layout stays in mkacc_layout2.hpp and is still checked) -- and the two-buffer LDS schedule with a barrier only in
+oracle's NTT (reference order) -- and the two-buffer LDS schedule with a barrier only in
 the cross-wave transposes is checked race-free over a sequence of gate-steps.
 Test infrastructure: imports oracle/ only.
 usage: python3 tools/widereg2_model.py      (about a minute)"""
@@ -22,9 +20,7 @@ def A2(p): return (bit(p,6), p&63, p>>7)
 def B2(p): return (bit(p,10), (p&7)|(bit(p,7)<<3)|(bit(p,8)<<4)|(bit(p,9)<<5), (p>>3)&15)
 def C2(p): return (bit(p,10), bit(p,5)|(bit(p,6)<<1)|(bit(p,9)<<2)|(bit(p,7)<<3)|(bit(p,4)<<4)|(bit(p,8)<<5), p&15)
 def D2(p): return (bit(p,10), (p&15)|(bit(p,8)<<4)|(bit(p,9)<<5), (p>>4)&15)
-# the 27-bit two-wave EVAL layout (of the retired mk_step3_kernel): the one-wave layout C split at slot bit 4
-def C4(p): return (bit(p,4), p>>5, p&15)
-L={'A':A2,'B':B2,'C':C2,'D':D2,'E':C4}
+L={'A':A2,'B':B2,'C':C2,'D':D2}
 inv={}
 for n,f in L.items():
     m={}
@@ -41,8 +37,6 @@ for n in L:
             for h in range(2):
                 banks=[pad(inv[n][(w,l,r)])%32 for l in range(32*h,32*h+32)]
                 assert len(set(banks))==32, (n,w,r,h)
-            if n == 'E':   # 27-bit words only
-                continue
             for q in range(4):
                 banks=[pad(inv[n][(w,l,r)])%16 for l in range(16*q,16*q+16)]
                 assert len(set(banks))==16, (n,w,r,q)
@@ -163,11 +157,9 @@ a=[int(v) for v in O.fill_uniform(N,Q,5)]
 e=fwd(a)
 ref=[int(v) for v in O.ntt_forward(np.array(a,dtype=np.uint64),Q,PSI)]
 assert e == ref, "forward transform"
-assert fwd(a, 'E') == ref, "forward transform (27-bit EVAL layout)"
 print("forward transform ok")
 b=inv_(ref)
 assert b == a, "inverse transform"
-assert inv_(ref, 'E') == a, "inverse transform (27-bit EVAL layout)"
 print("inverse transform ok")
 # mono: slot p (C2) exponent e*(2*brv11(p)+1) = e*(2*Lw+1) + ((e*brv4(r))<<8)
 for p in range(N):
