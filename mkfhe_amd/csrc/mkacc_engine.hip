@@ -113,6 +113,14 @@ const void* step_fn(int dg, int method, bool first, bool dscr, int ver) {
         default: return nullptr;
     }
 }
+const void* latd_fn(int dg, int method, bool first) {
+    switch (dg) {
+        case 2: return mkacc_tu::latd_dg2(method, first);
+        case 3: return mkacc_tu::latd_dg3(method, first);
+        case 4: return mkacc_tu::latd_dg4(method, first);
+        default: return nullptr;
+    }
+}
 const void* lat_fn(int dg, int method, bool first) {
     switch (dg) {
         case 2: return mkacc_tu::lat_dg2(method, first);
@@ -280,6 +288,15 @@ bool use_dscr(const mkacc_ctx* c) {
     return c->p.k >= kDscrMinK;
 }
 
+// Two-party batches of at most one gate per CU split each party's digits over two
+// waves (mk_latd_kernel: four waves of up to 256 VGPRs, one workgroup per CU);
+// MKACC_LATD=0 keeps one wave per party (mk_lat_kernel).
+bool use_latd(const mkacc_ctx* c, size_t B) {
+    if (c->p.k != 2 || B > (size_t)c->cus) return false;
+    const char* e = std::getenv("MKACC_LATD");
+    return !(e && e[0] == '0');
+}
+
 // Small batches take mk_lat_kernel (one wave per party) while the whole batch
 // is resident in one round: its workgroups are LDS-bound (tables + k
 // scratches: 2 per CU at k = 2..4, 1 at k = 8), and a second round costs more
@@ -353,9 +370,11 @@ struct StepChain {
         a.dscr = c->d_dscr ? c->d_dscr + g0 * step_scratch_words(c) : nullptr;
         // a null kernel must never reach hipLaunchKernelGGL (mkacc_create checks the set)
         if (lat) {
-            const void* fn = lat_fn((int)c->dg, c->method_class, first);
+            const bool split = use_latd(c, Bh);
+            const void* fn = split ? latd_fn((int)c->dg, c->method_class, first) : lat_fn((int)c->dg, c->method_class, first);
             if (!fn) return false;
-            launch_ptr(fn, dim3((unsigned)Bh), dim3(64 * k), lat_lds_bytes(k), st, a);
+            const uint32_t waves = split ? kLatdWaves : k;
+            launch_ptr(fn, dim3((unsigned)Bh), dim3(64 * waves), lat_lds_bytes(waves), st, a);
         } else {
             const void* fn = step_fn((int)c->dg, c->method_class, first, !first && use_dscr(c), c->step_ver);
             if (!fn) return false;
@@ -1363,7 +1382,7 @@ const char* mkacc_step_kernel_name(const mkacc_ctx* c, size_t B) {
     if (!c) return "";
     if (c->wide)
         return c->wfp ? "widereg2::step_kernel" : "wide::step_kernel";
-    if (use_lat(c, B)) return "mk_lat_kernel";
+    if (use_lat(c, B)) return use_latd(c, B) ? "mk_latd_kernel" : "mk_lat_kernel";
     return c->step_ver == 2 ? "mk_step2_kernel" : "mk_step_kernel";
 }
 int mkacc_is_wide(const mkacc_ctx* c) { return c && c->wide ? (c->wfp ? 2 : 1) : 0; }

@@ -734,6 +734,237 @@ __device__ __forceinline__ void f_part(const StepCtx& s, uint32_t index, uint64_
     }
 }
 
+// ---- two-party small batches with the digits split over waves (mk_latd_kernel) ----
+// mk_lat_kernel's step has 2 (dg + 1) transforms on its critical path: a party
+// pass (iNTT + dg digit NTTs) on every party's wave at once, then the f-part on
+// one wave.  For k = 2 this kernel runs each party on two waves and the f-part on
+// dg waves (one workgroup of four waves per gate, one per SIMD): every wave of a
+// party recomputes its iNTT (no exchange, off the critical path) and transforms
+// and multiplies only its share of the digits; the lazy sums are reduced once per
+// wave and added through LDS.  Critical path: iNTT + ceil(dg / 2) digit NTTs, then
+// iNTT + one digit NTT.  Sums exact mod Q, so bit-exact like the other kernels.
+constexpr uint32_t kLatdWaves = 4;
+// digits [d0, d1) of party u: uj (its partial party sum, from acc_u * 2^32 at digit 0
+// when the bound allows) and sv (its share of sumV) as lazy 64-bit sums
+template <int DG, int METHOD, bool FIRST>
+__device__ __forceinline__ void party_digits(const StepCtx& s, uint32_t u, uint32_t d0, uint32_t d1,
+                                             uint64_t (&sv)[kRegs], uint64_t (&uj)[kRegs]) {
+    const uint32_t Q = s.m.Q, polyB = kN * 4u;
+    uint32_t x[kRegs];
+#pragma unroll
+    for (int gq = 0; gq < 8; ++gq) {
+        const u32x4 t = aload4(s.rin, s.vo, u * polyB + gq * 1024u);
+        x[4 * gq] = t.x; x[4 * gq + 1] = t.y; x[4 * gq + 2] = t.z; x[4 * gq + 3] = t.w;
+    }
+    if (!FIRST) {
+        // acctemp = acc * (X^c - 1)                     (xzw.cpp:336-338)
+        uint2 mw[kRegs];
+#pragma unroll
+        for (int r = 0; r < kRegs; ++r) mw[r] = s.mp.at(s.tb.psi, r);
+        sched_fence();
+#pragma unroll
+        for (int r = 0; r < kRegs; ++r) x[r] = mul_shoup_lazy(x[r], mw[r], Q);
+    }
+    ntt_inv(x, s.lds, s.tw_inv, s.tb.twi, s.l, Q);
+    PackedDigits<DG> pd;
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) {
+        x[r] = pd.put(r, sdd_offset(x[r], s.sd), s.sd);
+        if ((r & 7) == 7) sched_fence();
+    }
+    const StepRes sr = s.res();
+#pragma unroll 1
+    for (uint32_t i = d0; i < d1; ++i) {
+        if (i > 0) {
+#pragma unroll
+            for (int r = 0; r < kRegs; ++r) x[r] = pd.get(r, (int)i + 1, s.sd);
+        }
+        ntt_fwd<fwd_c<METHOD>>(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, s.l, Q, s.m.m1);
+        digit_range<DG>(x, Q);
+        vcc_fence();   // the digit-0 branch follows the last butterflies
+        if (i == 0) {
+            const DigitMac<DG, METHOD, FIRST, true> mac(sr, 0, u);
+            KeyGroup kg[mac.kBuf];
+#pragma unroll
+            for (int j = 0; j < mac.kPrefetch; ++j) mac.issue(kg[j], j);
+            mac.run(x, uj, sv, kg);
+        } else {
+            const DigitMac<DG, METHOD, FIRST, false> mac(sr, (int)i, u);
+            KeyGroup kg[mac.kBuf];
+#pragma unroll
+            for (int j = 0; j < mac.kPrefetch; ++j) mac.issue(kg[j], j);
+            mac.run(x, uj, sv, kg);
+        }
+        vcc_fence();   // the loop branch follows the MAC's reductions
+    }
+}
+// f-part digit f of party `index` (mk-acc-xzw.cpp:272-289): x = sumV in [0, 2Q);
+// w enters with the index party's sum (digit 0's wave) or 0 and leaves as its
+// share of acc'[index] in [0, 2Q)
+template <int DG, int METHOD, bool FIRST>
+__device__ __forceinline__ void f_digit(const StepCtx& s, uint32_t f, uint64_t (&w)[kRegs], uint32_t (&x)[kRegs]) {
+    const uint32_t Q = s.m.Q;
+    const StepRes sr = s.res();
+    ntt_inv(x, s.lds, s.tw_inv, s.tb.twi, s.l, Q);
+    PackedDigits<DG> pd;
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) {
+        x[r] = pd.put(r, sdd_offset(x[r], s.sd), s.sd);
+        if ((r & 7) == 7) sched_fence();
+    }
+    if (f > 0) {
+#pragma unroll
+        for (int r = 0; r < kRegs; ++r) x[r] = pd.get(r, (int)f + 1, s.sd);
+    }
+    constexpr bool kSplit = METHOD == XZW && !FIRST;
+    uint64_t w2[kSplit ? kRegs : 1];
+    ntt_fwd<fwd_c<METHOD>>(x, s.lds, s.tw_fwd, s.tb.twf, s.tb.twfc, s.l, Q, s.m.m1);
+    digit_range<DG>(x, Q);
+    if constexpr (kSplit) {
+#pragma unroll
+        for (int r = 0; r < kRegs; ++r) w2[r] = 0;
+        const SplitMac<DG> mac(sr, (int)f);
+        KeyGroup kg[mac.kBuf];
+#pragma unroll
+        for (int j = 0; j < mac.kPrefetch; ++j) mac.issue(kg[j], j);
+        mac.run(x, w, w2, kg);
+    } else {
+        mac_index<DG, METHOD, FIRST>(x, (int)f, w, s.rk1, s.rk2, s.rks, s.tb.psi, s.mp, s.mn, s.vo, Q);
+    }
+    uint2 mw[kSplit ? kRegs : 1];
+    if constexpr (kSplit) {
+#pragma unroll
+        for (int r = 0; r < kRegs; ++r) mw[r] = s.mn.at(s.tb.psi, r);
+    }
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) {
+        uint32_t v = redc(w[r], Q, s.m.qinv);                                       // [0, 2Q)
+        if constexpr (kSplit) {
+            v += mul_shoup_lazy(redc(w2[r], Q, s.m.qinv), mw[r], Q);                 // [0, 4Q)
+            v = min(v, v - 2u * Q);
+        }
+        x[r] = v;
+    }
+}
+
+template <int DG, int METHOD, bool FIRST>
+__global__ __launch_bounds__(64 * kLatdWaves, 1) void mk_latd_kernel(StepArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    load_image(smem, a.img);
+    using Bd = Bounds<DG, METHOD, FIRST>;
+    const uint32_t l = threadIdx.x & 63u;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // this wave
+    const uint32_t gate = blockIdx.x;
+    const uint32_t c = __builtin_amdgcn_readfirstlane(a.cvals[gate]);
+    const uint32_t cneg = (2u * kN - c) & (2u * kN - 1u);
+    const uint32_t k = 2u, index = a.index;
+    const uint32_t polyB = kN * 4u;
+    uint32_t* const scratch = smem + kLdsTabWords + wv * kLdsWords;
+    const StepCtx s{tables(smem, a.img),
+                    scratch,
+                    a.tw_fwd,
+                    a.tw_inv,
+                    a.m,
+                    a.sd,
+                    make_mono(c, l),
+                    make_mono(FIRST || METHOD != XZW ? cneg : (cneg + kN) & (2u * kN - 1u), l),
+                    l,
+                    l * 16u,
+                    make_rsrc(a.acc_in + (size_t)gate * k * kN, k * polyB),
+                    make_rsrc(a.acc_out + (size_t)gate * k * kN, k * polyB),
+                    make_rsrc(a.key1, DG * 2 * polyB),
+                    make_rsrc(a.key2, DG * 2 * polyB),
+                    make_rsrc(a.keys, DG * 2 * polyB),
+                    make_rsrc(a.pkey, k * DG * polyB),
+                    make_rsrc(a.acc_in, 0u)};
+    const uint32_t Q = s.m.Q;
+    // party p = wv / 2 takes digits [0, dh) (half 0) or [dh, DG) (half 1)
+    const uint32_t p = wv >> 1, half = wv & 1u;
+    constexpr uint32_t kDh = (DG + 1) / 2;
+    uint64_t sv[kRegs], uj[kRegs];
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) sv[r] = uj[r] = 0;
+    party_digits<DG, METHOD, FIRST>(s, p, half ? kDh : 0u, half ? (uint32_t)DG : kDh, sv, uj);
+    // (1) party sums: acc'_p = the two halves (+ acc_p when it was not in the sum)
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) scratch[r * 64 + l] = redc(uj[r], Q, s.m.qinv);
+    vcc_fence();   // the branches below follow the reductions' multiply-adds
+    __syncthreads();
+    uint64_t w[kRegs];
+    // the f-part: wave 2 index takes digit 0 (it holds the index party's sum), the
+    // others digits 1, 2, ... in wave order after it
+    const uint32_t f = (wv + kLatdWaves - 2u * index) % kLatdWaves;
+    if (half == 0) {
+        const uint32_t* o = smem + kLdsTabWords + (wv + 1u) * kLdsWords;
+        uint32_t t4[kRegs];
+#pragma unroll
+        for (int r = 0; r < kRegs; ++r) t4[r] = scratch[r * 64 + l] + o[r * 64 + l];   // < 4Q
+        if constexpr (!Bd::kAccInSum && !FIRST) {
+#pragma unroll
+            for (int gq = 0; gq < 8; ++gq) {
+                const u32x4 t = aload4(s.rin, s.vo, p * polyB + gq * 1024u);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) t4[4 * gq + e] += t[e];                      // < 6Q
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < kRegs; ++r) {
+            uint32_t v = min(t4[r], t4[r] - 4u * Q);
+            t4[r] = min(v, v - 2u * Q);                                                 // [0, 2Q)
+        }
+        if (p != index) {
+#pragma unroll
+            for (int gq = 0; gq < 8; ++gq)
+                bstore4(u32x4{t4[4 * gq], t4[4 * gq + 1], t4[4 * gq + 2], t4[4 * gq + 3]}, s.rout, s.vo,
+                        p * polyB + gq * 1024u);
+        } else {
+#pragma unroll
+            for (int r = 0; r < kRegs; ++r) w[r] = mad64(t4[r], s.m.r32, 0);           // < 2 Q^2
+        }
+    }
+    if (f != 0) {
+#pragma unroll
+        for (int r = 0; r < kRegs; ++r) w[r] = 0;
+    }
+    __syncthreads();
+    // (2) sumV: every wave's share, [0, 2Q) each
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) scratch[r * 64 + l] = redc(sv[r], Q, s.m.qinv);
+    vcc_fence();
+    __syncthreads();
+    uint32_t x[kRegs];
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) {
+        uint32_t v = 0;
+        for (uint32_t q = 0; q < kLatdWaves; ++q) v += smem[kLdsTabWords + q * kLdsWords + r * 64 + l];   // < 8Q
+        v = min(v, v - 4u * Q);
+        x[r] = min(v, v - 2u * Q);                                                      // [0, 2Q)
+    }
+    __syncthreads();   // every wave has read the shares before the transforms reuse the scratch
+    // (3) f-part digit f on waves f < DG, then acc'[index] = the sum of their shares
+    if (f < DG) f_digit<DG, METHOD, FIRST>(s, f, w, x);
+    vcc_fence();
+    if (f < DG) {
+#pragma unroll
+        for (int r = 0; r < kRegs; ++r) scratch[r * 64 + l] = x[r];
+    }
+    __syncthreads();
+    if (f != 0) return;
+#pragma unroll
+    for (int r = 0; r < kRegs; ++r) {
+        uint32_t v = 0;
+        for (uint32_t q = 0; q < kLatdWaves; ++q) {
+            const uint32_t fq = (q + kLatdWaves - 2u * index) % kLatdWaves;
+            if (fq < DG) v += smem[kLdsTabWords + q * kLdsWords + r * 64 + l];               // < 2 DG Q <= 8Q
+        }
+        v = min(v, v - 4u * Q);
+        x[r] = min(v, v - 2u * Q);
+    }
+#pragma unroll
+    for (int gq = 0; gq < 8; ++gq)
+        bstore4(u32x4{x[4 * gq], x[4 * gq + 1], x[4 * gq + 2], x[4 * gq + 3]}, s.rout, s.vo, index * polyB + gq * 1024u);
+}
+
 // ---- batch prologue / epilogue kernels --------------------------------------
 
 // c = floor(ct * 2N / q) (mk-acc-xzw.cpp:110,125) or c = ct (mk-acc-xzw_B.cpp:119,124),
@@ -882,6 +1113,11 @@ StepFn pick_lat(int method, bool first) {
     if (method == XZW) return first ? mk_lat_kernel<DG, XZW, true> : mk_lat_kernel<DG, XZW, false>;
     return first ? mk_lat_kernel<DG, XZW_B, true> : mk_lat_kernel<DG, XZW_B, false>;
 }
+template <int DG>
+StepFn pick_latd(int method, bool first) {
+    if (method == XZW) return first ? mk_latd_kernel<DG, XZW, true> : mk_latd_kernel<DG, XZW, false>;
+    return first ? mk_latd_kernel<DG, XZW_B, true> : mk_latd_kernel<DG, XZW_B, false>;
+}
 
 }  // namespace
 
@@ -900,6 +1136,9 @@ MKACC_TU_API KernelPtr step2f_dg3(int method);
 MKACC_TU_API KernelPtr lat_dg2(int method, bool first);
 MKACC_TU_API KernelPtr lat_dg3(int method, bool first);
 MKACC_TU_API KernelPtr lat_dg4(int method, bool first);
+MKACC_TU_API KernelPtr latd_dg2(int method, bool first);   // mk_latd_kernel (k = 2, digits split over waves)
+MKACC_TU_API KernelPtr latd_dg3(int method, bool first);
+MKACC_TU_API KernelPtr latd_dg4(int method, bool first);
 MKACC_TU_API KernelPtr wide_step(int method, bool first);     // mkacc_wide.hpp (integer 64-bit words)
 MKACC_TU_API KernelPtr widereg2_step(int method, bool first);  // mkacc_widereg2.hpp (FP64, Q < 2^50)
 }  // namespace mkacc_tu

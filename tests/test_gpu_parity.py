@@ -169,6 +169,30 @@ def test_evalacc_small_batch_kernel(mk, oracle, case, lat, monkeypatch):
     assert np.array_equal(got, exp.astype(np.uint32))
 
 
+@pytest.mark.parametrize("meth", ["XZW", "XZW_B"])
+@pytest.mark.parametrize("logB", [9, 7, 6])   # dg = 2, 3, 4
+def test_evalacc_two_party_split_digit_kernel(mk, oracle, meth, logB, monkeypatch):
+    """Two parties, batches of at most one gate per CU: mk_latd_kernel (each party's
+    digits over two waves, the f-part's over dg waves) equals the oracle and the
+    one-wave-per-party kernel word for word, first step and later steps."""
+    monkeypatch.setenv("MKACC_LAT", "1")
+    om = oracle.XZW if meth == "XZW" else oracle.XZW_B
+    em = mk.MKNTRU if meth == "XZW" else mk.MKNTRU_LWE
+    q = 45181 if meth == "XZW" else 32749
+    B = 5
+    orc, evk, pkey, ct, acc = make_case(oracle, om, 2, 4, q, 1 << logB, B, seed=71 + logB)
+    exp = orc.evalacc_batch(evk, pkey, ct, acc, 8).astype(np.uint32)
+    outs = {}
+    for split, name in (("1", "mk_latd_kernel"), ("0", "mk_lat_kernel")):
+        monkeypatch.setenv("MKACC_LATD", split)
+        eng = mk.MKAccumulatorEngine(mk.make_params(em, 2, 4, 2048, Q_MK, q, 1 << logB))
+        assert eng.step_kernel_name(B) == name
+        eng.upload_keys(evk.astype(np.uint32), pkey.astype(np.uint32))
+        outs[split] = eng.eval_batch(ct.astype(np.uint32), acc.astype(np.uint32))
+        assert np.array_equal(outs[split], exp), name
+    assert np.array_equal(outs["1"], outs["0"])
+
+
 def test_interface_mirror_evalacc(mk, oracle):
     """UniEncAccumulatorXZW.EvalAcc updates acc in place like the reference."""
     orc, evk, pkey, ct, acc = make_case(oracle, oracle.XZW, 2, 3, 45181, 1 << 9, 1, seed=9)
