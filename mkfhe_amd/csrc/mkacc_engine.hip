@@ -121,6 +121,14 @@ const void* latd_fn(int dg, int method, bool first) {
         default: return nullptr;
     }
 }
+const void* latdrun_fn(int dg, int method) {
+    switch (dg) {
+        case 2: return mkacc_tu::latdrun_dg2(method);
+        case 3: return mkacc_tu::latdrun_dg3(method);
+        case 4: return mkacc_tu::latdrun_dg4(method);
+        default: return nullptr;
+    }
+}
 const void* lat_fn(int dg, int method, bool first) {
     switch (dg) {
         case 2: return mkacc_tu::lat_dg2(method, first);
@@ -135,6 +143,11 @@ const void* lat_fn(int dg, int method, bool first) {
 template <class A>
 void launch_ptr(const void* fn, dim3 grid, dim3 block, size_t lds, hipStream_t s, A a) {
     void* args[] = {&a};
+    (void)hipLaunchKernel(fn, grid, block, args, lds, s);
+}
+template <class A, class R>
+void launch_ptr2(const void* fn, dim3 grid, dim3 block, size_t lds, hipStream_t s, A a, R r) {
+    void* args[] = {&a, &r};
     (void)hipLaunchKernel(fn, grid, block, args, lds, s);
 }
 
@@ -347,10 +360,8 @@ struct StepChain {
     StepChain(mkacc_ctx* c_, size_t B_, size_t g0_, size_t Bh_, hipStream_t st_)
         : c(c_), B(B_), g0(g0_), Bh(Bh_), ao(g0_ * c_->p.k * kN), st(st_), cur(c_->d_acc0 + ao), nxt(c_->d_acc1 + ao),
           lat(use_lat(c_, Bh_)) {}
-    // one accumulator step (u, i); false if the build has no kernel for it
-    bool step(uint32_t u, uint32_t i, size_t lds) {
+    StepArgs args(uint32_t u, uint32_t i) const {
         const uint32_t k = c->p.k, n = c->p.n;
-        const bool first = (u == 0 && i == 0);
         StepArgs a;
         a.acc_in = cur;
         a.acc_out = nxt;
@@ -368,6 +379,13 @@ struct StepChain {
         a.m = c->mod;
         a.sd = c->sd;
         a.dscr = c->d_dscr ? c->d_dscr + g0 * step_scratch_words(c) : nullptr;
+        return a;
+    }
+    // one accumulator step (u, i); false if the build has no kernel for it
+    bool step(uint32_t u, uint32_t i, size_t lds) {
+        const uint32_t k = c->p.k;
+        const bool first = (u == 0 && i == 0);
+        const StepArgs a = args(u, i);
         // a null kernel must never reach hipLaunchKernelGGL (mkacc_create checks the set)
         if (lat) {
             const bool split = use_latd(c, Bh);
@@ -388,8 +406,36 @@ struct StepChain {
         std::swap(cur, nxt);
         return true;
     }
+    // steps [t0, t1) (t = u n + i, t0 >= 1) in one mk_latd_run_kernel launch
+    // (use_latd batches); false if the build has no kernel for it
+    bool run(uint32_t t0, uint32_t t1) {
+        const uint32_t n = c->p.n;
+        const void* fn = latdrun_fn((int)c->dg, c->method_class);
+        if (!fn || t0 == 0 || t0 >= t1) return false;
+        const StepArgs a = args(t0 / n, t0 % n);
+        LatdRun r;
+        r.keys = c->d_keys;
+        r.cvals = c->d_cvals + g0;
+        r.acc0 = cur;
+        r.acc1 = nxt;
+        r.kbw = key_block_words(c);
+        r.cstride = (uint32_t)B;
+        r.n = n;
+        r.t0 = t0;
+        r.t1 = t1;
+        r.key2off = c->nk == 2 ? (uint32_t)(c->dg * 2 * kN) : 0u;
+        launch_ptr2(fn, dim3((unsigned)Bh), dim3(64 * kLatdWaves), lat_lds_bytes(kLatdWaves), st, a, r);
+        if ((t1 - t0) & 1u) std::swap(cur, nxt);
+        return true;
+    }
     uint32_t* result() const { return cur - ao; }   // the full-batch buffer holding the result
 };
+
+// Batches of the split-digit kernel run the steps after the first in one launch
+// (mk_latd_run_kernel); MKACC_LATD_RUN=0 (build flag, A/B) keeps one launch per step.
+#ifndef MKACC_LATD_RUN
+#define MKACC_LATD_RUN 1
+#endif
 
 // Joins the slice streams a batch forked from the context stream back into it on
 // every exit path: later work on c->stream -- a key upload's
@@ -430,6 +476,10 @@ uint32_t* launch_steps(mkacc_ctx* c, size_t B) {
     const size_t ns = std::min<size_t>((size_t)c->nstreams, B / unit);
     if (ns < 2) {
         StepChain ch(c, B, 0, B, c->stream);
+        if (MKACC_LATD_RUN && ch.lat && use_latd(c, B) && (size_t)k * n > 1) {
+            if (!ch.step(0, 0, lds) || !ch.run(1, k * n)) return nullptr;
+            return ch.result();
+        }
         for (uint32_t u = 0; u < k; ++u)
             for (uint32_t i = 0; i < n; ++i)
                 if (!ch.step(u, i, lds)) return nullptr;

@@ -848,9 +848,7 @@ __device__ __forceinline__ void f_digit(const StepCtx& s, uint32_t f, uint64_t (
 }
 
 template <int DG, int METHOD, bool FIRST>
-__global__ __launch_bounds__(64 * kLatdWaves, 1) void mk_latd_kernel(StepArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    load_image(smem, a.img);
+__device__ __forceinline__ void latd_step(const StepArgs& a, uint32_t* smem) {
     using Bd = Bounds<DG, METHOD, FIRST>;
     const uint32_t l = threadIdx.x & 63u;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // this wave
@@ -963,6 +961,48 @@ __global__ __launch_bounds__(64 * kLatdWaves, 1) void mk_latd_kernel(StepArgs a)
 #pragma unroll
     for (int gq = 0; gq < 8; ++gq)
         bstore4(u32x4{x[4 * gq], x[4 * gq + 1], x[4 * gq + 2], x[4 * gq + 3]}, s.rout, s.vo, index * polyB + gq * 1024u);
+}
+
+template <int DG, int METHOD, bool FIRST>
+__global__ __launch_bounds__(64 * kLatdWaves, 1) void mk_latd_kernel(StepArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    load_image(smem, a.img);
+    latd_step<DG, METHOD, FIRST>(a, smem);
+}
+
+// Steps [t0, t1) (t = u n + i, none of them the first) of a batch of at most one
+// gate per CU in ONE launch: each workgroup runs its gate's steps back to back,
+// with the LDS tables loaded once and no launch between steps.  A step's
+// accumulator stores are complete (vmcnt) and the workgroup has passed a barrier
+// before the next step's waves read them: the waves of a workgroup share the CU's
+// write-through L1, so no cache maintenance is needed at workgroup scope.
+struct LatdRun {
+    const uint32_t* keys;   // key blocks [k][n + 1] of kbw words (mkacc_engine key_step)
+    const uint32_t* cvals;  // [k n][cstride] exponents, this launch's gates at column 0
+    uint32_t* acc0;         // step t0's input; t0 + 1's input in acc1, and so on
+    uint32_t* acc1;
+    uint64_t kbw;           // words per key block
+    uint32_t cstride, n, t0, t1, key2off;
+};
+template <int DG, int METHOD>
+__global__ __launch_bounds__(64 * kLatdWaves, 1) void mk_latd_run_kernel(StepArgs a, LatdRun r) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    load_image(smem, a.img);
+#pragma unroll 1
+    for (uint32_t t = r.t0; t < r.t1; ++t) {
+        const uint32_t u = t / r.n, i = t - u * r.n;
+        StepArgs b = a;
+        b.key1 = r.keys + ((uint64_t)u * (r.n + 1) + i) * r.kbw;
+        b.key2 = b.key1 + r.key2off;
+        b.cvals = r.cvals + (uint64_t)t * r.cstride;
+        b.index = u;
+        const bool odd = ((t - r.t0) & 1u) != 0;
+        b.acc_in = odd ? r.acc1 : r.acc0;
+        b.acc_out = odd ? r.acc0 : r.acc1;
+        latd_step<DG, METHOD, false>(b, smem);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
 }
 
 // ---- batch prologue / epilogue kernels --------------------------------------
@@ -1118,6 +1158,10 @@ StepFn pick_latd(int method, bool first) {
     if (method == XZW) return first ? mk_latd_kernel<DG, XZW, true> : mk_latd_kernel<DG, XZW, false>;
     return first ? mk_latd_kernel<DG, XZW_B, true> : mk_latd_kernel<DG, XZW_B, false>;
 }
+template <int DG>
+const void* pick_latd_run(int method) {
+    return method == XZW ? (const void*)mk_latd_run_kernel<DG, XZW> : (const void*)mk_latd_run_kernel<DG, XZW_B>;
+}
 
 }  // namespace
 
@@ -1139,6 +1183,9 @@ MKACC_TU_API KernelPtr lat_dg4(int method, bool first);
 MKACC_TU_API KernelPtr latd_dg2(int method, bool first);   // mk_latd_kernel (k = 2, digits split over waves)
 MKACC_TU_API KernelPtr latd_dg3(int method, bool first);
 MKACC_TU_API KernelPtr latd_dg4(int method, bool first);
+MKACC_TU_API KernelPtr latdrun_dg2(int method);   // mk_latd_run_kernel (the later steps in one launch)
+MKACC_TU_API KernelPtr latdrun_dg3(int method);
+MKACC_TU_API KernelPtr latdrun_dg4(int method);
 MKACC_TU_API KernelPtr wide_step(int method, bool first);     // mkacc_wide.hpp (integer 64-bit words)
 MKACC_TU_API KernelPtr widereg2_step(int method, bool first);  // mkacc_widereg2.hpp (FP64, Q < 2^50)
 }  // namespace mkacc_tu
