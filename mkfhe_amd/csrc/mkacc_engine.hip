@@ -129,6 +129,14 @@ const void* latdrun_fn(int dg, int method) {
         default: return nullptr;
     }
 }
+const void* latrun_fn(int dg, int method) {
+    switch (dg) {
+        case 2: return mkacc_tu::latrun_dg2(method);
+        case 3: return mkacc_tu::latrun_dg3(method);
+        case 4: return mkacc_tu::latrun_dg4(method);
+        default: return nullptr;
+    }
+}
 const void* lat_fn(int dg, int method, bool first) {
     switch (dg) {
         case 2: return mkacc_tu::lat_dg2(method, first);
@@ -406,11 +414,13 @@ struct StepChain {
         std::swap(cur, nxt);
         return true;
     }
-    // steps [t0, t1) (t = u n + i, t0 >= 1) in one mk_latd_run_kernel launch
-    // (use_latd batches); false if the build has no kernel for it
+    // steps [t0, t1) (t = u n + i, t0 >= 1) in one mk_latd_run_kernel (use_latd
+    // batches) or mk_lat_run_kernel launch; false if the build has no kernel for it
     bool run(uint32_t t0, uint32_t t1) {
         const uint32_t n = c->p.n;
-        const void* fn = latdrun_fn((int)c->dg, c->method_class);
+        const bool split = use_latd(c, Bh);
+        const uint32_t waves = split ? kLatdWaves : c->p.k;
+        const void* fn = split ? latdrun_fn((int)c->dg, c->method_class) : latrun_fn((int)c->dg, c->method_class);
         if (!fn || t0 == 0 || t0 >= t1) return false;
         const StepArgs a = args(t0 / n, t0 % n);
         LatdRun r;
@@ -424,7 +434,7 @@ struct StepChain {
         r.t0 = t0;
         r.t1 = t1;
         r.key2off = c->nk == 2 ? (uint32_t)(c->dg * 2 * kN) : 0u;
-        launch_ptr2(fn, dim3((unsigned)Bh), dim3(64 * kLatdWaves), lat_lds_bytes(kLatdWaves), st, a, r);
+        launch_ptr2(fn, dim3((unsigned)Bh), dim3(64 * waves), lat_lds_bytes(waves), st, a, r);
         if ((t1 - t0) & 1u) std::swap(cur, nxt);
         return true;
     }
@@ -435,6 +445,10 @@ struct StepChain {
 // (mk_latd_run_kernel); MKACC_LATD_RUN=0 (build flag, A/B) keeps one launch per step.
 #ifndef MKACC_LATD_RUN
 #define MKACC_LATD_RUN 1
+#endif
+// and those of the one-wave-per-party kernel (mk_lat_run_kernel); MKACC_LAT_RUN=0
+#ifndef MKACC_LAT_RUN
+#define MKACC_LAT_RUN 1
 #endif
 
 // Joins the slice streams a batch forked from the context stream back into it on
@@ -476,7 +490,9 @@ uint32_t* launch_steps(mkacc_ctx* c, size_t B) {
     const size_t ns = std::min<size_t>((size_t)c->nstreams, B / unit);
     if (ns < 2) {
         StepChain ch(c, B, 0, B, c->stream);
-        if (MKACC_LATD_RUN && ch.lat && use_latd(c, B) && (size_t)k * n > 1) {
+        const bool run = use_latd(c, B) ? MKACC_LATD_RUN
+                                        : MKACC_LAT_RUN && k <= kLatRunMaxK && (size_t)k * B <= (size_t)c->cus * 4;
+        if (ch.lat && (size_t)k * n > 1 && run) {
             if (!ch.step(0, 0, lds) || !ch.run(1, k * n)) return nullptr;
             return ch.result();
         }

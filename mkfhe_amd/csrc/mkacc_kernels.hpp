@@ -548,9 +548,7 @@ __global__ __launch_bounds__(kThreads, 2) void mk_step_kernel(StepArgs a) {
 constexpr uint32_t kLatMaxK = 8;
 constexpr size_t lat_lds_bytes(uint32_t k) { return (size_t)(kLdsTabWords + k * kLdsWords) * 4; }
 template <int DG, int METHOD, bool FIRST>
-__global__ __launch_bounds__(64 * kLatMaxK, 1) void mk_lat_kernel(StepArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    load_image(smem, a.img);
+__device__ __forceinline__ void lat_step(const StepArgs a, uint32_t* smem) {
     const uint32_t l = threadIdx.x & 63u;
     const uint32_t u = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // this wave's party
     const uint32_t gate = blockIdx.x;
@@ -580,10 +578,12 @@ __global__ __launch_bounds__(64 * kLatMaxK, 1) void mk_lat_kernel(StepArgs a) {
     uint64_t sv[kRegs], w[kRegs];
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) sv[r] = 0;
-    if (u == index)
+    if (u == index) {
         party_pass<DG, METHOD, FIRST, true>(s, u, sv, w);
-    else
+    } else {
         party_pass<DG, METHOD, FIRST, false>(s, u, sv, w);
+        vcc_fence();   // the branches' join follows the party's last reductions
+    }
     // this party's sumV share, [0, 2Q), into the wave's own (now idle) scratch
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) scratch[r * 64 + l] = redc(sv[r], Q, s.m.qinv);
@@ -607,6 +607,12 @@ __global__ __launch_bounds__(64 * kLatMaxK, 1) void mk_lat_kernel(StepArgs a) {
         x[r] = min(v, v - 2u * Q);                                                               // [0, 2Q)
     }
     f_part<DG, METHOD, FIRST>(s, index, w, x);
+}
+template <int DG, int METHOD, bool FIRST>
+__global__ __launch_bounds__(64 * kLatMaxK, 1) void mk_lat_kernel(StepArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    load_image(smem, a.img);
+    lat_step<DG, METHOD, FIRST>(a, smem);
 }
 
 // One accumulator step for one gate per wavefront.
@@ -848,7 +854,7 @@ __device__ __forceinline__ void f_digit(const StepCtx& s, uint32_t f, uint64_t (
 }
 
 template <int DG, int METHOD, bool FIRST>
-__device__ __forceinline__ void latd_step(const StepArgs& a, uint32_t* smem) {
+__device__ __forceinline__ void latd_step(const StepArgs a, uint32_t* smem) {
     using Bd = Bounds<DG, METHOD, FIRST>;
     const uint32_t l = threadIdx.x & 63u;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // this wave
@@ -984,22 +990,43 @@ struct LatdRun {
     uint64_t kbw;           // words per key block
     uint32_t cstride, n, t0, t1, key2off;
 };
+// step t's arguments from the launch's first-step arguments
+__device__ __forceinline__ StepArgs run_args(const StepArgs& a, const LatdRun& r, uint32_t t) {
+    const uint32_t u = t / r.n, i = t - u * r.n;
+    StepArgs b = a;
+    b.key1 = r.keys + ((uint64_t)u * (r.n + 1) + i) * r.kbw;
+    b.key2 = b.key1 + r.key2off;
+    b.cvals = r.cvals + (uint64_t)t * r.cstride;
+    b.index = u;
+    const bool odd = ((t - r.t0) & 1u) != 0;
+    b.acc_in = odd ? r.acc1 : r.acc0;
+    b.acc_out = odd ? r.acc0 : r.acc1;
+    return b;
+}
 template <int DG, int METHOD>
 __global__ __launch_bounds__(64 * kLatdWaves, 1) void mk_latd_run_kernel(StepArgs a, LatdRun r) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     load_image(smem, a.img);
 #pragma unroll 1
     for (uint32_t t = r.t0; t < r.t1; ++t) {
-        const uint32_t u = t / r.n, i = t - u * r.n;
-        StepArgs b = a;
-        b.key1 = r.keys + ((uint64_t)u * (r.n + 1) + i) * r.kbw;
-        b.key2 = b.key1 + r.key2off;
-        b.cvals = r.cvals + (uint64_t)t * r.cstride;
-        b.index = u;
-        const bool odd = ((t - r.t0) & 1u) != 0;
-        b.acc_in = odd ? r.acc1 : r.acc0;
-        b.acc_out = odd ? r.acc0 : r.acc1;
-        latd_step<DG, METHOD, false>(b, smem);
+        latd_step<DG, METHOD, false>(run_args(a, r, t), smem);
+        vcc_fence();   // the loop branch follows the step's last reductions
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+}
+// the same for mk_lat_kernel (one wave per party) at k <= kLatRunMaxK: the register
+// file of one wave per SIMD (VGPRs + AGPRs; at 256 the loop spills), so the host takes
+// it only for batches whose k B waves are resident at once (one wave per SIMD)
+constexpr uint32_t kLatRunMaxK = 4;
+template <int DG, int METHOD>
+__global__ __launch_bounds__(64 * kLatRunMaxK, 1) void mk_lat_run_kernel(StepArgs a, LatdRun r) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    load_image(smem, a.img);
+#pragma unroll 1
+    for (uint32_t t = r.t0; t < r.t1; ++t) {
+        lat_step<DG, METHOD, false>(run_args(a, r, t), smem);
+        vcc_fence();   // the loop branch follows the step's last reductions
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
@@ -1162,6 +1189,10 @@ template <int DG>
 const void* pick_latd_run(int method) {
     return method == XZW ? (const void*)mk_latd_run_kernel<DG, XZW> : (const void*)mk_latd_run_kernel<DG, XZW_B>;
 }
+template <int DG>
+const void* pick_lat_run(int method) {
+    return method == XZW ? (const void*)mk_lat_run_kernel<DG, XZW> : (const void*)mk_lat_run_kernel<DG, XZW_B>;
+}
 
 }  // namespace
 
@@ -1186,6 +1217,9 @@ MKACC_TU_API KernelPtr latd_dg4(int method, bool first);
 MKACC_TU_API KernelPtr latdrun_dg2(int method);   // mk_latd_run_kernel (the later steps in one launch)
 MKACC_TU_API KernelPtr latdrun_dg3(int method);
 MKACC_TU_API KernelPtr latdrun_dg4(int method);
+MKACC_TU_API KernelPtr latrun_dg2(int method);    // mk_lat_run_kernel (the later steps in one launch)
+MKACC_TU_API KernelPtr latrun_dg3(int method);
+MKACC_TU_API KernelPtr latrun_dg4(int method);
 MKACC_TU_API KernelPtr wide_step(int method, bool first);     // mkacc_wide.hpp (integer 64-bit words)
 MKACC_TU_API KernelPtr widereg2_step(int method, bool first);  // mkacc_widereg2.hpp (FP64, Q < 2^50)
 }  // namespace mkacc_tu

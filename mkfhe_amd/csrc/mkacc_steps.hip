@@ -45,6 +45,7 @@ KernelPtr MKACC_CAT(latd_dg, MKACC_TU_DG)(int method, bool first) {
     return (KernelPtr)pick_latd<MKACC_TU_DG>(method, first);
 }
 KernelPtr MKACC_CAT(latdrun_dg, MKACC_TU_DG)(int method) { return pick_latd_run<MKACC_TU_DG>(method); }
+KernelPtr MKACC_CAT(latrun_dg, MKACC_TU_DG)(int method) { return pick_lat_run<MKACC_TU_DG>(method); }
 #elif MKACC_TU_PART == 2
 KernelPtr MKACC_CAT(step2_dg, MKACC_TU_DG)(int method) { return (KernelPtr)pick_step2<MKACC_TU_DG, false>(method); }
 #else
