@@ -441,15 +441,15 @@ struct StepChain {
     uint32_t* result() const { return cur - ao; }   // the full-batch buffer holding the result
 };
 
-// Batches of the split-digit kernel run the steps after the first in one launch
-// (mk_latd_run_kernel); MKACC_LATD_RUN=0 (build flag, A/B) keeps one launch per step.
-#ifndef MKACC_LATD_RUN
-#define MKACC_LATD_RUN 1
-#endif
-// and those of the one-wave-per-party kernel (mk_lat_run_kernel); MKACC_LAT_RUN=0
-#ifndef MKACC_LAT_RUN
-#define MKACC_LAT_RUN 1
-#endif
+// Small batches run the steps after the first in one launch: every batch of the
+// split-digit kernel (mk_latd_run_kernel: -9 % at B = 1, -22 % at B = 256,
+// profiles/r5/ab_latd_run_v24.txt) and those of the one-wave-per-party kernel whose
+// k B waves are resident at once at k <= 4 (mk_lat_run_kernel, ab_lat_run_v25.txt).
+bool use_run(const mkacc_ctx* c, size_t B) {
+    const size_t k = c->p.k;
+    if (!use_lat(c, B) || k * c->p.n < 2) return false;
+    return use_latd(c, B) || (k <= kLatRunMaxK && k * B <= (size_t)c->cus * 4);
+}
 
 // Joins the slice streams a batch forked from the context stream back into it on
 // every exit path: later work on c->stream -- a key upload's
@@ -490,9 +490,7 @@ uint32_t* launch_steps(mkacc_ctx* c, size_t B) {
     const size_t ns = std::min<size_t>((size_t)c->nstreams, B / unit);
     if (ns < 2) {
         StepChain ch(c, B, 0, B, c->stream);
-        const bool run = use_latd(c, B) ? MKACC_LATD_RUN
-                                        : MKACC_LAT_RUN && k <= kLatRunMaxK && (size_t)k * B <= (size_t)c->cus * 4;
-        if (ch.lat && (size_t)k * n > 1 && run) {
+        if (use_run(c, B)) {
             if (!ch.step(0, 0, lds) || !ch.run(1, k * n)) return nullptr;
             return ch.result();
         }
