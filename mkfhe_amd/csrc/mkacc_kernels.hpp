@@ -1019,8 +1019,12 @@ __global__ __launch_bounds__(64 * kLatdWaves, 1) void mk_latd_run_kernel(StepArg
 // file of one wave per SIMD (VGPRs + AGPRs; at 256 the loop spills), so the host takes
 // it only for batches whose k B waves are resident at once (one wave per SIMD)
 constexpr uint32_t kLatRunMaxK = 4;
+// workgroups per CU the loop is built for: two at dg = 2 (spill-free at 256 VGPRs;
+// k = 4, B = 512: 90.6 -> 82.8 ms, B <= 256 within 1 %, profiles/r5/ab_lat_run_occ_v28.txt),
+// one above (two would spill 20-52 B per lane)
+constexpr uint32_t lat_run_occ(uint32_t dg) { return dg == 2 ? 2 : 1; }
 template <int DG, int METHOD>
-__global__ __launch_bounds__(64 * kLatRunMaxK, 1) void mk_lat_run_kernel(StepArgs a, LatdRun r) {
+__global__ __launch_bounds__(64 * kLatRunMaxK, lat_run_occ(DG)) void mk_lat_run_kernel(StepArgs a, LatdRun r) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     load_image(smem, a.img);
 #pragma unroll 1
