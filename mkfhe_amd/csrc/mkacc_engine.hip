@@ -448,7 +448,7 @@ struct StepChain {
 bool use_run(const mkacc_ctx* c, size_t B) {
     const size_t k = c->p.k;
     if (!use_lat(c, B) || k * c->p.n < 2) return false;
-    return use_latd(c, B) || (k <= kLatRunMaxK && k * B <= (size_t)c->cus * 4 * lat_run_occ(c->dg));
+    return use_latd(c, B) || (k <= lat_run_max_k(c->dg) && k * B <= (size_t)c->cus * 4 * lat_run_occ(c->dg));
 }
 
 // Joins the slice streams a batch forked from the context stream back into it on

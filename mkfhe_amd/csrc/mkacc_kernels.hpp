@@ -1023,8 +1023,12 @@ constexpr uint32_t kLatRunMaxK = 4;
 // k = 4, B = 512: 90.6 -> 82.8 ms, B <= 256 within 1 %, profiles/r5/ab_lat_run_occ_v28.txt),
 // one above (two would spill 20-52 B per lane)
 constexpr uint32_t lat_run_occ(uint32_t dg) { return dg == 2 ? 2 : 1; }
+// parties the loop is built for: up to kLatMaxK at dg = 2 (eight waves of 256 VGPRs
+// are the same register budget as two four-wave workgroups), kLatRunMaxK above
+constexpr uint32_t lat_run_max_k(uint32_t dg) { return dg == 2 ? kLatMaxK : kLatRunMaxK; }
 template <int DG, int METHOD>
-__global__ __launch_bounds__(64 * kLatRunMaxK, lat_run_occ(DG)) void mk_lat_run_kernel(StepArgs a, LatdRun r) {
+__global__ __launch_bounds__(64 * lat_run_max_k(DG), DG == 2 ? 1 : lat_run_occ(DG)) void mk_lat_run_kernel(StepArgs a,
+                                                                                                       LatdRun r) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     load_image(smem, a.img);
 #pragma unroll 1

@@ -79,6 +79,7 @@ CASES = [
     ("XZW_B", 16, 2, 32749, 1 << 7, 3),   # STD128_MKNTRU_LWE_4 shape: 16 parties, dg=3
     ("XZW", 8, 3, 45181, 1 << 6, 2),      # STD128_MKNTRU_3 shape (config 4): 8 parties, dg=4
     ("XZW_B", 3, 3, 32749, 1 << 6, 3),    # dg=4, binary keys
+    ("XZW", 8, 2, 45181, 1 << 9, 2),      # STD100_MKNTRU_3 shape: 8 parties, dg=2
 ]
 
 
