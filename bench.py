@@ -50,7 +50,7 @@ METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 # measured on this pool (tools/ubench_intops.hip, profiles/round1_ubench_intops.txt)
 PEAK_SHOUP_MULMOD_TPS = 7.744e12     # 27-bit Shoup mod-mul / s, whole chip
 # 64-bit word path (tools/ubench_wide.hip, profiles/r2/ubench_wide.txt, 50-bit Q):
-PEAK_FP64_MULMOD_TPS = 5.7455e12     # exact FP64 product (mkacc_widefp.hpp) / s
+PEAK_FP64_MULMOD_TPS = 5.7455e12     # exact FP64 product (mkacc_fp64.hpp, widereg2 kernel) / s
 PEAK_INT64_MULMOD_TPS = 1.7433e12    # limb-built 64-bit Shoup product (mkacc_wide.hpp) / s
 PEAK_HBM_GBS = 8000.0                # MI355X_MICROARCH.md (spec)
 Q50 = 1125899906826241               # config 5 stress modulus
@@ -467,7 +467,7 @@ def run_rank(args, env: dict, make_engine, make_checker, torch_device: str, back
         # (mkacc_engine.hip launch_steps / wide_launch_batch): one accumulator step of the
         # batch is then `slices` launches, and per_launch_us is the time of one such step
         slices = 1
-        if is_cuda and kname in ("mk_step_kernel", "mk_step2_kernel", "mk_step3_kernel", "widereg2::step_kernel"):
+        if is_cuda and kname in ("mk_step_kernel", "mk_step2_kernel", "widereg2::step_kernel"):
             import torch
             cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
             ev = os.environ.get("MKACC_STREAMS", "")
@@ -518,7 +518,8 @@ def run_rank(args, env: dict, make_engine, make_checker, torch_device: str, back
                              "slice launch with its own (overlapping) duration" if slices > 1 else
                              "the pass time / (k n): small batches at k <= 4 run the steps after the first in one launch "
                              "(mk_latd_run_kernel / mk_lat_run_kernel, DESIGN.md s3)" if kname in
-                             ("mk_lat_kernel", "mk_latd_kernel") else "one launch"))},
+                             ("mk_lat_kernel", "mk_latd_kernel", "mk_lat_run_kernel", "mk_latd_run_kernel")
+                             else "one launch"))},
             # VALU view: algorithmic mod-muls per launch against the measured rate of the
             # product the kernel is built on (32-bit Shoup; FP64 or 64-bit Shoup on the wide path)
             "roofline_valu": {

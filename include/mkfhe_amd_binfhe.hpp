@@ -762,13 +762,23 @@ public:
             fp.acc.Q != m_kp.acc.Q || fp.acc.baseG != m_kp.acc.baseG || fp.ks.qKS != m_kp.ks.qKS)
             throw config_error(path + " was generated for a different context");
         UniEncBTKey ek;
+        // a section the file does not have stays empty; a damaged file (a size past
+        // its end, truncation, a checksum) throws
         auto get = [&](const char* nm, std::vector<uint32_t>& v) {
             v.resize(mkkg_file_section_words(path.c_str(), nm));
-            if (!v.empty()) checkk(mkkg_file_read_section(path.c_str(), nm, v.data(), v.size()));
+            if (!v.empty()) {
+                checkk(mkkg_file_read_section(path.c_str(), nm, v.data(), v.size()));
+            } else if (mkkg_file_read_section(path.c_str(), nm, nullptr, 0) != MKACC_OK) {
+                const std::string e = mkkg_last_error();
+                if (e.find("has no section") == std::string::npos) throw config_error(path + ": " + e);
+            }
         };
         get("crs", ek.crs); get("skN", ek.fvec); get("skN_eval", ek.f_eval); get("skNinv_eval", ek.finv_eval);
         get("pkey", ek.pkey); get("evk", ek.evk); get("ksk", ek.ksk); get("ksk_a", ek.ksk_a); get("ksk_b", ek.ksk_b);
-        if (ek.evk.size() != mkkg_evk_words(&m_kp) || ek.pkey.size() != mkkg_pkey_words(&m_kp))
+        const bool lwe = m_method == MKNTRU_LWE;
+        if (ek.evk.size() != mkkg_evk_words(&m_kp) || ek.pkey.size() != mkkg_pkey_words(&m_kp) ||
+            (lwe ? ek.ksk_a.size() != mkkg_ksk_mklwe_a_words(&m_kp) || ek.ksk_b.size() != mkkg_ksk_mklwe_b_words(&m_kp)
+                 : ek.ksk.size() != mkkg_ksk_mntru_words(&m_kp)))
             throw config_error(path + ": key sizes do not match the context");
         up_keys(ek.evk.data(), ek.pkey.data());
         if (m_method == MKNTRU_LWE)

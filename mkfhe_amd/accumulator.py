@@ -150,7 +150,7 @@ class MKAccumulatorEngine:
 
     @property
     def wide_fp(self) -> bool:
-        """True if the 64-bit word path runs its FP64 kernels (Q < 2^50, mkacc_widefp.hpp)."""
+        """True if the 64-bit word path runs its FP64 kernels (Q < 2^50, mkacc_fp64.hpp / mkacc_widereg2.hpp)."""
         return _lib.load().mkacc_is_wide(self._h) == 2
 
     def step_kernel_name(self, B: int) -> str:

@@ -24,7 +24,8 @@ import sys
 _HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(_HERE)
 SOURCES = [os.path.join(_HERE, "csrc", f) for f in ("mkacc_engine.hip", "mkacc_steps.hip")]
-HEADERS = [os.path.join(_HERE, "csrc", f) for f in ("mkacc_kernels.hpp", "mkacc_step2.hpp", "mkacc_device.hpp", "mkacc_host_math.hpp",
+HEADERS = [os.path.join(_HERE, "csrc", f) for f in ("mkacc_kernels.hpp", "mkacc_step2.hpp", "mkacc_quad.hpp",
+                                                    "mkacc_device.hpp", "mkacc_host_math.hpp",
                                                     "mkacc_gate.hpp", "mkacc_wide.hpp", "mkacc_fp64.hpp",
                                                     "mkacc_widereg2.hpp", "mkacc_layout2.hpp")] + [
     os.path.join(ROOT, "include", "mkfhe_amd.h")]
@@ -69,22 +70,30 @@ def _stale(out, deps) -> bool:
     return any(os.path.getmtime(f) > t for f in deps)
 
 
-def build_keys(force: bool = False, verbose: bool = False) -> str:
-    """Host key-material library (plain C++, no GPU)."""
-    if not force and not _stale(KEYS_OUT, KEYS_SOURCES + KEYS_HEADERS):
-        return KEYS_OUT
-    os.makedirs(os.path.dirname(KEYS_OUT), exist_ok=True)
+# AddressSanitizer + UBSan build of the key library (tests/test_sanitize.py loads it
+# through MKFHE_KEYS_LIB with libasan preloaded): lib/variants/libmkfhe_keys_asan.so
+SANITIZE = ["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"]
+KEYS_ASAN_OUT = os.path.join(_HERE, "lib", "variants", "libmkfhe_keys_asan.so")
+
+
+def build_keys(force: bool = False, verbose: bool = False, sanitize: bool = False) -> str:
+    """Host key-material library (plain C++, no GPU); sanitize: the ASan/UBSan build."""
+    out = KEYS_ASAN_OUT if sanitize else KEYS_OUT
+    if not force and not _stale(out, KEYS_SOURCES + KEYS_HEADERS):
+        return out
+    os.makedirs(os.path.dirname(out), exist_ok=True)
     cxx = os.environ.get("CXX", "g++")
+    opt = SANITIZE if sanitize else ["-O3"]
     # inline helpers stay private to each library (both include mkacc_host_math.hpp)
-    cmd = [cxx, "-O3", "-march=x86-64-v3", "-std=c++17", "-fPIC", "-shared", "-pthread",
+    cmd = [cxx, *opt, "-march=x86-64-v3", "-std=c++17", "-fPIC", "-shared", "-pthread",
            "-fvisibility-inlines-hidden", "-Wl,-Bsymbolic",
            "-I", os.path.join(ROOT, "include"), "-I", os.path.join(_HERE, "csrc"),
-           *_id_defines("MKKG", keys_ids(), []), "-o", KEYS_OUT + ".tmp"] + KEYS_SOURCES
+           *_id_defines("MKKG", keys_ids(), ["sanitize"] if sanitize else []), "-o", out + ".tmp"] + KEYS_SOURCES
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)
-    os.replace(KEYS_OUT + ".tmp", KEYS_OUT)
-    return KEYS_OUT
+    os.replace(out + ".tmp", out)
+    return out
 
 
 # Machine-scheduler strategy of the step2 unit at dg = 3 (the headline kernel):
@@ -102,6 +111,8 @@ STEP2_BFLY = {2: ["-DMKACC_BFLY_C=1"], 3: ["-DMKACC_BFLY_C=1"]}
 # and mk_lat_kernel (small batches, few waves per SIMD to hide a wait state): a
 # 64-gate STD128_MKNTRU batch 65.7 -> 63.0 ms (profiles/r5/ab_lat_bfly_c.txt)
 LAT_BFLY = ["-DMKACC_BFLY_C=1"]
+# and mk_quad_kernel (one wave per SIMD: the asm form's wait states are not hidden)
+QUAD_BFLY = ["-DMKACC_BFLY_C=1"]
 # mk_step_kernel at dg = 4 (config 4): the forward transforms only (MKACC_BFLY_C=2);
 # in every transform it needs 8 B of scratch and is 0.6 % slower, forward-only is
 # spill-free and 1.0-1.1 % faster (profiles/r5/ab_c4_bfly_c.txt)
@@ -124,6 +135,7 @@ UNITS = [("engine", "mkacc_engine.hip", [])] + [
     for d in (2, 3)] + [
     (f"step2f_dg{d}", "mkacc_steps.hip", [f"-DMKACC_TU_DG={d}", "-DMKACC_TU_PART=3"] + STEP2_SCHED.get(d, []))
     for d in (2, 3)] + [
+    (f"quad_dg{d}", "mkacc_steps.hip", [f"-DMKACC_TU_DG={d}", "-DMKACC_TU_PART=4"] + QUAD_BFLY) for d in (2, 3, 4, 5)] + [
     ("wide", "mkacc_steps.hip", ["-DMKACC_TU_WIDE=1"]), ("widereg2", "mkacc_steps.hip", ["-DMKACC_TU_WIDE=2"])]
 
 
@@ -148,9 +160,26 @@ def included_files(path: str, seen=None) -> list[str]:
     return seen
 
 
+_COMPILER_ID: dict[str, str] = {}
+
+
+def compiler_id(hipcc: str) -> str:
+    """The toolchain a unit object was built with: `hipcc --version` (ROCm and clang
+    versions) plus the resolved path and mtime of the compiler binary, so a cached
+    object is never linked next to units from another toolchain."""
+    if hipcc not in _COMPILER_ID:
+        r = subprocess.run([hipcc, "--version"], capture_output=True, text=True)
+        real = os.path.realpath(hipcc)
+        st = os.stat(real) if os.path.exists(real) else None
+        _COMPILER_ID[hipcc] = f"{r.stdout}|{real}|{st.st_mtime_ns if st else 0}"
+    return _COMPILER_ID[hipcc]
+
+
 def unit_key(path: str, cmd: list[str]) -> str:
-    """Identity of one translation unit's compile: its sources and its command line."""
+    """Identity of one translation unit's compile: its sources, its command line and
+    the compiler (compiler_id)."""
     h = hashlib.sha256(" ".join(cmd).encode())
+    h.update(compiler_id(cmd[0]).encode())
     for f in included_files(path):
         with open(f, "rb") as fh:
             h.update(f.encode() + b"\0" + fh.read())
@@ -263,7 +292,9 @@ def build_variant(name: str, flags: list[str], verbose: bool = False, only=None)
 
 
 if __name__ == "__main__":
-    if "--variant" in sys.argv:
+    if "--keys-asan" in sys.argv:
+        print(build_keys(force="--force" in sys.argv, verbose=True, sanitize=True))
+    elif "--variant" in sys.argv:
         args = list(sys.argv[1:])
         only = None
         if "--units" in args:

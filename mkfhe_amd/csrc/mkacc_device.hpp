@@ -316,6 +316,11 @@ constexpr int kTwlPairs = kTwlC + 1024;    // 2016 pairs per direction
 // arithmetic instead of stalling the wave.  A stream is a list of chunks
 // {stage, first pair m0, pair count}; LD / AP are the direction's load and
 // butterfly functors.
+// MKACC_TW_FENCE = 0 lets the scheduler move work across chunk boundaries (more
+// independent butterflies in flight for a lone wave per SIMD; more live registers).
+#ifndef MKACC_TW_FENCE
+#define MKACC_TW_FENCE 1
+#endif
 struct TwChunk { int s, m0, cnt; };
 template <class SEQ, int I, int W, class LD, class AP>
 __device__ __forceinline__ void tw_pipe(uint2 (&wa)[W], uint2 (&wb)[W], const LD& ld, const AP& ap) {
@@ -325,7 +330,7 @@ __device__ __forceinline__ void tw_pipe(uint2 (&wa)[W], uint2 (&wb)[W], const LD
         ld.template go<n.s, n.m0, n.cnt>((I + 1) % 2 ? wb : wa);
     }
     ap.template go<c.s, c.m0, c.cnt>(I % 2 ? wb : wa);
-    sched_fence();
+    if constexpr (MKACC_TW_FENCE) sched_fence();
     if constexpr (I + 1 < SEQ::N) tw_pipe<SEQ, I + 1>(wa, wb, ld, ap);
 }
 // forward pass A (stages 0..4, layout A): wave-uniform twiddles, scalar loads

@@ -137,6 +137,24 @@ const void* latrun_fn(int dg, int method) {
         default: return nullptr;
     }
 }
+const void* quad_fn(int dg, int method, bool first) {
+    switch (dg) {
+        case 2: return mkacc_tu::quad_dg2(method, first);
+        case 3: return mkacc_tu::quad_dg3(method, first);
+        case 4: return mkacc_tu::quad_dg4(method, first);
+        case 5: return mkacc_tu::quad_dg5(method, first);
+        default: return nullptr;
+    }
+}
+const void* quadrun_fn(int dg, int method) {
+    switch (dg) {
+        case 2: return mkacc_tu::quadrun_dg2(method);
+        case 3: return mkacc_tu::quadrun_dg3(method);
+        case 4: return mkacc_tu::quadrun_dg4(method);
+        case 5: return mkacc_tu::quadrun_dg5(method);
+        default: return nullptr;
+    }
+}
 const void* lat_fn(int dg, int method, bool first) {
     switch (dg) {
         case 2: return mkacc_tu::lat_dg2(method, first);
@@ -156,6 +174,11 @@ void launch_ptr(const void* fn, dim3 grid, dim3 block, size_t lds, hipStream_t s
 template <class A, class R>
 void launch_ptr2(const void* fn, dim3 grid, dim3 block, size_t lds, hipStream_t s, A a, R r) {
     void* args[] = {&a, &r};
+    (void)hipLaunchKernel(fn, grid, block, args, lds, s);
+}
+template <class A, class R, class T>
+void launch_ptr3(const void* fn, dim3 grid, dim3 block, size_t lds, hipStream_t s, A a, R r, T t) {
+    void* args[] = {&a, &r, &t};
     (void)hipLaunchKernel(fn, grid, block, args, lds, s);
 }
 
@@ -216,6 +239,12 @@ struct mkacc_ctx {
     int cus = 256;                // compute units of the device (mk_lat_kernel residency)
     int method_class = XZW;   // XZW or XZW_B
     int step_ver = 1;         // batch step kernel generation (step_version)
+    // kernel-choice overrides, read once at mkacc_create (-1: unset, 0 / 1 forced):
+    // MKACC_LAT (small-batch kernels), MKACC_LATD (split-digit kernel), MKACC_DSCR
+    // (d_i scratch), so every launch and mkacc_step_kernel_name agree for the
+    // context's lifetime
+    int env_lat = -1, env_latd = -1, env_dscr = -1, env_quad = -1;
+    uint32_t* d_qimg = nullptr;   // mk_quad_kernel tables: TF, TI, TW (mkacc_quad.hpp), 3N pairs
     uint32_t dg = 0, nk = 0;
     Mod mod{};
     SddConsts sd{};
@@ -304,9 +333,13 @@ const uint32_t* key_step(const mkacc_ctx* c, uint32_t u, uint32_t i, uint32_t j)
 constexpr uint32_t kDscrMinK = 4;
 bool use_dscr(const mkacc_ctx* c) {
     if (c->method_class != XZW || c->p.k < 2 || c->step_ver != 1) return false;
-    const char* e = std::getenv("MKACC_DSCR");
-    if (e && *e) return e[0] != '0';
+    if (c->env_dscr >= 0) return c->env_dscr != 0;
     return c->p.k >= kDscrMinK;
+}
+// an environment switch: -1 unset, else 0 (value starting with '0') or 1
+int env_switch(const char* name) {
+    const char* e = std::getenv(name);
+    return e && *e ? (e[0] != '0') : -1;
 }
 
 // Two-party batches of at most one gate per CU split each party's digits over two
@@ -314,8 +347,7 @@ bool use_dscr(const mkacc_ctx* c) {
 // MKACC_LATD=0 keeps one wave per party (mk_lat_kernel).
 bool use_latd(const mkacc_ctx* c, size_t B) {
     if (c->p.k != 2 || B > (size_t)c->cus) return false;
-    const char* e = std::getenv("MKACC_LATD");
-    return !(e && e[0] == '0');
+    return c->env_latd != 0;
 }
 
 // Small batches take mk_lat_kernel (one wave per party) while the whole batch
@@ -327,9 +359,16 @@ bool use_latd(const mkacc_ctx* c, size_t B) {
 constexpr size_t kLdsPerCu = 160 * 1024;
 bool use_lat(const mkacc_ctx* c, size_t B) {
     if (c->p.k < 2 || c->p.k > kLatMaxK || c->dg > 4) return false;
-    const char* e = std::getenv("MKACC_LAT");
-    if (e && *e) return e[0] != '0';
+    if (c->env_lat >= 0) return c->env_lat != 0;
     return B <= (size_t)c->cus * (kLdsPerCu / lat_lds_bytes(c->p.k));
+}
+
+// Small batches of at most one gate per CU take mk_quad_kernel (every polynomial
+// spread over the four waves of the gate's workgroup, mkacc_quad.hpp) when
+// MKACC_QUAD=1.
+bool use_quad(const mkacc_ctx* c, size_t B) {
+    if (c->wide || c->dg < 2 || c->dg > 5 || B > (size_t)c->cus) return false;
+    return c->env_quad == 1;
 }
 
 // Per-gate scratch words of the batch step kernel: mk_step_kernel DSCR keeps the
@@ -364,10 +403,10 @@ struct StepChain {
     hipStream_t st;
     uint32_t* cur;
     uint32_t* nxt;
-    bool lat;
+    bool lat, quad;
     StepChain(mkacc_ctx* c_, size_t B_, size_t g0_, size_t Bh_, hipStream_t st_)
         : c(c_), B(B_), g0(g0_), Bh(Bh_), ao(g0_ * c_->p.k * kN), st(st_), cur(c_->d_acc0 + ao), nxt(c_->d_acc1 + ao),
-          lat(use_lat(c_, Bh_)) {}
+          lat(use_lat(c_, Bh_)), quad(use_quad(c_, Bh_)) {}
     StepArgs args(uint32_t u, uint32_t i) const {
         const uint32_t k = c->p.k, n = c->p.n;
         StepArgs a;
@@ -395,12 +434,16 @@ struct StepChain {
         const bool first = (u == 0 && i == 0);
         const StepArgs a = args(u, i);
         // a null kernel must never reach hipLaunchKernelGGL (mkacc_create checks the set)
-        if (lat) {
+        if (quad) {
+            const void* fn = quad_fn((int)c->dg, c->method_class, first);
+            if (!fn) return false;
+            launch_ptr2(fn, dim3((unsigned)Bh), dim3(64 * quad::kWaves), quad::kLdsBytes, st, a, QuadArgs{c->d_qimg});
+        } else if (lat) {
             const bool split = use_latd(c, Bh);
             const void* fn = split ? latd_fn((int)c->dg, c->method_class, first) : lat_fn((int)c->dg, c->method_class, first);
             if (!fn) return false;
             const uint32_t waves = split ? kLatdWaves : k;
-            launch_ptr(fn, dim3((unsigned)Bh), dim3(64 * waves), lat_lds_bytes(waves), st, a);
+            launch_ptr(fn, dim3((unsigned)Bh), dim3(64 * waves), split ? latd_lds_bytes() : lat_lds_bytes(waves), st, a);
         } else {
             const void* fn = step_fn((int)c->dg, c->method_class, first, !first && use_dscr(c), c->step_ver);
             if (!fn) return false;
@@ -419,8 +462,10 @@ struct StepChain {
     bool run(uint32_t t0, uint32_t t1) {
         const uint32_t n = c->p.n;
         const bool split = use_latd(c, Bh);
-        const uint32_t waves = split ? kLatdWaves : c->p.k;
-        const void* fn = split ? latdrun_fn((int)c->dg, c->method_class) : latrun_fn((int)c->dg, c->method_class);
+        const uint32_t waves = quad ? quad::kWaves : split ? kLatdWaves : c->p.k;
+        const void* fn = quad    ? quadrun_fn((int)c->dg, c->method_class)
+                         : split ? latdrun_fn((int)c->dg, c->method_class)
+                                 : latrun_fn((int)c->dg, c->method_class);
         if (!fn || t0 == 0 || t0 >= t1) return false;
         const StepArgs a = args(t0 / n, t0 % n);
         LatdRun r;
@@ -434,7 +479,11 @@ struct StepChain {
         r.t0 = t0;
         r.t1 = t1;
         r.key2off = c->nk == 2 ? (uint32_t)(c->dg * 2 * kN) : 0u;
-        launch_ptr2(fn, dim3((unsigned)Bh), dim3(64 * waves), lat_lds_bytes(waves), st, a, r);
+        if (quad)
+            launch_ptr3(fn, dim3((unsigned)Bh), dim3(64 * waves), quad::kLdsBytes, st, a, r, QuadArgs{c->d_qimg});
+        else
+            launch_ptr2(fn, dim3((unsigned)Bh), dim3(64 * waves), split ? latd_lds_bytes() : lat_lds_bytes(waves), st, a,
+                        r);
         if ((t1 - t0) & 1u) std::swap(cur, nxt);
         return true;
     }
@@ -445,10 +494,18 @@ struct StepChain {
 // split-digit kernel (mk_latd_run_kernel: -9 % at B = 1, -22 % at B = 256,
 // profiles/r5/ab_latd_run_v24.txt) and those of the one-wave-per-party kernel whose
 // k B waves are resident at once at k <= 4 (mk_lat_run_kernel, ab_lat_run_v25.txt).
+// Residency counts whole workgroups: a CU holds 4 SIMDs x lat_run_occ waves of the
+// loop's register budget, i.e. floor(4 occ / k) workgroups of k waves, and no more
+// than its LDS allows (k = 5..7 fit once per CU, not 8 occ / k times).
 bool use_run(const mkacc_ctx* c, size_t B) {
     const size_t k = c->p.k;
-    if (!use_lat(c, B) || k * c->p.n < 2) return false;
-    return use_latd(c, B) || (k <= lat_run_max_k(c->dg) && k * B <= (size_t)c->cus * 4 * lat_run_occ(c->dg));
+    if (k * c->p.n < 2) return false;
+    if (use_quad(c, B)) return true;
+    if (!use_lat(c, B)) return false;
+    if (use_latd(c, B)) return true;
+    if (k > lat_run_max_k(c->dg)) return false;
+    const size_t wgs = std::min<size_t>(4 * lat_run_occ(c->dg) / k, kLdsPerCu / lat_lds_bytes((uint32_t)k));
+    return wgs > 0 && B <= (size_t)c->cus * wgs;
 }
 
 // Joins the slice streams a batch forked from the context stream back into it on
@@ -1273,6 +1330,10 @@ int mkacc_create(const mkacc_params* pin, int device, mkacc_ctx** out) {
             c->cus = ncu;
     }
     c->method_class = p.method == MKACC_METHOD_MKNTRU ? XZW : XZW_B;
+    c->env_lat = env_switch("MKACC_LAT");
+    c->env_latd = env_switch("MKACC_LATD");
+    c->env_dscr = env_switch("MKACC_DSCR");
+    c->env_quad = env_switch("MKACC_QUAD");
     c->dg = dg;
     c->step_ver = step_version((int)dg);
     c->nk = c->method_class == XZW ? 2 : 1;
@@ -1378,6 +1439,15 @@ int mkacc_create(const mkacc_params* pin, int device, mkacc_ctx** out) {
             img[kPsm1Off + psi_pos(e)] = pair((pw[e] + Q - 1) % Q);
         }
     }
+    // mk_quad_kernel tables (mkacc_quad.hpp): TF = the forward table, TI[2^b + t] =
+    // psi^-(t 2^(11-b)) for every bit b (negated pairs), TW[i] = psi^-i
+    std::vector<uint2> qimg(3 * kN, make_uint2(0, 0));
+    for (int i = 0; i < kN; ++i) qimg[i] = htf[i];
+    for (int b = 0; b < kLogN; ++b)
+        for (int t = 0; t < (1 << b); ++t) qimg[kN + (1 << b) + t] = npair(pwi[(size_t)t << (11 - b)]);
+    for (int i = 0; i < kN; ++i) qimg[2 * kN + i] = pair(pwi[i]);
+    HIP_TRY(hipMalloc(&c->d_qimg, qimg.size() * sizeof(uint2)));
+    HIP_TRY(hipMemcpy(c->d_qimg, qimg.data(), qimg.size() * sizeof(uint2), hipMemcpyHostToDevice));
     HIP_TRY(hipMalloc(&c->d_img, img.size() * sizeof(uint2)));
     HIP_TRY(hipMemcpy(c->d_twf, htf.data(), htf.size() * sizeof(uint2), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->d_twi, hti.data(), hti.size() * sizeof(uint2), hipMemcpyHostToDevice));
@@ -1390,7 +1460,7 @@ void mkacc_destroy(mkacc_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (void* p : {(void*)c->d_twf, (void*)c->d_twi, (void*)c->d_img, (void*)c->d_keys, (void*)c->d_pkey,
+    for (void* p : {(void*)c->d_twf, (void*)c->d_twi, (void*)c->d_img, (void*)c->d_qimg, (void*)c->d_keys, (void*)c->d_pkey,
                     (void*)c->d_acc0, (void*)c->d_acc1, (void*)c->d_cvals, (void*)c->d_dscr, (void*)c->d_ct,
                     (void*)c->d_io, (void*)c->d_ksk, (void*)c->d_lweA, (void*)c->d_lweB, (void*)c->d_tv,
                     (void*)c->d_digits, (void*)c->d_bh, (void*)c->d_gin, (void*)c->d_gout, (void*)c->d_wtwf,
@@ -1446,7 +1516,13 @@ const char* mkacc_step_kernel_name(const mkacc_ctx* c, size_t B) {
     if (!c) return "";
     if (c->wide)
         return c->wfp ? "widereg2::step_kernel" : "wide::step_kernel";
-    if (use_lat(c, B)) return use_latd(c, B) ? "mk_latd_kernel" : "mk_lat_kernel";
+    // small batches: the kernel that runs the steps after the first (all but one of
+    // the k n steps; the first is one launch of mk_latd_kernel / mk_lat_kernel)
+    if (use_quad(c, B)) return use_run(c, B) ? "mk_quad_run_kernel" : "mk_quad_kernel";
+    if (use_lat(c, B)) {
+        if (use_run(c, B)) return use_latd(c, B) ? "mk_latd_run_kernel" : "mk_lat_run_kernel";
+        return use_latd(c, B) ? "mk_latd_kernel" : "mk_lat_kernel";
+    }
     return c->step_ver == 2 ? "mk_step2_kernel" : "mk_step_kernel";
 }
 int mkacc_is_wide(const mkacc_ctx* c) { return c && c->wide ? (c->wfp ? 2 : 1) : 0; }

@@ -267,7 +267,9 @@ struct StepRes {
 // (Bounds::kAccInSum at dg = 4): acc_u is read again at digit 0, shortly after the
 // rotation read, instead of after the last digit (+3.4 % at config 4,
 // profiles/r4/ab_c4_canon.txt; the index party's pass too measured the same, run v36).
-template <int DG, int METHOD, bool FIRST, bool START, int DS = 0, bool CANON = false>
+// PF >= 0 overrides the prefetch depth (the small-batch kernels: one wave per SIMD,
+// register file to spare, every key group an exposed L2 / HBM latency).
+template <int DG, int METHOD, bool FIRST, bool START, int DS = 0, bool CANON = false, int PF = -1>
 struct DigitMac {
     using Bd = Bounds<DG, METHOD, FIRST, CANON>;
     static_assert(DS == 0 || (METHOD == XZW && !FIRST), "d_i scratch: XZW steps after the first");
@@ -277,7 +279,8 @@ struct DigitMac {
     // a d_i reload comes from HBM and frees the k2 / psi registers: prefetched
     // 3 groups ahead at DG <= 3, 2 at DG >= 4 (3 spill 10 VGPRs there); 1 group measured
     // 1-4% slower (profiles/r2/ab_dscr.txt)
-    static constexpr int kPrefetch = DS == 2 ? (DG <= 3 ? 3 : 2) : Prefetch<DG>::value;
+    static constexpr int kPrefetch = PF >= 0 ? PF : DS == 2 ? (DG <= 3 ? 3 : 2) : Prefetch<DG>::value;
+    static_assert(kPrefetch < 8, "a MAC streams 8 key groups");
     static constexpr int kBuf = kPrefetch + 1;
     const StepRes& sr;
     uint32_t koff, poff, aoff, doff;
@@ -328,14 +331,14 @@ struct DigitMac {
 
 // w += h * f_i                                  (xzw.cpp:281-288)
 // (first step, and XZW_B: f-words reduced to canonical, Bounds' f-part bound)
-template <int DG, int METHOD, bool FIRST>
+template <int DG, int METHOD, bool FIRST, int PF = -1>
 __device__ __forceinline__ void mac_index(const uint32_t (&h)[kRegs], int i, uint64_t (&w)[kRegs],
                                           __amdgpu_buffer_rsrc_t rk1, __amdgpu_buffer_rsrc_t rk2,
                                           __amdgpu_buffer_rsrc_t rks, const uint2* psi, const Mono& mp,
                                           const Mono& mn, uint32_t vo, uint32_t Q) {
     const uint32_t polyB = kN * 4u;
     const uint32_t koff = (uint32_t)(2 * i + 1) * polyB;
-    constexpr int kPrefetch = Prefetch<DG>::value;
+    constexpr int kPrefetch = PF >= 0 ? PF : Prefetch<DG>::value;
     KeyGroup kg[kPrefetch + 1];
     auto issue = [&](KeyGroup& t, int gq) {
         const uint32_t go = gq * 1024u;
@@ -364,9 +367,9 @@ __device__ __forceinline__ void mac_index(const uint32_t (&h)[kRegs], int i, uin
 //   sum_i h_i f_i = sum_i h_i (ev1 + ev2)'_i + (X^(N-c) - 1) sum_i h_i ev2'_i
 // two lazy sums per slot here and ONE monomial product per slot after the last
 // digit (step_body) instead of one per slot and digit.
-template <int DG>
+template <int DG, int PF = -1>
 struct SplitMac {
-    static constexpr int kPrefetch = Prefetch<DG>::value;
+    static constexpr int kPrefetch = PF >= 0 ? PF : Prefetch<DG>::value;
     static constexpr int kBuf = kPrefetch + 1;
     const StepRes& sr;
     uint32_t koff;
@@ -750,6 +753,66 @@ __device__ __forceinline__ void f_part(const StepCtx& s, uint32_t index, uint64_
 // wave and added through LDS.  Critical path: iNTT + ceil(dg / 2) digit NTTs, then
 // iNTT + one digit NTT.  Sums exact mod Q, so bit-exact like the other kernels.
 constexpr uint32_t kLatdWaves = 4;
+// Latency switches of the split-digit kernel (one wave per SIMD: the wave's own
+// memory latency is exposed, not hidden by other waves):
+//   MKACC_LATD_PFD    key groups a MAC streams ahead (-1: the batch kernels' depth)
+//   MKACC_LATD_KPF    1: the waves the f-part leaves idle pull the next step's key
+//                     block into L2 while it runs (mk_latd_run_kernel)
+//   MKACC_LATD_TWLDS  1: the per-lane NTT twiddles of both directions in LDS
+//                     (the batch kernels read them from L1/L2 behind other waves)
+#ifndef MKACC_LATD_PFD
+#define MKACC_LATD_PFD -1
+#endif
+#ifndef MKACC_LATD_KPF
+#define MKACC_LATD_KPF 0
+#endif
+#ifndef MKACC_LATD_TWLDS
+#define MKACC_LATD_TWLDS 0
+#endif
+constexpr int kLatdPfd = MKACC_LATD_PFD;
+// LDS: [forward + inverse per-lane twiddle image][psi^e - 1][4 transpose scratches]
+// with MKACC_LATD_TWLDS, else the batch kernels' [stage-10 twiddles][psi^e - 1][...]
+constexpr int kLatdImgPairs = kTwlPairs + kInvImgPairs;   // image pairs [0, kLatdImgPairs): both directions
+constexpr int kLatdTabWords = MKACC_LATD_TWLDS ? 2 * (kLatdImgPairs + kPsiPairs) : kLdsTabWords;
+constexpr size_t latd_lds_bytes() { return (size_t)(kLatdTabWords + kLatdWaves * kLdsWords) * 4; }
+static_assert(latd_lds_bytes() <= 160 * 1024, "one split-digit workgroup per CU");
+static_assert(kLatdImgPairs % 2 == 0 && kLatdImgPairs == kPsiOff, "both directions' images are contiguous, dwordx4 copy");
+__device__ __forceinline__ void load_image_latd(uint32_t* smem, const uint32_t* img) {
+    if constexpr (MKACC_LATD_TWLDS) {
+        const uint4* src = reinterpret_cast<const uint4*>(img);
+        uint4* dst = reinterpret_cast<uint4*>(smem);
+        for (int i = threadIdx.x; i < kLatdImgPairs / 2; i += blockDim.x) dst[i] = src[i];
+        for (int i = threadIdx.x; i < kN; i += blockDim.x) dst[kLatdImgPairs / 2 + i] = src[kPsm1Off / 2 + i];
+        __syncthreads();
+    } else {
+        load_image(smem, img);
+    }
+}
+__device__ __forceinline__ Tables tables_latd(uint32_t* smem, const uint32_t* img) {
+    if constexpr (MKACC_LATD_TWLDS) {
+        const uint2* t = reinterpret_cast<const uint2*>(smem);
+        return Tables{t, t + kTwlPairs, t + kTwlC, t + kLatdImgPairs};
+    } else {
+        return tables(smem, img);
+    }
+}
+// Pull [p, p + BYTES) into L2: one dword per 64-byte line, PARTS waves sharing the
+// lines.  The loads are consumed only by an empty asm, so the wave waits for them
+// once, at its next barrier, and nothing else waits behind them.
+template <uint32_t BYTES, uint32_t PARTS>
+__device__ __forceinline__ void l2_touch(const uint32_t* p, uint32_t part, uint32_t l) {
+    constexpr uint32_t kChunks = BYTES / 4096u;   // 64 lanes x 64 B per load
+    static_assert(BYTES % 4096u == 0, "whole chunks");
+    constexpr uint32_t kPer = (kChunks + PARTS - 1) / PARTS;
+    const __amdgpu_buffer_rsrc_t r = make_rsrc(p, BYTES);   // a chunk past the end loads 0, no access
+    uint32_t v[kPer];
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; ++j) v[j] = __builtin_amdgcn_raw_buffer_load_b32(r, l * 64u, (j * PARTS + part) * 4096u, 0);
+    uint32_t acc = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; ++j) acc |= v[j];
+    asm volatile("" ::"v"(acc));
+}
 // digits [d0, d1) of party u: uj (its partial party sum, from acc_u * 2^32 at digit 0
 // when the bound allows) and sv (its share of sumV) as lazy 64-bit sums
 template <int DG, int METHOD, bool FIRST>
@@ -789,13 +852,13 @@ __device__ __forceinline__ void party_digits(const StepCtx& s, uint32_t u, uint3
         digit_range<DG>(x, Q);
         vcc_fence();   // the digit-0 branch follows the last butterflies
         if (i == 0) {
-            const DigitMac<DG, METHOD, FIRST, true> mac(sr, 0, u);
+            const DigitMac<DG, METHOD, FIRST, true, 0, false, kLatdPfd> mac(sr, 0, u);
             KeyGroup kg[mac.kBuf];
 #pragma unroll
             for (int j = 0; j < mac.kPrefetch; ++j) mac.issue(kg[j], j);
             mac.run(x, uj, sv, kg);
         } else {
-            const DigitMac<DG, METHOD, FIRST, false> mac(sr, (int)i, u);
+            const DigitMac<DG, METHOD, FIRST, false, 0, false, kLatdPfd> mac(sr, (int)i, u);
             KeyGroup kg[mac.kBuf];
 #pragma unroll
             for (int j = 0; j < mac.kPrefetch; ++j) mac.issue(kg[j], j);
@@ -829,13 +892,13 @@ __device__ __forceinline__ void f_digit(const StepCtx& s, uint32_t f, uint64_t (
     if constexpr (kSplit) {
 #pragma unroll
         for (int r = 0; r < kRegs; ++r) w2[r] = 0;
-        const SplitMac<DG> mac(sr, (int)f);
+        const SplitMac<DG, kLatdPfd> mac(sr, (int)f);
         KeyGroup kg[mac.kBuf];
 #pragma unroll
         for (int j = 0; j < mac.kPrefetch; ++j) mac.issue(kg[j], j);
         mac.run(x, w, w2, kg);
     } else {
-        mac_index<DG, METHOD, FIRST>(x, (int)f, w, s.rk1, s.rk2, s.rks, s.tb.psi, s.mp, s.mn, s.vo, Q);
+        mac_index<DG, METHOD, FIRST, kLatdPfd>(x, (int)f, w, s.rk1, s.rk2, s.rks, s.tb.psi, s.mp, s.mn, s.vo, Q);
     }
     uint2 mw[kSplit ? kRegs : 1];
     if constexpr (kSplit) {
@@ -853,8 +916,10 @@ __device__ __forceinline__ void f_digit(const StepCtx& s, uint32_t f, uint64_t (
     }
 }
 
+// pf: the next step's key block (the run kernel), pulled into L2 by the waves the
+// f-part leaves idle (MKACC_LATD_KPF); null for none
 template <int DG, int METHOD, bool FIRST>
-__device__ __forceinline__ void latd_step(const StepArgs a, uint32_t* smem) {
+__device__ __forceinline__ void latd_step(const StepArgs a, uint32_t* smem, const uint32_t* pf = nullptr) {
     using Bd = Bounds<DG, METHOD, FIRST>;
     const uint32_t l = threadIdx.x & 63u;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // this wave
@@ -863,8 +928,8 @@ __device__ __forceinline__ void latd_step(const StepArgs a, uint32_t* smem) {
     const uint32_t cneg = (2u * kN - c) & (2u * kN - 1u);
     const uint32_t k = 2u, index = a.index;
     const uint32_t polyB = kN * 4u;
-    uint32_t* const scratch = smem + kLdsTabWords + wv * kLdsWords;
-    const StepCtx s{tables(smem, a.img),
+    uint32_t* const scratch = smem + kLatdTabWords + wv * kLdsWords;
+    const StepCtx s{tables_latd(smem, a.img),
                     scratch,
                     a.tw_fwd,
                     a.tw_inv,
@@ -899,7 +964,7 @@ __device__ __forceinline__ void latd_step(const StepArgs a, uint32_t* smem) {
     // others digits 1, 2, ... in wave order after it
     const uint32_t f = (wv + kLatdWaves - 2u * index) % kLatdWaves;
     if (half == 0) {
-        const uint32_t* o = smem + kLdsTabWords + (wv + 1u) * kLdsWords;
+        const uint32_t* o = smem + kLatdTabWords + (wv + 1u) * kLdsWords;
         uint32_t t4[kRegs];
 #pragma unroll
         for (int r = 0; r < kRegs; ++r) t4[r] = scratch[r * 64 + l] + o[r * 64 + l];   // < 4Q
@@ -940,7 +1005,7 @@ __device__ __forceinline__ void latd_step(const StepArgs a, uint32_t* smem) {
 #pragma unroll
     for (int r = 0; r < kRegs; ++r) {
         uint32_t v = 0;
-        for (uint32_t q = 0; q < kLatdWaves; ++q) v += smem[kLdsTabWords + q * kLdsWords + r * 64 + l];   // < 8Q
+        for (uint32_t q = 0; q < kLatdWaves; ++q) v += smem[kLatdTabWords + q * kLdsWords + r * 64 + l];   // < 8Q
         v = min(v, v - 4u * Q);
         x[r] = min(v, v - 2u * Q);                                                      // [0, 2Q)
     }
@@ -948,6 +1013,9 @@ __device__ __forceinline__ void latd_step(const StepArgs a, uint32_t* smem) {
     // (3) f-part digit f on waves f < DG, then acc'[index] = the sum of their shares
     if (f < DG) f_digit<DG, METHOD, FIRST>(s, f, w, x);
     vcc_fence();
+    if constexpr (MKACC_LATD_KPF && DG < (int)kLatdWaves) {
+        if (f >= DG && pf) l2_touch<(METHOD == XZW ? 2u : 1u) * DG * 2u * kN * 4u, kLatdWaves - DG>(pf, f - DG, l);
+    }
     if (f < DG) {
 #pragma unroll
         for (int r = 0; r < kRegs; ++r) scratch[r * 64 + l] = x[r];
@@ -959,7 +1027,7 @@ __device__ __forceinline__ void latd_step(const StepArgs a, uint32_t* smem) {
         uint32_t v = 0;
         for (uint32_t q = 0; q < kLatdWaves; ++q) {
             const uint32_t fq = (q + kLatdWaves - 2u * index) % kLatdWaves;
-            if (fq < DG) v += smem[kLdsTabWords + q * kLdsWords + r * 64 + l];               // < 2 DG Q <= 8Q
+            if (fq < DG) v += smem[kLatdTabWords + q * kLdsWords + r * 64 + l];              // < 2 DG Q <= 8Q
         }
         v = min(v, v - 4u * Q);
         x[r] = min(v, v - 2u * Q);
@@ -972,7 +1040,7 @@ __device__ __forceinline__ void latd_step(const StepArgs a, uint32_t* smem) {
 template <int DG, int METHOD, bool FIRST>
 __global__ __launch_bounds__(64 * kLatdWaves, 1) void mk_latd_kernel(StepArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    load_image(smem, a.img);
+    load_image_latd(smem, a.img);
     latd_step<DG, METHOD, FIRST>(a, smem);
 }
 
@@ -990,11 +1058,16 @@ struct LatdRun {
     uint64_t kbw;           // words per key block
     uint32_t cstride, n, t0, t1, key2off;
 };
+// key block of step t
+__device__ __forceinline__ const uint32_t* run_keys(const LatdRun& r, uint32_t t) {
+    const uint32_t u = t / r.n, i = t - u * r.n;
+    return r.keys + ((uint64_t)u * (r.n + 1) + i) * r.kbw;
+}
 // step t's arguments from the launch's first-step arguments
 __device__ __forceinline__ StepArgs run_args(const StepArgs& a, const LatdRun& r, uint32_t t) {
-    const uint32_t u = t / r.n, i = t - u * r.n;
+    const uint32_t u = t / r.n;
     StepArgs b = a;
-    b.key1 = r.keys + ((uint64_t)u * (r.n + 1) + i) * r.kbw;
+    b.key1 = run_keys(r, t);
     b.key2 = b.key1 + r.key2off;
     b.cvals = r.cvals + (uint64_t)t * r.cstride;
     b.index = u;
@@ -1006,10 +1079,10 @@ __device__ __forceinline__ StepArgs run_args(const StepArgs& a, const LatdRun& r
 template <int DG, int METHOD>
 __global__ __launch_bounds__(64 * kLatdWaves, 1) void mk_latd_run_kernel(StepArgs a, LatdRun r) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    load_image(smem, a.img);
+    load_image_latd(smem, a.img);
 #pragma unroll 1
     for (uint32_t t = r.t0; t < r.t1; ++t) {
-        latd_step<DG, METHOD, false>(run_args(a, r, t), smem);
+        latd_step<DG, METHOD, false>(run_args(a, r, t), smem, t + 1 < r.t1 ? run_keys(r, t + 1) : nullptr);
         vcc_fence();   // the loop branch follows the step's last reductions
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -1177,6 +1250,7 @@ StepFn pick_step(int method, bool first, bool dscr) {
 
 #include "mkacc_step2.hpp"
 #include "mkacc_layout2.hpp"
+#include "mkacc_quad.hpp"
 
 template <int DG, bool FIRST>
 StepFn pick_step2(int method) {
@@ -1228,6 +1302,14 @@ MKACC_TU_API KernelPtr latdrun_dg4(int method);
 MKACC_TU_API KernelPtr latrun_dg2(int method);    // mk_lat_run_kernel (the later steps in one launch)
 MKACC_TU_API KernelPtr latrun_dg3(int method);
 MKACC_TU_API KernelPtr latrun_dg4(int method);
+MKACC_TU_API KernelPtr quad_dg2(int method, bool first);   // mk_quad_kernel (a gate per workgroup, quarter polynomials)
+MKACC_TU_API KernelPtr quad_dg3(int method, bool first);
+MKACC_TU_API KernelPtr quad_dg4(int method, bool first);
+MKACC_TU_API KernelPtr quad_dg5(int method, bool first);
+MKACC_TU_API KernelPtr quadrun_dg2(int method);            // mk_quad_run_kernel (the later steps in one launch)
+MKACC_TU_API KernelPtr quadrun_dg3(int method);
+MKACC_TU_API KernelPtr quadrun_dg4(int method);
+MKACC_TU_API KernelPtr quadrun_dg5(int method);
 MKACC_TU_API KernelPtr wide_step(int method, bool first);     // mkacc_wide.hpp (integer 64-bit words)
 MKACC_TU_API KernelPtr widereg2_step(int method, bool first);  // mkacc_widereg2.hpp (FP64, Q < 2^50)
 }  // namespace mkacc_tu

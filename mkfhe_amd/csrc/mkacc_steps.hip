@@ -4,6 +4,7 @@
 //   -DMKACC_TU_DG=d -DMKACC_TU_PART=1   mk_lat_kernel instantiations of digit count d (2..4)
 //   -DMKACC_TU_DG=d -DMKACC_TU_PART=2   mk_step2_kernel instantiations of digit count d (2, 3), later steps
 //   -DMKACC_TU_DG=d -DMKACC_TU_PART=3   the same kernel's first (KDM) step
+//   -DMKACC_TU_DG=d -DMKACC_TU_PART=4   mk_quad_kernel / mk_quad_run_kernel of digit count d (2..5)
 //   -DMKACC_TU_WIDE=1 / 2               64-bit word step kernels (integer / FP64 register-resident)
 // and the host unit (mkacc_engine.hip) launches them through mkacc_tu.
 #include "mkacc_kernels.hpp"
@@ -48,6 +49,9 @@ KernelPtr MKACC_CAT(latdrun_dg, MKACC_TU_DG)(int method) { return pick_latd_run<
 KernelPtr MKACC_CAT(latrun_dg, MKACC_TU_DG)(int method) { return pick_lat_run<MKACC_TU_DG>(method); }
 #elif MKACC_TU_PART == 2
 KernelPtr MKACC_CAT(step2_dg, MKACC_TU_DG)(int method) { return (KernelPtr)pick_step2<MKACC_TU_DG, false>(method); }
+#elif MKACC_TU_PART == 4
+KernelPtr MKACC_CAT(quad_dg, MKACC_TU_DG)(int method, bool first) { return pick_quad<MKACC_TU_DG>(method, first); }
+KernelPtr MKACC_CAT(quadrun_dg, MKACC_TU_DG)(int method) { return pick_quad_run<MKACC_TU_DG>(method); }
 #else
 KernelPtr MKACC_CAT(step2f_dg, MKACC_TU_DG)(int method) { return (KernelPtr)pick_step2<MKACC_TU_DG, true>(method); }
 #endif

@@ -22,6 +22,7 @@
 #include <random>
 #include <stdexcept>
 #include <string>
+#include <sys/types.h>
 #include <thread>
 #include <vector>
 
@@ -1088,13 +1089,48 @@ void unpack_params(const uint64_t (&w)[kParamWords], mkkg_params& p) {
 
 struct File {
     FILE* f = nullptr;
-    explicit File(const char* path, const char* mode) : f(path ? std::fopen(path, mode) : nullptr) {}
+    uint64_t size = 0;   // bytes, for reads: every size a file supplies is checked against it
+    explicit File(const char* path, const char* mode) : f(path ? std::fopen(path, mode) : nullptr) {
+        if (f && mode[0] == 'r') {
+            if (fseeko(f, 0, SEEK_END) == 0) {
+                const off_t e = ftello(f);
+                size = e > 0 ? (uint64_t)e : 0;
+            }
+            if (fseeko(f, 0, SEEK_SET) != 0) {
+                std::fclose(f);
+                f = nullptr;
+            }
+        }
+    }
     ~File() {
         if (f) std::fclose(f);
     }
+    File(const File&) = delete;
+    File& operator=(const File&) = delete;
     bool get(void* p, size_t n) { return std::fread(p, 1, n, f) == n; }
     bool put(const void* p, size_t n) { return std::fwrite(p, 1, n, f) == n; }
+    // bytes left after the current position
+    uint64_t left() const {
+        const off_t at = ftello(f);
+        return at < 0 || (uint64_t)at > size ? 0 : size - (uint64_t)at;
+    }
 };
+
+constexpr uint64_t kSectionHead = 16 + 8;   // name, words
+constexpr uint64_t kSectionTail = 8;        // checksum
+
+// A parameter block must describe a context this library can serve (the checks
+// of every key routine, unpack) before any reader sizes a buffer from it.
+int check_file_params(const mkkg_params& p, uint32_t kind) {
+    if (kind < MKKG_FILE_MNTRU_SK || kind > MKKG_FILE_CIPHERTEXT) return fail(MKACC_E_ARG, "unknown key file kind");
+    if (p.acc.k > 1024 || p.acc.n > (1u << 16) || p.acc.N > (1u << 16))
+        return fail(MKACC_E_ARG, "key file parameter block out of range");
+    for (double d : {p.sigma, p.sigma_unienc, p.sigma_r})
+        if (!std::isfinite(d) || d < 0 || d > 1e9) return fail(MKACC_E_ARG, "key file parameter block: bad sigma");
+    P chk;
+    if (unpack(&p, chk)) return fail(MKACC_E_ARG, "key file parameter block is not a valid MK parameter set");
+    return MKACC_OK;
+}
 
 // header; leaves the file positioned at the first section
 int read_header(File& fl, uint32_t* kind, mkkg_params* p, uint32_t* count) {
@@ -1105,13 +1141,18 @@ int read_header(File& fl, uint32_t* kind, mkkg_params* p, uint32_t* count) {
     if (!fl.get(magic, 8) || std::memcmp(magic, kMagic, 8)) return fail(MKACC_E_ARG, "not an MKFHEKEY file");
     if (!fl.get(&ver, 4) || ver != kFileVersion) return fail(MKACC_E_ARG, "unsupported key file version");
     if (!fl.get(&knd, 4) || !fl.get(w, sizeof(w)) || !fl.get(&cnt, 4)) return fail(MKACC_E_ARG, "truncated key file");
+    mkkg_params prm;
+    unpack_params(w, prm);
+    if (int rc = check_file_params(prm, knd)) return rc;
+    if (cnt > fl.left() / (kSectionHead + kSectionTail)) return fail(MKACC_E_ARG, "truncated key file (section count)");
     if (kind) *kind = knd;
-    if (p) unpack_params(w, *p);
+    if (p) *p = prm;
     if (count) *count = cnt;
     return MKACC_OK;
 }
 
-// find section `name`; on success the file is positioned at its data and *words is set
+// find section `name`; on success the file is positioned at its data and *words is
+// set, bounded by the bytes the file still holds (data + checksum)
 int seek_section(File& fl, const char* name, uint64_t* words) {
     uint32_t count = 0;
     int rc = read_header(fl, nullptr, nullptr, &count);
@@ -1120,11 +1161,14 @@ int seek_section(File& fl, const char* name, uint64_t* words) {
         char nm[16];
         uint64_t w = 0;
         if (!fl.get(nm, 16) || !fl.get(&w, 8)) return fail(MKACC_E_ARG, "truncated key file");
+        const uint64_t left = fl.left();
+        if (left < kSectionTail || w > (left - kSectionTail) / 4)
+            return fail(MKACC_E_ARG, "truncated key file (section larger than the file)");
         if (!std::strncmp(nm, name, 16)) {
             *words = w;
             return MKACC_OK;
         }
-        if (std::fseek(fl.f, (long)(w * 4 + 8), SEEK_CUR)) return fail(MKACC_E_ARG, "truncated key file");
+        if (fseeko(fl.f, (off_t)(w * 4 + kSectionTail), SEEK_CUR)) return fail(MKACC_E_ARG, "truncated key file");
     }
     return fail(MKACC_E_ARG, std::string("key file has no section ") + name);
 }

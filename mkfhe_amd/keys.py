@@ -365,10 +365,19 @@ def file_info(path: str):
 
 
 def read_section(path: str, name: str, shape) -> np.ndarray | None:
+    """Section `name` as an array of `shape`; None only if the file has no such
+    section (optional ones, e.g. the other method's key-switching key).  A damaged
+    file (truncated, a size past its end, a bad parameter block) raises."""
     L = load()
     words = L.mkkg_file_section_words(os.fsencode(path), name.encode())
     if words == 0:
-        return None
+        rc = L.mkkg_file_read_section(os.fsencode(path), name.encode(), None, 0)
+        if rc == 0:
+            return np.empty(0, np.uint32).reshape(shape) if int(np.prod(shape)) == 0 else None
+        msg = L.mkkg_last_error().decode()
+        if "has no section" in msg:
+            return None
+        raise MkaccError(rc, msg)
     out = np.empty(int(np.prod(shape)), np.uint32)
     if out.size != words:
         raise MkaccError(-1, f"section {name}: {words} words, expected shape {shape}")

@@ -12,7 +12,10 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "build", "libmkfhe_oracle.so")
+_DEFAULT_LIB = os.path.join(_HERE, "build", "libmkfhe_oracle.so")
+# MKFHE_ORACLE_LIB: another build of the same source (the sanitizer build,
+# `make -C oracle asan`, tests/test_sanitize.py); used as is, never rebuilt here
+_LIB_PATH = os.environ.get("MKFHE_ORACLE_LIB") or _DEFAULT_LIB
 
 XZW = 0
 XZW_B = 1
@@ -40,6 +43,8 @@ def build() -> str:
     src = os.path.join(_HERE, "mkfhe_oracle.c")
 
     def stale():
+        if _LIB_PATH != _DEFAULT_LIB:
+            return False
         return (not os.path.exists(_LIB_PATH)) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src)
 
     if stale():

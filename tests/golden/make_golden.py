@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Generate tests/golden/*.json (committed fixtures; run here, never on the GPU box).
 
-  python tests/golden/make_golden.py [--kats-only | --big-batch]
+  python tests/golden/make_golden.py [--kats-only | --big-batch [mkntru|mklwe] | --gates-only]
 
 reference_kats.json
     Known-answer vectors held by the reference's own unit tests for the
@@ -14,9 +14,10 @@ evalacc_full.json
     MNTRU test-vector accumulator, run through the CPU oracle; stored as the
     SHA-256 of the little-endian uint64 output plus sample coefficients.
     The GPU tests regenerate the inputs from the seeds and compare digests.
-evalacc_b4096.json (--big-batch)
-    The bench's own shape: STD128_MKNTRU, full n, B = 4096 seeded gates in one
-    batch, whole-output SHA-256 and per-gate digests.
+evalacc_b4096.json (--big-batch mkntru), evalacc_b4096_mklwe.json (--big-batch mklwe)
+    The benched shapes: STD128_MKNTRU (headline) and STD100_MKNTRU_LWE_2
+    (config 3, MK-LWE k = 4), full n, B = 4096 seeded gates in one batch,
+    whole-output SHA-256 and per-gate digests.
 gates_realkeys.json (--gates-only regenerates just this file)
     NAND gates with real keys (seeded NTL-free key generation,
     mkfhe_amd/keys.py), evaluated by the oracle: digest of the output
@@ -191,26 +192,34 @@ def make_gates():
     return out
 
 
-# The bench shape itself: STD128_MKNTRU, full n, B = 4096 gates in one launch
-# grid (every wave slot of every workgroup, two rounds of the 2048 slots).
-BIG_BATCH = ("STD128_MKNTRU_B4096", pyoracle.XZW, 2, 765, 45181, 1 << 7, Q_MK, 4096, 8100)
+# The bench shapes themselves, full n, B = 4096 gates in one batch (every wave
+# slot of every workgroup, two rounds of the 2048 slots; the batch kernels cut it
+# into two slices on two streams): the headline's STD128_MKNTRU and config 3's
+# STD100_MKNTRU_LWE_2 (MK-LWE, k = 4, the XZW_B step kernel).
+# key: (name, method, k, n, q, baseG, Q, B, seed, fixture file)
+BIG_BATCHES = {
+    "mkntru": ("STD128_MKNTRU_B4096", pyoracle.XZW, 2, 765, 45181, 1 << 7, Q_MK, 4096, 8100, "evalacc_b4096.json"),
+    "mklwe": ("STD100_MKNTRU_LWE_2_B4096", pyoracle.XZW_B, 4, 500, 32749, 1 << 9, Q_MK, 4096, 8200,
+              "evalacc_b4096_mklwe.json"),
+}
+BIG_BATCH = BIG_BATCHES["mkntru"][:9]
 
 
-def big_batch_inputs(B=None):
-    name, method, k, n, q, baseG, Q, B0, seed = BIG_BATCH
+def big_batch_inputs(B=None, which="mkntru"):
+    name, method, k, n, q, baseG, Q, B0, seed, _ = BIG_BATCHES[which]
     return evalacc_inputs(method, k, n, q, baseG, Q, B or B0, seed)
 
 
-def make_big_batch():
-    """SHA-256 of the whole [4096][2][2048] output plus per-gate digests (so a
-    failure names the gates); ~20 CPU-minutes of oracle time."""
-    name, method, k, n, q, baseG, Q, B, seed = BIG_BATCH
-    orc, evk, pkey, ct, acc = big_batch_inputs()
+def make_big_batch(which="mkntru"):
+    """SHA-256 of the whole [4096][k][2048] output plus per-gate digests (so a
+    failure names the gates); 20-40 CPU-minutes of oracle time."""
+    name, method, k, n, q, baseG, Q, B, seed, _ = BIG_BATCHES[which]
+    orc, evk, pkey, ct, acc = big_batch_inputs(which=which)
     res = orc.evalacc_batch(evk, pkey, ct, acc, os.cpu_count() or 1)
     per_gate = [hashlib.sha256(np.ascontiguousarray(res[b], dtype="<u8").tobytes()).hexdigest()[:16]
                 for b in range(B)]
-    return {"name": name, "method": "XZW", "k": k, "n": n, "q": q, "baseG": baseG, "Q": Q, "B": B, "seed": seed,
-            "sha256": digest(res), "gate_sha256_16": per_gate}
+    return {"name": name, "method": "XZW" if method == pyoracle.XZW else "XZW_B", "k": k, "n": n, "q": q,
+            "baseG": baseG, "Q": Q, "B": B, "seed": seed, "sha256": digest(res), "gate_sha256_16": per_gate}
 
 
 def main():
@@ -219,7 +228,9 @@ def main():
     if "--kats-only" in sys.argv:
         return
     if "--big-batch" in sys.argv:
-        json.dump(make_big_batch(), open(os.path.join(HERE, "evalacc_b4096.json"), "w"))
+        i = sys.argv.index("--big-batch")
+        which = sys.argv[i + 1] if i + 1 < len(sys.argv) else "mkntru"
+        json.dump(make_big_batch(which), open(os.path.join(HERE, BIG_BATCHES[which][9]), "w"))
         return
     json.dump(make_gates(), open(os.path.join(HERE, "gates_realkeys.json"), "w"), indent=1)
     if "--gates-only" in sys.argv:

@@ -157,23 +157,28 @@ def test_mkntru_b_gate_is_rejected(mk):
         eng.eval_nand_mklwe(z, np.zeros(1, np.uint32), z + 1, np.zeros(1, np.uint32))
 
 
-def _big():
-    f = os.path.join(ROOT, "tests", "golden", "evalacc_b4096.json")
+def _big(fname):
+    f = os.path.join(ROOT, "tests", "golden", fname)
     return json.load(open(f)) if os.path.exists(f) else None
 
 
-def test_bench_shape_b4096_full_n(mk, oracle):
-    """STD128_MKNTRU, n = 765, B = 4096 in one batch (every wave slot of every
-    workgroup, two rounds of the chip's 2048 slots -- the launch bench.py times):
-    the whole output against the committed oracle digest, two runs identical."""
+@pytest.mark.parametrize("which", ["mkntru", "mklwe"])
+def test_bench_shape_b4096_full_n(mk, oracle, which):
+    """The benched shapes at full n, B = 4096 in one batch (every wave slot of every
+    workgroup, two rounds of the chip's 2048 slots, cut into two slices on two
+    streams -- the launches bench.py times): STD128_MKNTRU (headline, XZW, k = 2)
+    and STD100_MKNTRU_LWE_2 (config 3, XZW_B, k = 4).  The whole output against
+    the committed oracle digest, per gate, and two runs identical."""
     import hashlib
     import sys
     sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
     import make_golden
-    g = _big()
-    assert g is not None, "tests/golden/evalacc_b4096.json missing (make_golden.py --big-batch)"
-    orc, evk, pkey, ct, acc = make_golden.big_batch_inputs()
-    eng = _engine(mk, mk.MKNTRU, 2, 765, 45181, 1 << 7)
+    name, method, k, n, q, baseG, Q, B, seed, fname = make_golden.BIG_BATCHES[which]
+    g = _big(fname)
+    assert g is not None, f"tests/golden/{fname} missing (make_golden.py --big-batch {which})"
+    orc, evk, pkey, ct, acc = make_golden.big_batch_inputs(which=which)
+    eng = _engine(mk, mk.MKNTRU if method == oracle.XZW else mk.MKNTRU_LWE, k, n, q, baseG)
+    assert eng.step_kernel_name(B) == "mk_step2_kernel"
     eng.upload_keys(evk.astype(np.uint32), pkey.astype(np.uint32))
     r1 = eng.eval_batch(ct.astype(np.uint32), acc.astype(np.uint32))
     r2 = eng.eval_batch(ct.astype(np.uint32), acc.astype(np.uint32))

@@ -182,3 +182,67 @@ def test_gate_errors(mk_gpu, oracle):
     with pytest.raises(mk.MkaccError) as e:                 # ct word >= q
         eng.eval_nand_mntru(np.zeros((k, n), np.uint32), c1 + 45181, c2)
     assert e.value.code == -5
+
+
+# Whole gates at the batch size bench.py times: B = 4100 gates run as slices of the
+# batch step kernel (units of CUs x 4 = 1024 gates at 256 CUs) on 2 or 4 streams,
+# checked on both sides of every unit boundary.  MK-NTRU k = 2 (headline kernel,
+# dg = 3), MK-LWE k = 4 (config 3's XZW_B step2 kernel) and MK-NTRU k = 8 at dg = 4
+# (config 4's mk_step_kernel with the d_i scratch); short n keeps the oracle fast.
+BIG_GATES = [("mntru", 2, 3, 7, "2"), ("mntru", 2, 3, 7, "4"), ("mklwe", 4, 2, 9, "2"), ("mklwe", 4, 2, 9, "3"),
+             ("mntru", 8, 2, 6, "2")]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,k,n,logB,streams", BIG_GATES,
+                         ids=[f"{c[0]}-k{c[1]}-logB{c[3]}-s{c[4]}" for c in BIG_GATES])
+def test_nand_gate_big_batch_slices(mk_gpu, oracle, kind, k, n, logB, streams, monkeypatch):
+    mk = mk_gpu
+    monkeypatch.setenv("MKACC_STREAMS", streams)
+    B, baseKS = 4100, 32
+    pick = [0, 1, 1023, 1024, 2047, 2048, 2049, 3071, 3072, 4099]
+    seed = 500 + 10 * k + logB
+    if kind == "mntru":
+        q = qKS = 45181
+        orc, evk, pkey, _, _ = make_case(oracle, oracle.XZW, k, n, q, 1 << logB, 1, seed=seed)
+        dks = oracle.ks_digits(qKS, baseKS)
+        ksk = oracle.fill_uniform(k * N * dks * n, qKS, seed * 7 + 1).reshape(k, N * dks, n)
+        eng = mk.MKAccumulatorEngine(mk.make_params(mk.MKNTRU, k, n, N, Q_MK, q, 1 << logB))
+        assert eng.step_kernel_name(B) == ("mk_step2_kernel" if logB > 6 else "mk_step_kernel")
+        eng.upload_keys(evk.astype(np.uint32), pkey.astype(np.uint32))
+        eng.upload_ksk_mntru(ksk.astype(np.uint32), qKS, baseKS, n)
+        ct1 = oracle.fill_uniform(B * k * n, q, seed + 1).reshape(B, k, n)
+        ct2 = oracle.fill_uniform(B * k * n, q, seed + 2).reshape(B, k, n)
+        nand = oracle.fill_uniform(k * n, q, seed + 3).reshape(k, n)
+        ct1[1024, 0, 0], ct2[1024, 0, 0] = q - 1, q - 1
+        got = eng.eval_nand_mntru(nand.astype(np.uint32), ct1.astype(np.uint32), ct2.astype(np.uint32))
+        assert got.shape == (B, k, n)
+        heads = np.stack([oracle.mntru_head(nand, ct1[b], ct2[b], q) for b in pick])
+        acc0 = np.broadcast_to(orc.mntru_testvector(4), (len(pick), k, N)).copy()
+        acc = orc.evalacc_batch(evk, pkey, heads, acc0, 8)                 # BootstrapGateCore (:1072-1130)
+        for j, b in enumerate(pick):
+            exp = orc.mntru_tail_ksk1(acc[j], ksk, qKS, baseKS, n)
+            assert np.array_equal(got[b], exp.astype(np.uint32)), b
+    else:
+        q = qKS = 32749
+        orc, evk, pkey, _, _ = make_case(oracle, oracle.XZW_B, k, n, q, 1 << logB, 1, seed=seed)
+        dks = oracle.ks_digits(qKS, baseKS)
+        A = oracle.fill_uniform(k * N * baseKS * dks * n, qKS, seed * 7 + 2).reshape(k, N, baseKS, dks, n)
+        Bk = oracle.fill_uniform(k * N * baseKS * dks, qKS, seed * 7 + 3).reshape(k, N, baseKS, dks)
+        eng = mk.MKAccumulatorEngine(mk.make_params(mk.MKNTRU_LWE, k, n, N, Q_MK, q, 1 << logB))
+        assert eng.step_kernel_name(B) == "mk_step2_kernel"
+        eng.upload_keys(evk.astype(np.uint32), pkey.astype(np.uint32))
+        eng.upload_ksk_mklwe(A.astype(np.uint32), Bk.astype(np.uint32), qKS, baseKS, n)
+        a1 = oracle.fill_uniform(B * k * n, q, seed + 1).reshape(B, k, n)
+        a2 = oracle.fill_uniform(B * k * n, q, seed + 2).reshape(B, k, n)
+        b1 = oracle.fill_uniform(B, q, seed + 3)
+        b2 = oracle.fill_uniform(B, q, seed + 4)
+        a1[2048, 0, :2] = 0
+        a2[2048, 0, :2] = [0, q - 1]
+        got_a, got_b = eng.eval_nand_mklwe(a1, b1, a2, b2)
+        assert got_a.shape == (B, k, n) and got_b.shape == (B,)
+        heads = [orc.mklwe_head(a1[b], b1[b], a2[b], b2[b], q) for b in pick]
+        acc = orc.evalacc_batch(evk, pkey, np.stack([h[0] for h in heads]), np.stack([h[1] for h in heads]), 8)
+        for j, b in enumerate(pick):
+            ea, eb = orc.mklwe_tail(acc[j], A, Bk, qKS, baseKS, n)            # (:1004-1067), mklwe-pke.cpp:260-298
+            assert np.array_equal(got_a[b], ea.astype(np.uint32)) and int(got_b[b]) == eb, b

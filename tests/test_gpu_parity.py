@@ -80,6 +80,7 @@ CASES = [
     ("XZW", 8, 3, 45181, 1 << 6, 2),      # STD128_MKNTRU_3 shape (config 4): 8 parties, dg=4
     ("XZW_B", 3, 3, 32749, 1 << 6, 3),    # dg=4, binary keys
     ("XZW", 8, 2, 45181, 1 << 9, 2),      # STD100_MKNTRU_3 shape: 8 parties, dg=2
+    ("XZW_B", 6, 2, 32749, 1 << 9, 3),    # 6 parties, dg=2 (one-launch step loop at k = 5..8)
 ]
 
 
@@ -184,10 +185,11 @@ def test_evalacc_two_party_split_digit_kernel(mk, oracle, meth, logB, monkeypatc
     orc, evk, pkey, ct, acc = make_case(oracle, om, 2, 4, q, 1 << logB, B, seed=71 + logB)
     exp = orc.evalacc_batch(evk, pkey, ct, acc, 8).astype(np.uint32)
     outs = {}
-    for split, name in (("1", "mk_latd_kernel"), ("0", "mk_lat_kernel")):
+    for split, name in (("1", "mk_latd_run_kernel"), ("0", "mk_lat_run_kernel")):
         monkeypatch.setenv("MKACC_LATD", split)
         eng = mk.MKAccumulatorEngine(mk.make_params(em, 2, 4, 2048, Q_MK, q, 1 << logB))
-        assert eng.step_kernel_name(B) == name
+        monkeypatch.delenv("MKACC_LATD")            # read once, at context creation
+        assert eng.step_kernel_name(B) == name       # steps 1..kn-1 in one launch (step 0: its own)
         eng.upload_keys(evk.astype(np.uint32), pkey.astype(np.uint32))
         outs[split] = eng.eval_batch(ct.astype(np.uint32), acc.astype(np.uint32))
         assert np.array_equal(outs[split], exp), name
@@ -273,9 +275,11 @@ def test_evalacc_many_gates_every_wave_slot(mk, oracle, lat, monkeypatch):
         assert not bad, f"gates differing from the oracle: {bad[:16]}"
 
 
-# (k, n, log2 B_g): the headline kernel's shape (mk_step2_kernel, dg = 3) and the
-# config-4 kernel's (mk_step_kernel with its d_i scratch, k >= 4, dg = 4)
-SPLIT_SHAPES = {"step2-k2-dg3": (2, 3, 7), "dscr-k4-dg4": (4, 2, 6)}
+# (method, k, n, log2 B_g): the headline kernel's shape (mk_step2_kernel, dg = 3),
+# config 3's (the MK-LWE step2 kernel, XZW_B, k = 4, dg = 2) and the config-4
+# kernel's (mk_step_kernel with its d_i scratch, k >= 4, dg = 4)
+SPLIT_SHAPES = {"step2-k2-dg3": ("XZW", 2, 3, 7), "step2-mklwe-k4-dg2": ("XZW_B", 4, 2, 9),
+                "dscr-k4-dg4": ("XZW", 4, 2, 6)}
 
 
 @pytest.mark.parametrize("streams", ["2", "3", "4"])
@@ -285,18 +289,23 @@ def test_two_stream_batch_split(mk, oracle, shape, streams, monkeypatch):
     slices whose step launches run on streams of their own: the output equals the
     one-stream run word for word, and a spread sample across the slice boundaries
     equals the oracle.  B = 4100 (units of 1024 gates at 256 CUs): 2048 + 2052,
-    1024 + 1024 + 2052, 1024 x 3 + 1028.  Both default batch kernels: the config-4
-    one reads its per-gate d_i scratch at the slice's gate offset."""
-    k, n, logb = SPLIT_SHAPES[shape]
+    1024 + 1024 + 2052, 1024 x 3 + 1028.  Every default batch kernel: MK-NTRU and
+    MK-LWE step2 kernels, and the config-4 one, which reads its per-gate d_i scratch
+    at the slice's gate offset."""
+    meth, k, n, logb = SPLIT_SHAPES[shape]
     monkeypatch.setenv("MKACC_LAT", "0")
-    q, baseG, B = 45181, 1 << logb, 4100
-    orc, evk, pkey, ct, acc = make_case(oracle, oracle.XZW, k, n, q, baseG, B, seed=91 + k)
-    params = mk.make_params(mk.MKNTRU, k, n, 2048, Q_MK, q, baseG)
+    om = oracle.XZW if meth == "XZW" else oracle.XZW_B
+    q, baseG, B = (45181 if meth == "XZW" else 32749), 1 << logb, 4100
+    orc, evk, pkey, ct, acc = make_case(oracle, om, k, n, q, baseG, B, seed=91 + k + (meth == "XZW_B"))
+    # monomial edge exponents on both sides of every slice boundary
+    for g in (1023, 1024, 2047, 2048, 3071, 3072):
+        ct[g, 0, 0] = 0 if g % 2 else (q - 1 if om == oracle.XZW else 2 * 2048)
+    params = mk.make_params(mk.MKNTRU if meth == "XZW" else mk.MKNTRU_LWE, k, n, 2048, Q_MK, q, baseG)
     outs = {}
     for ns in ("1", streams):
         monkeypatch.setenv("MKACC_STREAMS", ns)
         eng = mk.MKAccumulatorEngine(params)
-        assert eng.step_kernel_name(B) == ("mk_step2_kernel" if k == 2 else "mk_step_kernel")
+        assert eng.step_kernel_name(B) == ("mk_step_kernel" if logb == 6 else "mk_step2_kernel")
         eng.upload_keys(evk.astype(np.uint32), pkey.astype(np.uint32))
         outs[ns] = eng.eval_batch(ct.astype(np.uint32), acc.astype(np.uint32))
         del eng
@@ -304,3 +313,73 @@ def test_two_stream_batch_split(mk, oracle, shape, streams, monkeypatch):
     pick = [0, 1, 1023, 1024, 2047, 2048, 3071, 3072, 4099]
     exp = orc.evalacc_batch(evk, pkey, ct[pick], acc[pick], 8)
     assert np.array_equal(outs[streams][pick], exp.astype(np.uint32))
+
+
+@pytest.mark.parametrize("k,B", [(5, 256), (6, 256), (3, 512)])
+def test_small_batch_run_kernel_at_its_residency_limit(mk, oracle, k, B, monkeypatch):
+    """mk_lat_run_kernel (the steps after the first in one launch) is taken only while
+    every gate's workgroup is resident at once: floor(4 occ / k) workgroups per CU,
+    capped by LDS -- at k = 5, 6 one per CU, so B = 256 on 256 CUs is the limit.  The
+    whole batch equals the oracle on a spread sample, the first and last gate
+    included."""
+    monkeypatch.delenv("MKACC_LAT", raising=False)
+    orc, evk, pkey, ct, acc = make_case(oracle, oracle.XZW, k, 2, 45181, 1 << 9, B, seed=300 + k)
+    eng = mk.MKAccumulatorEngine(mk.make_params(mk.MKNTRU, k, 2, 2048, Q_MK, 45181, 1 << 9))
+    import torch
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    if cus != 256:
+        pytest.skip(f"sized for 256 CUs, device has {cus}")
+    assert eng.step_kernel_name(B) == "mk_lat_run_kernel"
+    assert eng.step_kernel_name(B + 1) != "mk_lat_run_kernel"
+    eng.upload_keys(evk.astype(np.uint32), pkey.astype(np.uint32))
+    got = eng.eval_batch(ct.astype(np.uint32), acc.astype(np.uint32))
+    pick = [0, 1, B // 2, B - 2, B - 1]
+    exp = orc.evalacc_batch(evk, pkey, ct[pick], acc[pick], 8)
+    assert np.array_equal(got[pick], exp.astype(np.uint32))
+
+
+QUAD_CASES = [c for c in CASES]
+
+
+@pytest.mark.parametrize("case", QUAD_CASES,
+                         ids=[f"{c[0]}-k{c[1]}-n{c[2]}-logB{c[4].bit_length() - 1}" for c in QUAD_CASES])
+def test_evalacc_quad_kernel(mk, oracle, case, monkeypatch):
+    """mk_quad_kernel (one gate per workgroup, every polynomial spread over its four
+    waves, mkacc_quad.hpp; MKACC_QUAD=1) equals the oracle for both methods, k = 1..16,
+    dg = 2..5, with the monomial edge cases c = 0, 2N - 1 (and 2N for XZW_B): the first
+    step in its own launch, the others in one mk_quad_run_kernel launch."""
+    meth, k, n, q, baseG, B = case
+    monkeypatch.setenv("MKACC_QUAD", "1")
+    om = oracle.XZW if meth == "XZW" else oracle.XZW_B
+    em = mk.MKNTRU if meth == "XZW" else mk.MKNTRU_LWE
+    orc, evk, pkey, ct, acc = make_case(oracle, om, k, n, q, baseG, B + 2, seed=k * 41 + n)
+    ct[0, 0, 0] = 0
+    if om == oracle.XZW:
+        ct[-1, k - 1, n - 1] = q - 1
+    else:
+        ct[-1, k - 1, n - 1] = 4096
+        ct[0, 0, n - 1] = 4095
+    exp = orc.evalacc_batch(evk, pkey, ct, acc, 8)
+    eng = mk.MKAccumulatorEngine(mk.make_params(em, k, n, 2048, Q_MK, q, baseG))
+    assert eng.step_kernel_name(B + 2) == ("mk_quad_run_kernel" if k * n > 1 else "mk_quad_kernel")
+    eng.upload_keys(evk.astype(np.uint32), pkey.astype(np.uint32))
+    got = eng.eval_batch(ct.astype(np.uint32), acc.astype(np.uint32))
+    assert np.array_equal(got, exp.astype(np.uint32))
+
+
+@pytest.mark.parametrize("name,B", [("STD128_MKNTRU", 3), ("STD100_MKNTRU_LWE", 2), ("STD100_MKNTRU_LWE_2", 256)])
+def test_evalacc_quad_kernel_full_paramsets(mk, oracle, name, B, monkeypatch):
+    """The quad kernel at full n (1530 / 1000 / 2000 steps in one launch), up to one
+    gate per CU, against the oracle on a spread sample."""
+    monkeypatch.setenv("MKACC_QUAD", "1")
+    p = mk.paramset(name)
+    om = oracle.XZW if p.method == mk.MKNTRU else oracle.XZW_B
+    orc, evk, pkey, ct, acc = make_case(oracle, om, p.k, p.n, p.q, p.baseG, B, seed=p.n + B)
+    acc[:] = orc.mntru_testvector(4)
+    eng = mk.MKAccumulatorEngine(p)
+    assert eng.step_kernel_name(B) == "mk_quad_run_kernel"
+    eng.upload_keys(evk.astype(np.uint32), pkey.astype(np.uint32))
+    got = eng.eval_batch(ct.astype(np.uint32), acc.astype(np.uint32))
+    pick = sorted({0, B // 2, B - 1})
+    exp = orc.evalacc_batch(evk, pkey, ct[pick], acc[pick], 8)
+    assert np.array_equal(got[pick], exp.astype(np.uint32))

@@ -324,3 +324,44 @@ def test_key_file_rejects_corruption(lib, tmp_path):
         K.load_secret_key(f)
     with pytest.raises(Exception):
         K.load_btkey(str(tmp_path / "missing.mkfk"))
+
+
+def test_key_file_rejects_bad_sizes_and_params(lib, tmp_path):
+    """The reader bounds every file-supplied size by the bytes the file holds and
+    refuses a parameter block that is not a valid MK parameter set, before any
+    buffer is sized from it (the format is ours: the reference serialises no MK
+    key, binfhecontext-ser.h:10-24)."""
+    import struct
+    p = K.paramset("STD100_MKNTRU_LWE", 2)
+    sk = K.mklwe_keygen(p, 78)
+    f = str(tmp_path / "s.mkfk")
+    K.save_secret_key(f, p, sk)
+    good = bytes(open(f, "rb").read())
+    head = 8 + 4 + 4 + 18 * 8 + 4                        # magic, version, kind, params, count
+    assert good[head:head + 1] == b"s"                    # the first section: name, words, data
+
+    def bad(raw, match):
+        open(f, "wb").write(bytes(raw))
+        with pytest.raises(Exception, match=match):
+            K.load_secret_key(f)
+
+    bad(good[:len(good) // 2], "truncated")               # cut inside the data
+    bad(good[:head + 10], "truncated")                    # cut inside a section header
+    raw = bytearray(good)
+    raw[head + 16:head + 24] = struct.pack("<Q", 1 << 62)  # section words far past the end
+    bad(raw, "larger than the file")
+    raw = bytearray(good)
+    raw[head + 16:head + 24] = struct.pack("<Q", (len(good) - head) // 4)   # one word too many
+    bad(raw, "larger than the file")
+    raw = bytearray(good)
+    raw[head - 4:head] = struct.pack("<I", 0xFFFFFFFF)    # section count
+    bad(raw, "section count")
+    raw = bytearray(good)
+    raw[12:16] = struct.pack("<I", 77)                    # kind
+    bad(raw, "kind")
+    for word, value in ((3, 3), (4, 4), (1, 1 << 20), (6, 3), (12, 0x7FF8000000000000)):   # N, Q, k, baseG, sigma NaN
+        raw = bytearray(good)
+        raw[16 + 8 * word:24 + 8 * word] = struct.pack("<Q", value)
+        bad(raw, "parameter block")
+    open(f, "wb").write(good)
+    assert np.array_equal(K.load_secret_key(f)[1].s, sk.s)

@@ -18,7 +18,7 @@
 #   pmcset NAME SET [bench args]   one --pmc pass of a named SQ/TCC counter set
 export TMPDIR=/tmp
 T=${1:-x}
-O=gpurun_out/r5
+O=gpurun_out/${GRUN:-r6}
 mkdir -p "$O"
 
 gtests() {
@@ -110,11 +110,13 @@ pmc() {
 PMC_SQ1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES"
 PMC_SQ2="SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INST_CYCLES_VMEM GRBM_GUI_ACTIVE"
 PMC_L2="SQ_INSTS_SMEM SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA TCP_TOTAL_CACHE_ACCESSES_sum TCC_HIT_sum TCC_MISS_sum GRBM_COUNT"
+# instruction cache (SQ block on gfx950: counts toward the 8 SQ counters)
+PMC_IC="SQC_ICACHE_REQ SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_BUSY_CYCLES"
 pmcset() {
     local name=$1 set=$2
     shift 2
     local cs
-    case $set in sq1) cs=$PMC_SQ1 ;; sq2) cs=$PMC_SQ2 ;; l2) cs=$PMC_L2 ;; *) echo "unknown set $set"; return 1 ;; esac
+    case $set in sq1) cs=$PMC_SQ1 ;; sq2) cs=$PMC_SQ2 ;; l2) cs=$PMC_L2 ;; ic) cs=$PMC_IC ;; *) echo "unknown set $set"; return 1 ;; esac
     mkdir -p "$O/${T}_pmc_$name"
     MKACC_STREAMS=1 timeout -s KILL 300 rocprofv3 --pmc $cs -d "$O/${T}_pmc_$name/$set" -o run --output-format csv \
         -- python3 bench.py --steps 1 --warmup 0 --cpu-baseline 0 --check-gates 4 --n-override 32 "$@" \
