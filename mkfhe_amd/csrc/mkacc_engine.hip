@@ -364,11 +364,13 @@ bool use_lat(const mkacc_ctx* c, size_t B) {
 }
 
 // Small batches of at most one gate per CU take mk_quad_kernel (every polynomial
-// spread over the four waves of the gate's workgroup, mkacc_quad.hpp) when
-// MKACC_QUAD=1.
+// spread over the four waves of the gate's workgroup, mkacc_quad.hpp) for every k and
+// dg: one STD128_MKNTRU gate 43.7 -> 24.2 ms against the split-digit kernel, B = 256
+// 5.87 k -> 10.5 k gates/s, STD128_MKNTRU_3 one gate 486 -> 323 ms, B = 256 491 ->
+// 794 gates/s (profiles/r6/v5_ab_*, v6_ab_*).  MKACC_QUAD=0 keeps the older kernels.
 bool use_quad(const mkacc_ctx* c, size_t B) {
     if (c->wide || c->dg < 2 || c->dg > 5 || B > (size_t)c->cus) return false;
-    return c->env_quad == 1;
+    return c->env_quad != 0;
 }
 
 // Per-gate scratch words of the batch step kernel: mk_step_kernel DSCR keeps the

@@ -177,56 +177,94 @@ __device__ __forceinline__ void bfly_lds(uint32_t& a, uint32_t& b, const uint2* 
     ct_bfly_lazy<false, C>(a, b, tab[base + o], Q);
 }
 
-// Forward negacyclic NTT of the quarter polynomial: QA (coefficients, < 4Q) -> QD (EVAL,
-// [0, 4Q)); the reference's table and order (transformnat-impl.h:300-354) with the lazy
-// Shoup butterflies of ntt_fwd (values grow by < 2Q per stage, the last one reduces).
-// `xs` selects the cross buffer (uniform).
-template <bool C>
-__device__ __forceinline__ void ntt_fwd_q(uint32_t (&x)[kR], const Ctx& s, uint32_t xs) {
+// Forward negacyclic NTT of NP quarter polynomials at once: QA (coefficients, < 4Q) ->
+// QD (EVAL, [0, 4Q)); the reference's table and order (transformnat-impl.h:300-354)
+// with the lazy Shoup butterflies of ntt_fwd (values grow by < 2Q per stage, the last
+// one reduces).  The NP transforms (a pass's digit NTTs) run stage by stage together:
+// NP x 4 independent butterflies per stage for a lone wave per SIMD, each stage's
+// twiddles read once; the exchanges go polynomial by polynomial (a wave's LDS
+// operations execute in order, so one region serves them all), each cross exchange
+// on the next cross buffer.
+template <int NP, bool C>
+__device__ __forceinline__ void ntt_fwd_q(uint32_t (&x)[NP][kR], const Ctx& s, uint32_t& xs) {
     const uint32_t Q = s.m.Q, l = s.l, q = s.q;
     {   // QA: bits 10, 9, 8 -- twiddle 2^st + (j >> (b + 1)) depends on register bits only
         const ConstTable twc{(const_u64*)opaque(s.tws)};
         const uint2 w0 = twc[1], w1a = twc[2], w1b = twc[3], w2[4] = {twc[4], twc[5], twc[6], twc[7]};
 #pragma unroll
-        for (int r = 0; r < 4; ++r) ct_bfly_lazy<true, C>(x[r], x[r + 4], w0, Q);
+        for (int p = 0; p < NP; ++p)
 #pragma unroll
-        for (int r = 0; r < 8; ++r)
-            if (!(r & 2)) ct_bfly_lazy<true, C>(x[r], x[r + 2], (r & 4) ? w1b : w1a, Q);
+            for (int r = 0; r < 4; ++r) ct_bfly_lazy<true, C>(x[p][r], x[p][r + 4], w0, Q);
 #pragma unroll
-        for (int r = 0; r < 8; r += 2) ct_bfly_lazy<true, C>(x[r], x[r + 1], w2[r >> 1], Q);
+        for (int p = 0; p < NP; ++p)
+#pragma unroll
+            for (int r = 0; r < 8; ++r)
+                if (!(r & 2)) ct_bfly_lazy<true, C>(x[p][r], x[p][r + 2], (r & 4) ? w1b : w1a, Q);
+#pragma unroll
+        for (int p = 0; p < NP; ++p)
+#pragma unroll
+            for (int r = 0; r < 8; r += 2) ct_bfly_lazy<true, C>(x[p][r], x[p][r + 1], w2[r >> 1], Q);
     }
-    xintra<QA, QB, MI3>(x, s.ib, s.a_mi3, s.b_mi3);
+#pragma unroll
+    for (int p = 0; p < NP; ++p) xintra<QA, QB, MI3>(x[p], s.ib, s.a_mi3, s.b_mi3);
     {   // QB: bits 7, 6, 5; lane bits 5..3 = j bits 10..8
         const uint32_t lb = (l >> 3) & 7u;
-        const uint32_t t7 = 8u + lb, t6 = 16u + 2u * lb, t5 = 32u + 4u * lb;
+        const uint2 w7 = s.tf[8u + lb];
+        const uint2 w6[2] = {s.tf[16u + 2u * lb], s.tf[17u + 2u * lb]};
+        const uint2 w5[4] = {s.tf[32u + 4u * lb], s.tf[33u + 4u * lb], s.tf[34u + 4u * lb], s.tf[35u + 4u * lb]};
 #pragma unroll
-        for (int r = 0; r < 4; ++r) bfly_lds<C>(x[r], x[r + 4], s.tf, t7, 0, Q);
+        for (int p = 0; p < NP; ++p)
 #pragma unroll
-        for (int r = 0; r < 8; ++r)
-            if (!(r & 2)) bfly_lds<C>(x[r], x[r + 2], s.tf, t6, (uint32_t)(r >> 2), Q);
+            for (int r = 0; r < 4; ++r) ct_bfly_lazy<false, C>(x[p][r], x[p][r + 4], w7, Q);
 #pragma unroll
-        for (int r = 0; r < 8; r += 2) bfly_lds<C>(x[r], x[r + 1], s.tf, t5, (uint32_t)(r >> 1), Q);
+        for (int p = 0; p < NP; ++p)
+#pragma unroll
+            for (int r = 0; r < 8; ++r)
+                if (!(r & 2)) ct_bfly_lazy<false, C>(x[p][r], x[p][r + 2], w6[r >> 2], Q);
+#pragma unroll
+        for (int p = 0; p < NP; ++p)
+#pragma unroll
+            for (int r = 0; r < 8; r += 2) ct_bfly_lazy<false, C>(x[p][r], x[p][r + 1], w5[r >> 1], Q);
     }
-    xintra<QB, QC, MI3>(x, s.ib, s.b_mi3, s.c_mi3);
+#pragma unroll
+    for (int p = 0; p < NP; ++p) xintra<QB, QC, MI3>(x[p], s.ib, s.b_mi3, s.c_mi3);
     {   // QC: bits 4, 3, 2; lane = j bits 10..5
-        const uint32_t t4 = 64u + l, t3 = 128u + 2u * l, t2 = 256u + 4u * l;
+        const uint2 w4 = s.tf[64u + l];
+        const uint2 w3[2] = {s.tf[128u + 2u * l], s.tf[129u + 2u * l]};
+        const uint2 w2[4] = {s.tf[256u + 4u * l], s.tf[257u + 4u * l], s.tf[258u + 4u * l], s.tf[259u + 4u * l]};
 #pragma unroll
-        for (int r = 0; r < 4; ++r) bfly_lds<C>(x[r], x[r + 4], s.tf, t4, 0, Q);
+        for (int p = 0; p < NP; ++p)
 #pragma unroll
-        for (int r = 0; r < 8; ++r)
-            if (!(r & 2)) bfly_lds<C>(x[r], x[r + 2], s.tf, t3, (uint32_t)(r >> 2), Q);
+            for (int r = 0; r < 4; ++r) ct_bfly_lazy<false, C>(x[p][r], x[p][r + 4], w4, Q);
 #pragma unroll
-        for (int r = 0; r < 8; r += 2) bfly_lds<C>(x[r], x[r + 1], s.tf, t2, (uint32_t)(r >> 1), Q);
+        for (int p = 0; p < NP; ++p)
+#pragma unroll
+            for (int r = 0; r < 8; ++r)
+                if (!(r & 2)) ct_bfly_lazy<false, C>(x[p][r], x[p][r + 2], w3[r >> 2], Q);
+#pragma unroll
+        for (int p = 0; p < NP; ++p)
+#pragma unroll
+            for (int r = 0; r < 8; r += 2) ct_bfly_lazy<false, C>(x[p][r], x[p][r + 1], w2[r >> 1], Q);
     }
-    xcross<QC, QD>(x, s.xb + xs * kCrossWords, s.c_mx5, s.d_mx5);
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        xcross<QC, QD>(x[p], s.xb + xs * kCrossWords, s.c_mx5, s.d_mx5);
+        xs ^= 1u;
+    }
     {   // QD: bits 1, 0; j = lane << 5 | q << 3 | r
         const uint32_t t1 = 512u + 8u * l + 2u * q, t0 = 1024u + 16u * l + 4u * q;
+        const uint2 w1[2] = {s.tf[t1], s.tf[t1 + 1u]};
+        const uint2 w0[4] = {s.tf[t0], s.tf[t0 + 1u], s.tf[t0 + 2u], s.tf[t0 + 3u]};
 #pragma unroll
-        for (int r = 0; r < 8; ++r)
-            if (!(r & 2)) bfly_lds<C>(x[r], x[r + 2], s.tf, t1, (uint32_t)(r >> 2), Q);
+        for (int p = 0; p < NP; ++p)
+#pragma unroll
+            for (int r = 0; r < 8; ++r)
+                if (!(r & 2)) ct_bfly_lazy<false, C>(x[p][r], x[p][r + 2], w1[r >> 2], Q);
         const uint32_t m1 = s.m.m1;
 #pragma unroll
-        for (int r = 0; r < 8; r += 2) ct_bfly_last<C>(x[r], x[r + 1], s.tf[t0 + (uint32_t)(r >> 1)], Q, m1);
+        for (int p = 0; p < NP; ++p)
+#pragma unroll
+            for (int r = 0; r < 8; r += 2) ct_bfly_last<C>(x[p][r], x[p][r + 1], w0[r >> 1], Q, m1);
     }
 }
 
@@ -237,7 +275,7 @@ __device__ __forceinline__ void ntt_fwd_q(uint32_t (&x)[kR], const Ctx& s, uint3
 // the lazy butterfly: < 2Q + 11 x 2Q = 24Q < 2^32; the twist's Shoup product takes
 // any 32-bit word.
 template <bool C>
-__device__ __forceinline__ void ntt_inv_q(uint32_t (&x)[kR], const Ctx& s, uint32_t xs) {
+__device__ __forceinline__ void ntt_inv_q(uint32_t (&x)[kR], const Ctx& s, uint32_t& xs) {
     const uint32_t Q = s.m.Q, l = s.l, q = s.q;
     {   // QD: bits 0, 1, 2 -- t = j mod 2^b from register bits only
         const ConstTable twc{(const_u64*)opaque(s.tis)};
@@ -251,6 +289,7 @@ __device__ __forceinline__ void ntt_inv_q(uint32_t (&x)[kR], const Ctx& s, uint3
         for (int r = 0; r < 4; ++r) ct_bfly_lazy<true, C>(x[r], x[r + 4], w2[r & 3], Q);
     }
     xcross<QD, IB>(x, s.xb + xs * kCrossWords, s.d_mx5, s.ib_mx5);
+    xs ^= 1u;
     {   // IB: bits 3, 4, 5; j bit 2 = lane bit 0, bits 1, 0 = q
         const uint32_t t = ((l & 1u) << 2) | q;
         const uint32_t b3 = 8u + t, b4 = 16u + t, b5 = 32u + t;
@@ -351,25 +390,21 @@ __device__ __forceinline__ void issue_keys(QKeys<DG, METHOD, FIRST>& kk, const Q
     }
 }
 
-// iNTT -> SDD -> dg forward NTTs of the quarter: x (QD, [0, 2Q)) -> G[i] (QD)
+// iNTT -> SDD -> dg forward NTTs of the quarter: x (QD, [0, 2Q)) -> G[i] (QD); the
+// digit NTTs run together (ntt_fwd_q<DG>)
 template <int DG, bool C>
 __device__ __forceinline__ void digits_q(const Ctx& s, uint32_t (&x)[kR], uint32_t (&G)[DG][kR], uint32_t& xs) {
     ntt_inv_q<C>(x, s, xs);
-    xs ^= 1u;
     PackedDigits<DG, kR> pd;
 #pragma unroll
     for (int r = 0; r < kR; ++r) G[0][r] = pd.put(r, sdd_offset(x[r], s.sd), s.sd);
-    ntt_fwd_q<C>(G[0], s, xs);
-    xs ^= 1u;
-    digit_range<DG>(G[0], s.m.Q);
 #pragma unroll
-    for (int i = 1; i < DG; ++i) {
+    for (int i = 1; i < DG; ++i)
 #pragma unroll
         for (int r = 0; r < kR; ++r) G[i][r] = pd.get(r, i + 1, s.sd);
-        ntt_fwd_q<C>(G[i], s, xs);
-        xs ^= 1u;
-        digit_range<DG>(G[i], s.m.Q);
-    }
+    ntt_fwd_q<DG, C>(G, s, xs);
+#pragma unroll
+    for (int i = 0; i < DG; ++i) digit_range<DG>(G[i], s.m.Q);
 }
 
 // the MAC of one pass over this wave's 8 slots (mac2's algebra):

@@ -111,6 +111,9 @@ EVALACC_CASES = [
     ("STD100_MKNTRU_LWE_2", pyoracle.XZW_B, 4, 500, 32749, 1 << 9, Q_MK, 2),
     ("STD128_MKNTRU_3", pyoracle.XZW, 8, 765, 45181, 1 << 6, Q_MK, 1),
     ("CFG5_Q50_STD100_SHAPE", pyoracle.XZW, 2, 560, 45181, 1 << 10, Q50, 2),
+    # the reference's k = 16 rows (binfhecontext.cpp:129-144): STD128_MKNTRU_4 at dg = 5
+    # (a 2.0 GB bootstrapping key in u32 words)
+    ("STD128_MKNTRU_4", pyoracle.XZW, 16, 765, 45181, 1 << 5, Q_MK, 1),
 ]
 
 
@@ -144,7 +147,9 @@ def make_evalacc():
 
 # paramset, method, seed
 GATE_CASES = [("STD128_MKNTRU", 0, 9100), ("STD100_MKNTRU_LWE", 2, 9200),
-              ("STD100_MKNTRU_LWE_2", 2, 9300), ("STD128_MKNTRU_3", 0, 9400)]
+              ("STD100_MKNTRU_LWE_2", 2, 9300), ("STD128_MKNTRU_3", 0, 9400),
+              # k = 16 (binfhecontext.cpp:129-144): MK-NTRU at dg = 2, MK-LWE at dg = 3
+              ("STD100_MKNTRU_4", 0, 9500), ("STD128_MKNTRU_LWE_4", 2, 9600)]
 
 
 def make_gates():

@@ -98,11 +98,16 @@ def test_gate_tail_mntru(mk_gpu, oracle):
 # (k = 8, dg = 2) through both the small-batch and the batch step kernel
 @pytest.mark.gpu
 @pytest.mark.parametrize("k,n,logB,lat", [(2, 4, 9, ""), (2, 3, 7, ""), (3, 2, 6, ""), (8, 2, 6, "1"), (8, 2, 6, "0"),
-                                          (8, 2, 9, "1"), (8, 2, 9, "0")])
+                                          (8, 2, 9, "1"), (8, 2, 9, "0"), (2, 3, 7, "q"), (8, 2, 6, "q"),
+                                          (16, 2, 5, "q")])
 def test_nand_gate_mntru(mk_gpu, oracle, k, n, logB, lat, monkeypatch):
     mk = mk_gpu
     if lat:
         monkeypatch.setenv("MKACC_LAT", lat)
+    if lat != "q":
+        monkeypatch.setenv("MKACC_QUAD", "0")   # B = 5 would take mk_quad_kernel
+    else:
+        monkeypatch.delenv("MKACC_LAT", raising=False)
     B = 5
     orc, eng, evk, pkey, ksk2, q, qKS, baseKS = _mntru_setup(mk, oracle, k, n, 1 << logB, B, seed=k * 10 + n)
     ct1 = oracle.fill_uniform(B * k * n, q, 31).reshape(B, k, n)
@@ -144,9 +149,10 @@ def test_gate_tail_mklwe(mk_gpu, oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("k,n", [(2, 4), (4, 2), (8, 2)])
-def test_nand_gate_mklwe(mk_gpu, oracle, k, n):
+@pytest.mark.parametrize("k,n,quad", [(2, 4, "0"), (4, 2, "0"), (8, 2, "0"), (2, 4, "1"), (4, 2, "1"), (16, 2, "1")])
+def test_nand_gate_mklwe(mk_gpu, oracle, k, n, quad, monkeypatch):
     mk = mk_gpu
+    monkeypatch.setenv("MKACC_QUAD", quad)   # "1": mk_quad_kernel (B = 6 gates, one per workgroup)
     B = 6
     orc, eng, evk, pkey, A, Bk, q, qKS, baseKS = _mklwe_setup(mk, oracle, k, n, 1 << 9, seed=k * 10 + n + 50)
     a1 = oracle.fill_uniform(B * k * n, q, 61).reshape(B, k, n)

@@ -118,7 +118,8 @@ def test_evalacc_dscr_modes(mk, oracle, case, dscr, monkeypatch):
     picks by k, MKACC_DSCR forces one) give the oracle's accumulators."""
     meth, k, n, q, baseG, B = case
     monkeypatch.setenv("MKACC_DSCR", dscr)   # read when the context sizes its workspace
-    monkeypatch.setenv("MKACC_LAT", "0")     # the batch step kernel (small B would take mk_lat_kernel)
+    monkeypatch.setenv("MKACC_LAT", "0")     # the batch step kernel (small B would take mk_lat_kernel
+    monkeypatch.setenv("MKACC_QUAD", "0")    # or mk_quad_kernel)
     orc, evk, pkey, ct, acc = make_case(oracle, oracle.XZW, k, n, q, baseG, B + 2, seed=k * 31 + n)
     exp = orc.evalacc_batch(evk, pkey, ct, acc, 8)
     eng = mk.MKAccumulatorEngine(mk.make_params(mk.MKNTRU, k, n, 2048, Q_MK, q, baseG))
@@ -132,10 +133,11 @@ def test_evalacc_step_kernels(mk, oracle, case, monkeypatch):
     """The batch step kernel the engine selects -- mk_step2_kernel (digit NTTs
     first, one key stream per pass) at dg <= 3, mk_step_kernel at dg >= 4 --
     gives the oracle's accumulators for every case shape, with the monomial edge
-    cases in the first and last gate; MKACC_LAT=0 keeps small batches off the
-    one-wave-per-party kernel."""
+    cases in the first and last gate; MKACC_LAT=0 and MKACC_QUAD=0 keep small batches
+    off the small-batch kernels."""
     meth, k, n, q, baseG, B = case
     monkeypatch.setenv("MKACC_LAT", "0")
+    monkeypatch.setenv("MKACC_QUAD", "0")
     om = oracle.XZW if meth == "XZW" else oracle.XZW_B
     em = mk.MKNTRU if meth == "XZW" else mk.MKNTRU_LWE
     orc, evk, pkey, ct, acc = make_case(oracle, om, k, n, q, baseG, B + 3, seed=k * 17 + n + 2)
@@ -160,7 +162,8 @@ def test_evalacc_small_batch_kernel(mk, oracle, case, lat, monkeypatch):
     batches; MKACC_LAT forces it on or off) gives the oracle's accumulators for
     both methods, k = 2..8 parties and dg = 2..4."""
     meth, k, n, q, baseG, B = case
-    monkeypatch.setenv("MKACC_LAT", lat)   # read at every launch
+    monkeypatch.setenv("MKACC_LAT", lat)   # read at context creation
+    monkeypatch.setenv("MKACC_QUAD", "0")  # small batches would take mk_quad_kernel
     om = oracle.XZW if meth == "XZW" else oracle.XZW_B
     em = mk.MKNTRU if meth == "XZW" else mk.MKNTRU_LWE
     orc, evk, pkey, ct, acc = make_case(oracle, om, k, n, q, baseG, B + 1, seed=k * 13 + n)
@@ -178,6 +181,7 @@ def test_evalacc_two_party_split_digit_kernel(mk, oracle, meth, logB, monkeypatc
     digits over two waves, the f-part's over dg waves) equals the oracle and the
     one-wave-per-party kernel word for word, first step and later steps."""
     monkeypatch.setenv("MKACC_LAT", "1")
+    monkeypatch.setenv("MKACC_QUAD", "0")
     om = oracle.XZW if meth == "XZW" else oracle.XZW_B
     em = mk.MKNTRU if meth == "XZW" else mk.MKNTRU_LWE
     q = 45181 if meth == "XZW" else 32749
@@ -264,6 +268,7 @@ def test_evalacc_many_gates_every_wave_slot(mk, oracle, lat, monkeypatch):
     step kernel and with the one-wave-per-party kernel.  Guards against the
     co-resident-workgroup corruption of round 1."""
     monkeypatch.setenv("MKACC_LAT", lat)
+    monkeypatch.setenv("MKACC_QUAD", "0")
     B = 512
     orc, evk, pkey, ct, acc = make_case(oracle, oracle.XZW, 2, 2, 45181, 1 << 7, B, seed=77)
     exp = orc.evalacc_batch(evk, pkey, ct, acc, 16).astype(np.uint32)
@@ -323,6 +328,7 @@ def test_small_batch_run_kernel_at_its_residency_limit(mk, oracle, k, B, monkeyp
     whole batch equals the oracle on a spread sample, the first and last gate
     included."""
     monkeypatch.delenv("MKACC_LAT", raising=False)
+    monkeypatch.setenv("MKACC_QUAD", "0")
     orc, evk, pkey, ct, acc = make_case(oracle, oracle.XZW, k, 2, 45181, 1 << 9, B, seed=300 + k)
     eng = mk.MKAccumulatorEngine(mk.make_params(mk.MKNTRU, k, 2, 2048, Q_MK, 45181, 1 << 9))
     import torch
