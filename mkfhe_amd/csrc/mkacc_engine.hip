@@ -137,24 +137,25 @@ const void* latrun_fn(int dg, int method) {
         default: return nullptr;
     }
 }
-const void* quad_fn(int dg, int method, bool first) {
+const void* quad_fn(int dg, int method, bool first, int occ) {
     switch (dg) {
-        case 2: return mkacc_tu::quad_dg2(method, first);
-        case 3: return mkacc_tu::quad_dg3(method, first);
-        case 4: return mkacc_tu::quad_dg4(method, first);
-        case 5: return mkacc_tu::quad_dg5(method, first);
+        case 2: return mkacc_tu::quad_dg2(method, first, occ);
+        case 3: return mkacc_tu::quad_dg3(method, first, occ);
+        case 4: return mkacc_tu::quad_dg4(method, first, occ);
+        case 5: return mkacc_tu::quad_dg5(method, first, occ);
         default: return nullptr;
     }
 }
-const void* quadrun_fn(int dg, int method) {
+const void* quadrun_fn(int dg, int method, int occ) {
     switch (dg) {
-        case 2: return mkacc_tu::quadrun_dg2(method);
-        case 3: return mkacc_tu::quadrun_dg3(method);
-        case 4: return mkacc_tu::quadrun_dg4(method);
-        case 5: return mkacc_tu::quadrun_dg5(method);
+        case 2: return mkacc_tu::quadrun_dg2(method, occ);
+        case 3: return mkacc_tu::quadrun_dg3(method, occ);
+        case 4: return mkacc_tu::quadrun_dg4(method, occ);
+        case 5: return mkacc_tu::quadrun_dg5(method, occ);
         default: return nullptr;
     }
 }
+size_t quad_lds(int occ) { return occ == 2 ? quad::kLdsBytes2 : quad::kLdsBytes; }
 const void* lat_fn(int dg, int method, bool first) {
     switch (dg) {
         case 2: return mkacc_tu::lat_dg2(method, first);
@@ -368,9 +369,20 @@ bool use_lat(const mkacc_ctx* c, size_t B) {
 // dg: one STD128_MKNTRU gate 43.7 -> 24.2 ms against the split-digit kernel, B = 256
 // 5.87 k -> 10.5 k gates/s, STD128_MKNTRU_3 one gate 486 -> 323 ms, B = 256 491 ->
 // 794 gates/s (profiles/r6/v5_ab_*, v6_ab_*).  MKACC_QUAD=0 keeps the older kernels.
-bool use_quad(const mkacc_ctx* c, size_t B) {
-    if (c->wide || c->dg < 2 || c->dg > 5 || B > (size_t)c->cus) return false;
-    return c->env_quad != 0;
+// Above one gate per CU and up to four per CU, mk_quad2_kernel (the twiddle tables in
+// HBM, two workgroups per CU, dg <= 4; batches above 2 x CUs in rounds) beats the
+// per-party and the batch kernels: STD128_MKNTRU B = 384 6.8 k -> 11.0 k gates/s,
+// 512 8.7 k -> 14.7 k, 1024 12.0 k -> 15.3 k; STD100_MKNTRU_LWE_2 B = 512 6.2 k -> 8.5 k,
+// 1024 7.3 k -> 8.8 k; STD128_MKNTRU_3 B = 512 409 -> 992, 1024 773 -> 1,022.  From 8
+// gates per CU the batch kernels win (STD128_MKNTRU B = 2048: 18.2 k against 15.8 k,
+// 4096: 19.2 k against 16.0 k; config 3 at 4096 11.3 k against 9.2 k; config 4 at 8192
+// 1,282 against 1,059) -- profiles/r6/v11_ab_*, v12_ab_*.  MKACC_QUAD=2 forces it for
+// any batch (A/B runs).  Returns the workgroups per CU of the quad kernel, 0 for none.
+int use_quad(const mkacc_ctx* c, size_t B) {
+    if (c->wide || c->dg < 2 || c->dg > 5 || c->env_quad == 0) return 0;
+    if (c->env_quad == 2) return c->dg <= 4 ? 2 : 0;
+    if (B <= (size_t)c->cus) return 1;
+    return B <= 4 * (size_t)c->cus && c->dg <= 4 ? 2 : 0;
 }
 
 // Per-gate scratch words of the batch step kernel: mk_step_kernel DSCR keeps the
@@ -405,7 +417,8 @@ struct StepChain {
     hipStream_t st;
     uint32_t* cur;
     uint32_t* nxt;
-    bool lat, quad;
+    bool lat;
+    int quad;   // use_quad: 0, or the quad kernel's workgroups per CU
     StepChain(mkacc_ctx* c_, size_t B_, size_t g0_, size_t Bh_, hipStream_t st_)
         : c(c_), B(B_), g0(g0_), Bh(Bh_), ao(g0_ * c_->p.k * kN), st(st_), cur(c_->d_acc0 + ao), nxt(c_->d_acc1 + ao),
           lat(use_lat(c_, Bh_)), quad(use_quad(c_, Bh_)) {}
@@ -437,9 +450,9 @@ struct StepChain {
         const StepArgs a = args(u, i);
         // a null kernel must never reach hipLaunchKernelGGL (mkacc_create checks the set)
         if (quad) {
-            const void* fn = quad_fn((int)c->dg, c->method_class, first);
+            const void* fn = quad_fn((int)c->dg, c->method_class, first, quad);
             if (!fn) return false;
-            launch_ptr2(fn, dim3((unsigned)Bh), dim3(64 * quad::kWaves), quad::kLdsBytes, st, a, QuadArgs{c->d_qimg});
+            launch_ptr2(fn, dim3((unsigned)Bh), dim3(64 * quad::kWaves), quad_lds(quad), st, a, QuadArgs{c->d_qimg});
         } else if (lat) {
             const bool split = use_latd(c, Bh);
             const void* fn = split ? latd_fn((int)c->dg, c->method_class, first) : lat_fn((int)c->dg, c->method_class, first);
@@ -465,7 +478,7 @@ struct StepChain {
         const uint32_t n = c->p.n;
         const bool split = use_latd(c, Bh);
         const uint32_t waves = quad ? quad::kWaves : split ? kLatdWaves : c->p.k;
-        const void* fn = quad    ? quadrun_fn((int)c->dg, c->method_class)
+        const void* fn = quad    ? quadrun_fn((int)c->dg, c->method_class, quad)
                          : split ? latdrun_fn((int)c->dg, c->method_class)
                                  : latrun_fn((int)c->dg, c->method_class);
         if (!fn || t0 == 0 || t0 >= t1) return false;
@@ -482,7 +495,7 @@ struct StepChain {
         r.t1 = t1;
         r.key2off = c->nk == 2 ? (uint32_t)(c->dg * 2 * kN) : 0u;
         if (quad)
-            launch_ptr3(fn, dim3((unsigned)Bh), dim3(64 * waves), quad::kLdsBytes, st, a, r, QuadArgs{c->d_qimg});
+            launch_ptr3(fn, dim3((unsigned)Bh), dim3(64 * waves), quad_lds(quad), st, a, r, QuadArgs{c->d_qimg});
         else
             launch_ptr2(fn, dim3((unsigned)Bh), dim3(64 * waves), split ? latd_lds_bytes() : lat_lds_bytes(waves), st, a,
                         r);
@@ -546,7 +559,8 @@ uint32_t* launch_steps(mkacc_ctx* c, size_t B) {
     const char* dl = std::getenv("MKACC_DBG_LDS");
     const size_t lds = kStepLdsBytes + (dl ? std::strtoul(dl, nullptr, 0) : 0);
     const size_t unit = (size_t)c->cus * 4;
-    const size_t ns = std::min<size_t>((size_t)c->nstreams, B / unit);
+    // a quad batch runs its later steps in one launch: one chain, no slices
+    const size_t ns = use_quad(c, B) ? 1 : std::min<size_t>((size_t)c->nstreams, B / unit);
     if (ns < 2) {
         StepChain ch(c, B, 0, B, c->stream);
         if (use_run(c, B)) {
@@ -1335,7 +1349,10 @@ int mkacc_create(const mkacc_params* pin, int device, mkacc_ctx** out) {
     c->env_lat = env_switch("MKACC_LAT");
     c->env_latd = env_switch("MKACC_LATD");
     c->env_dscr = env_switch("MKACC_DSCR");
-    c->env_quad = env_switch("MKACC_QUAD");
+    {
+        const char* e = std::getenv("MKACC_QUAD");   // 0, 1 or 2 (two workgroups per CU, any B)
+        c->env_quad = e && *e ? (e[0] == '0' ? 0 : e[0] == '2' ? 2 : 1) : -1;
+    }
     c->dg = dg;
     c->step_ver = step_version((int)dg);
     c->nk = c->method_class == XZW ? 2 : 1;
@@ -1520,7 +1537,9 @@ const char* mkacc_step_kernel_name(const mkacc_ctx* c, size_t B) {
         return c->wfp ? "widereg2::step_kernel" : "wide::step_kernel";
     // small batches: the kernel that runs the steps after the first (all but one of
     // the k n steps; the first is one launch of mk_latd_kernel / mk_lat_kernel)
-    if (use_quad(c, B)) return use_run(c, B) ? "mk_quad_run_kernel" : "mk_quad_kernel";
+    if (const int qo = use_quad(c, B))
+        return qo == 2 ? (use_run(c, B) ? "mk_quad2_run_kernel" : "mk_quad2_kernel")
+                       : (use_run(c, B) ? "mk_quad_run_kernel" : "mk_quad_kernel");
     if (use_lat(c, B)) {
         if (use_run(c, B)) return use_latd(c, B) ? "mk_latd_run_kernel" : "mk_lat_run_kernel";
         return use_latd(c, B) ? "mk_latd_kernel" : "mk_lat_kernel";

@@ -1302,14 +1302,14 @@ MKACC_TU_API KernelPtr latdrun_dg4(int method);
 MKACC_TU_API KernelPtr latrun_dg2(int method);    // mk_lat_run_kernel (the later steps in one launch)
 MKACC_TU_API KernelPtr latrun_dg3(int method);
 MKACC_TU_API KernelPtr latrun_dg4(int method);
-MKACC_TU_API KernelPtr quad_dg2(int method, bool first);   // mk_quad_kernel (a gate per workgroup, quarter polynomials)
-MKACC_TU_API KernelPtr quad_dg3(int method, bool first);
-MKACC_TU_API KernelPtr quad_dg4(int method, bool first);
-MKACC_TU_API KernelPtr quad_dg5(int method, bool first);
-MKACC_TU_API KernelPtr quadrun_dg2(int method);            // mk_quad_run_kernel (the later steps in one launch)
-MKACC_TU_API KernelPtr quadrun_dg3(int method);
-MKACC_TU_API KernelPtr quadrun_dg4(int method);
-MKACC_TU_API KernelPtr quadrun_dg5(int method);
+MKACC_TU_API KernelPtr quad_dg2(int method, bool first, int occ);   // mk_quad_kernel (a gate per workgroup, quarter polynomials)
+MKACC_TU_API KernelPtr quad_dg3(int method, bool first, int occ);
+MKACC_TU_API KernelPtr quad_dg4(int method, bool first, int occ);
+MKACC_TU_API KernelPtr quad_dg5(int method, bool first, int occ);
+MKACC_TU_API KernelPtr quadrun_dg2(int method, int occ);            // mk_quad_run_kernel (the later steps in one launch)
+MKACC_TU_API KernelPtr quadrun_dg3(int method, int occ);
+MKACC_TU_API KernelPtr quadrun_dg4(int method, int occ);
+MKACC_TU_API KernelPtr quadrun_dg5(int method, int occ);
 MKACC_TU_API KernelPtr wide_step(int method, bool first);     // mkacc_wide.hpp (integer 64-bit words)
 MKACC_TU_API KernelPtr widereg2_step(int method, bool first);  // mkacc_widereg2.hpp (FP64, Q < 2^50)
 }  // namespace mkacc_tu

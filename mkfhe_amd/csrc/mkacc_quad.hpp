@@ -102,16 +102,24 @@ constexpr uint32_t kLdsWordsQ = kIW + kWaves * kIntraWords;
 constexpr size_t kLdsBytes = (size_t)kLdsWordsQ * 4;
 static_assert(kLdsBytes <= 160 * 1024, "one quad workgroup per CU");
 static_assert(kTfW % 4 == 0 && kXW % 4 == 0, "dwordx4 table copies");
+// the two-workgroups-per-CU form (mk_quad2_kernel): the TF / TI / TW tables stay in
+// HBM (read through L1 / L2), LDS holds [psi^e - 1][2 cross buffers][4 intra regions]
+constexpr uint32_t kXW2 = kPsiW;
+constexpr uint32_t kIW2 = kXW2 + 2 * kCrossWords;
+constexpr size_t kLdsBytes2 = (size_t)(kIW2 + kWaves * kIntraWords) * 4;
+static_assert(2 * kLdsBytes2 <= 160 * 1024, "two quad2 workgroups per CU");
 
 // Table image in HBM (mkacc_ctx::d_qimg, mkacc_create): TF (= the reference forward
 // table, negated pairs), TI[2^b + t] = psi^-(t 2^(11-b)) (negated pairs), TW[i] =
 // psi^-i (Shoup pairs), 3N pairs, copied behind the psi^e - 1 table
+template <bool LDSTAB>
 __device__ __forceinline__ void load_tables(uint32_t* smem, const uint32_t* img, const uint32_t* qimg) {
     const uint4* s1 = reinterpret_cast<const uint4*>(img) + kPsm1Off / 2;
     const uint4* s2 = reinterpret_cast<const uint4*>(qimg);
     uint4* d = reinterpret_cast<uint4*>(smem);
     for (int i = threadIdx.x; i < kN; i += blockDim.x) d[i] = s1[i];
-    for (int i = threadIdx.x; i < 3 * kN / 2; i += blockDim.x) d[kN + i] = s2[i];
+    if constexpr (LDSTAB)
+        for (int i = threadIdx.x; i < 3 * kN / 2; i += blockDim.x) d[kN + i] = s2[i];
     __syncthreads();
 }
 
@@ -495,8 +503,11 @@ __device__ __forceinline__ void quad_step(const StepArgs& a, const Ctx& s0, uint
         const uint32_t u = index + 1 + t < k ? index + 1 + t : index + 1 + t - k;
         uint32_t x[kR], st[kR];
         QKeys<DG, METHOD, FIRST> kk;
+        // keys issued before the transforms, except in the first (KDM) step: its four
+        // key words per digit would hold 32 dg VGPRs across them (it runs once per gate)
+        constexpr bool kPf = MKACC_QUAD_PF && !FIRST;
         if (!fpart) {
-            if (MKACC_QUAD_PF) issue_keys<DG, METHOD, FIRST, false>(kk, rs, u);
+            if (kPf) issue_keys<DG, METHOD, FIRST, false>(kk, rs, u);
 #pragma unroll
             for (int g = 0; g < 2; ++g) {
                 const u32x4 v = bload4(rs.rin, rs.vo, u * polyB + rs.so + (uint32_t)g * 1024u);
@@ -515,7 +526,7 @@ __device__ __forceinline__ void quad_step(const StepArgs& a, const Ctx& s0, uint
         } else {
             // the index party's output: this wave's own stores earlier in the step
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (MKACC_QUAD_PF) issue_keys<DG, METHOD, FIRST, true>(kk, rs, index);
+            if (kPf) issue_keys<DG, METHOD, FIRST, true>(kk, rs, index);
 #pragma unroll
             for (int g = 0; g < 2; ++g) {
                 const u32x4 v = bload4(rs.rout, rs.vo, index * polyB + rs.so + (uint32_t)g * 1024u);
@@ -530,27 +541,29 @@ __device__ __forceinline__ void quad_step(const StepArgs& a, const Ctx& s0, uint
         digits_q<DG, C>(s, x, G, xs);
         vcc_fence();   // the MAC branch follows the last butterflies
         if (!fpart) {
-            if (!MKACC_QUAD_PF) issue_keys<DG, METHOD, FIRST, false>(kk, rs, u);
+            if (!kPf) issue_keys<DG, METHOD, FIRST, false>(kk, rs, u);
             mac_q<DG, METHOD, FIRST, false>(s, rs, kk, G, st, sv, mp, mn, u);
         } else {
-            if (!MKACC_QUAD_PF) issue_keys<DG, METHOD, FIRST, true>(kk, rs, index);
+            if (!kPf) issue_keys<DG, METHOD, FIRST, true>(kk, rs, index);
             mac_q<DG, METHOD, FIRST, true>(s, rs, kk, G, st, sv, mp, mn, index);
         }
         if (fpart) break;
     }
 }
 
+template <bool LDSTAB>
 __device__ __forceinline__ Ctx make_ctx(const StepArgs& a, uint32_t* smem, const uint32_t* qimg) {
     Ctx s;
     const uint2* t = reinterpret_cast<const uint2*>(smem);
+    const uint2* g = reinterpret_cast<const uint2*>(qimg);
     s.psi = t;
-    s.tf = t + kTfW / 2;
-    s.ti = t + kTiW / 2;
-    s.tw = t + kTwW / 2;
-    s.xb = smem + kXW;
+    s.tf = LDSTAB ? t + kTfW / 2 : g;
+    s.ti = LDSTAB ? t + kTiW / 2 : g + kN;
+    s.tw = LDSTAB ? t + kTwW / 2 : g + 2 * kN;
+    s.xb = smem + (LDSTAB ? kXW : kXW2);
     s.l = threadIdx.x & 63u;
     s.q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    s.ib = smem + kIW + s.q * kIntraWords;
+    s.ib = smem + (LDSTAB ? kIW : kIW2) + s.q * kIntraWords;
     s.tws = a.tw_fwd;
     s.tis = a.tw_inv;
     s.m = a.m;
@@ -566,12 +579,14 @@ struct QuadArgs {
     const uint32_t* qimg;   // TF, TI, TW tables (mkacc_ctx::d_qimg), 3N pairs
 };
 
-// one accumulator step (the first, KDM, or any other) for B gates, one workgroup each
-template <int DG, int METHOD, bool FIRST>
-__global__ __launch_bounds__(256, 1) void mk_quad_kernel(StepArgs a, QuadArgs qa) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    quad::load_tables(smem, a.img, qa.qimg);
-    const quad::Ctx s = quad::make_ctx(a, smem, qa.qimg);
+// one accumulator step (the first, KDM, or any other) for B gates, one workgroup each.
+// OCC = 1: the twiddle tables in LDS, one workgroup per CU (B <= CUs: every gate
+// resident at once, the kernel the engine takes); OCC = 2: the tables in HBM, two
+// workgroups per CU (mk_quad2_kernel, MKACC_QUAD=2)
+template <int DG, int METHOD, bool FIRST, int OCC>
+__device__ __forceinline__ void quad_one(const StepArgs& a, const QuadArgs& qa, uint32_t* smem) {
+    quad::load_tables<OCC == 1>(smem, a.img, qa.qimg);
+    const quad::Ctx s = quad::make_ctx<OCC == 1>(a, smem, qa.qimg);
     uint32_t xs = 0;
     quad::quad_step<DG, METHOD, FIRST>(a, s, xs);
 }
@@ -579,11 +594,10 @@ __global__ __launch_bounds__(256, 1) void mk_quad_kernel(StepArgs a, QuadArgs qa
 // back to back; a wave reads only the accumulator slots it wrote itself, so a step's
 // stores drain (vmcnt) before the next step's loads and no workgroup barrier is needed
 // between steps beyond those inside the transforms
-template <int DG, int METHOD>
-__global__ __launch_bounds__(256, 1) void mk_quad_run_kernel(StepArgs a, LatdRun r, QuadArgs qa) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    quad::load_tables(smem, a.img, qa.qimg);
-    const quad::Ctx s = quad::make_ctx(a, smem, qa.qimg);
+template <int DG, int METHOD, int OCC>
+__device__ __forceinline__ void quad_run(const StepArgs& a, const LatdRun& r, const QuadArgs& qa, uint32_t* smem) {
+    quad::load_tables<OCC == 1>(smem, a.img, qa.qimg);
+    const quad::Ctx s = quad::make_ctx<OCC == 1>(a, smem, qa.qimg);
     uint32_t xs = 0;
 #pragma unroll 1
     for (uint32_t t = r.t0; t < r.t1; ++t) {
@@ -592,13 +606,49 @@ __global__ __launch_bounds__(256, 1) void mk_quad_run_kernel(StepArgs a, LatdRun
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
 }
+template <int DG, int METHOD, bool FIRST>
+__global__ __launch_bounds__(256, 1) void mk_quad_kernel(StepArgs a, QuadArgs qa) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    quad_one<DG, METHOD, FIRST, 1>(a, qa, smem);
+}
+template <int DG, int METHOD>
+__global__ __launch_bounds__(256, 1) void mk_quad_run_kernel(StepArgs a, LatdRun r, QuadArgs qa) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    quad_run<DG, METHOD, 1>(a, r, qa, smem);
+}
+template <int DG, int METHOD, bool FIRST>
+__global__ __launch_bounds__(256, 2) void mk_quad2_kernel(StepArgs a, QuadArgs qa) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    quad_one<DG, METHOD, FIRST, 2>(a, qa, smem);
+}
+template <int DG, int METHOD>
+__global__ __launch_bounds__(256, 2) void mk_quad2_run_kernel(StepArgs a, LatdRun r, QuadArgs qa) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    quad_run<DG, METHOD, 2>(a, r, qa, smem);
+}
 
 template <int DG>
-const void* pick_quad(int method, bool first) {
+const void* pick_quad(int method, bool first, int occ) {
+    if (occ == 2) {
+        if constexpr (DG > 4) {
+            return nullptr;   // dg = 5 needs more than 256 registers per lane (it would spill)
+        } else {
+            if (method == XZW)
+                return first ? (const void*)mk_quad2_kernel<DG, XZW, true> : (const void*)mk_quad2_kernel<DG, XZW, false>;
+            return first ? (const void*)mk_quad2_kernel<DG, XZW_B, true> : (const void*)mk_quad2_kernel<DG, XZW_B, false>;
+        }
+    }
     if (method == XZW) return first ? (const void*)mk_quad_kernel<DG, XZW, true> : (const void*)mk_quad_kernel<DG, XZW, false>;
     return first ? (const void*)mk_quad_kernel<DG, XZW_B, true> : (const void*)mk_quad_kernel<DG, XZW_B, false>;
 }
 template <int DG>
-const void* pick_quad_run(int method) {
+const void* pick_quad_run(int method, int occ) {
+    if (occ == 2) {
+        if constexpr (DG > 4) {
+            return nullptr;
+        } else {
+            return method == XZW ? (const void*)mk_quad2_run_kernel<DG, XZW> : (const void*)mk_quad2_run_kernel<DG, XZW_B>;
+        }
+    }
     return method == XZW ? (const void*)mk_quad_run_kernel<DG, XZW> : (const void*)mk_quad_run_kernel<DG, XZW_B>;
 }

@@ -50,8 +50,10 @@ KernelPtr MKACC_CAT(latrun_dg, MKACC_TU_DG)(int method) { return pick_lat_run<MK
 #elif MKACC_TU_PART == 2
 KernelPtr MKACC_CAT(step2_dg, MKACC_TU_DG)(int method) { return (KernelPtr)pick_step2<MKACC_TU_DG, false>(method); }
 #elif MKACC_TU_PART == 4
-KernelPtr MKACC_CAT(quad_dg, MKACC_TU_DG)(int method, bool first) { return pick_quad<MKACC_TU_DG>(method, first); }
-KernelPtr MKACC_CAT(quadrun_dg, MKACC_TU_DG)(int method) { return pick_quad_run<MKACC_TU_DG>(method); }
+KernelPtr MKACC_CAT(quad_dg, MKACC_TU_DG)(int method, bool first, int occ) {
+    return pick_quad<MKACC_TU_DG>(method, first, occ);
+}
+KernelPtr MKACC_CAT(quadrun_dg, MKACC_TU_DG)(int method, int occ) { return pick_quad_run<MKACC_TU_DG>(method, occ); }
 #else
 KernelPtr MKACC_CAT(step2f_dg, MKACC_TU_DG)(int method) { return (KernelPtr)pick_step2<MKACC_TU_DG, true>(method); }
 #endif

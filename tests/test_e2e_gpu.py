@@ -123,7 +123,7 @@ def _mntru_oracle_gates(oracle, cc, c1, c2, idx):
 
 
 @pytest.mark.gpu
-def test_config4_eight_party_mkntru_gates_decrypt_correctly(oracle):
+def test_config4_eight_party_mkntru_gates_decrypt_correctly(oracle, monkeypatch):
     """Config 4's parameter set (STD128_MKNTRU_3: k = 8, n = 765, B_g = 2^6, dg = 4;
     binfhecontext.cpp:131) with real seeded keys: a 320-gate batch (the batch step
     kernel with its d_i scratch, the k = 8 extraction and KeySwitch2 of
@@ -131,6 +131,7 @@ def test_config4_eight_party_mkntru_gates_decrypt_correctly(oracle):
     equal the CPU oracle's full gates bit for bit.  The seed draws no r-defective
     key (asserted), so the truth table is deterministic."""
     from mkfhe_amd.binfhe import NAND
+    monkeypatch.setenv("MKACC_QUAD", "0")   # B = 320 would take mk_quad2_kernel
     cc = _ctx("STD128_MKNTRU_3", 0, 808)
     sk = cc.MNTRU_KeyGen()
     cc.MKBTKeyGen(sk)
@@ -148,7 +149,7 @@ def test_config4_eight_party_mkntru_gates_decrypt_correctly(oracle):
 
 
 @pytest.mark.gpu
-def test_config3_four_party_mklwe_gates_decrypt_correctly(oracle):
+def test_config3_four_party_mklwe_gates_decrypt_correctly(oracle, monkeypatch):
     """Config 3's parameter set (STD100_MKNTRU_LWE_2: MK-LWE, k = 4, n = 500;
     binfhecontext.cpp:142; UniEncAccumulatorXZW_B, mk-acc-xzw_B.cpp:103-132, and
     KeySwitch, mklwe-pke.cpp:260-298) with real seeded keys: a 640-gate batch (the
@@ -156,6 +157,7 @@ def test_config3_four_party_mklwe_gates_decrypt_correctly(oracle):
     full gates bit for bit."""
     from mkfhe_amd import keys as K
     from mkfhe_amd.binfhe import NAND
+    monkeypatch.setenv("MKACC_QUAD", "0")   # B = 640 would take mk_quad2_kernel
     cc = _ctx("STD100_MKNTRU_LWE_2", 2, 404)
     sk = cc.MKLWE_KeyGen()
     cc.MKBTKeyGen(sk)

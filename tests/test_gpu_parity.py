@@ -347,15 +347,18 @@ def test_small_batch_run_kernel_at_its_residency_limit(mk, oracle, k, B, monkeyp
 QUAD_CASES = [c for c in CASES]
 
 
+@pytest.mark.parametrize("occ", ["1", "2"])
 @pytest.mark.parametrize("case", QUAD_CASES,
                          ids=[f"{c[0]}-k{c[1]}-n{c[2]}-logB{c[4].bit_length() - 1}" for c in QUAD_CASES])
-def test_evalacc_quad_kernel(mk, oracle, case, monkeypatch):
+def test_evalacc_quad_kernel(mk, oracle, case, occ, monkeypatch):
     """mk_quad_kernel (one gate per workgroup, every polynomial spread over its four
     waves, mkacc_quad.hpp; MKACC_QUAD=1) equals the oracle for both methods, k = 1..16,
     dg = 2..5, with the monomial edge cases c = 0, 2N - 1 (and 2N for XZW_B): the first
     step in its own launch, the others in one mk_quad_run_kernel launch."""
     meth, k, n, q, baseG, B = case
-    monkeypatch.setenv("MKACC_QUAD", "1")
+    if occ == "2" and baseG == 1 << 5:
+        pytest.skip("the two-workgroups-per-CU form is built for dg <= 4")
+    monkeypatch.setenv("MKACC_QUAD", occ)   # "2": mk_quad2_kernel, tables in HBM, two workgroups per CU
     om = oracle.XZW if meth == "XZW" else oracle.XZW_B
     em = mk.MKNTRU if meth == "XZW" else mk.MKNTRU_LWE
     orc, evk, pkey, ct, acc = make_case(oracle, om, k, n, q, baseG, B + 2, seed=k * 41 + n)
@@ -367,7 +370,8 @@ def test_evalacc_quad_kernel(mk, oracle, case, monkeypatch):
         ct[0, 0, n - 1] = 4095
     exp = orc.evalacc_batch(evk, pkey, ct, acc, 8)
     eng = mk.MKAccumulatorEngine(mk.make_params(em, k, n, 2048, Q_MK, q, baseG))
-    assert eng.step_kernel_name(B + 2) == ("mk_quad_run_kernel" if k * n > 1 else "mk_quad_kernel")
+    pre = "mk_quad2" if occ == "2" else "mk_quad"
+    assert eng.step_kernel_name(B + 2) == (pre + "_run_kernel" if k * n > 1 else pre + "_kernel")
     eng.upload_keys(evk.astype(np.uint32), pkey.astype(np.uint32))
     got = eng.eval_batch(ct.astype(np.uint32), acc.astype(np.uint32))
     assert np.array_equal(got, exp.astype(np.uint32))
