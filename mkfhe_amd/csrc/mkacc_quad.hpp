@@ -630,12 +630,13 @@ __global__ __launch_bounds__(256, 2) void mk_quad2_run_kernel(StepArgs a, LatdRu
 template <int DG>
 const void* pick_quad(int method, bool first, int occ) {
     if (occ == 2) {
+        // dg = 5 needs more than 256 registers per lane (it would spill); the first step
+        // runs mk_quad_kernel at either occupancy (the engine's StepChain::step)
         if constexpr (DG > 4) {
-            return nullptr;   // dg = 5 needs more than 256 registers per lane (it would spill)
+            return nullptr;
         } else {
-            if (method == XZW)
-                return first ? (const void*)mk_quad2_kernel<DG, XZW, true> : (const void*)mk_quad2_kernel<DG, XZW, false>;
-            return first ? (const void*)mk_quad2_kernel<DG, XZW_B, true> : (const void*)mk_quad2_kernel<DG, XZW_B, false>;
+            if (first) return nullptr;
+            return method == XZW ? (const void*)mk_quad2_kernel<DG, XZW, false> : (const void*)mk_quad2_kernel<DG, XZW_B, false>;
         }
     }
     if (method == XZW) return first ? (const void*)mk_quad_kernel<DG, XZW, true> : (const void*)mk_quad_kernel<DG, XZW, false>;

@@ -71,7 +71,7 @@ BUDGET = [
     (r"mk_lat_run_kernel<\d, [01]>", 256, 1),             # the small-batch kernel's later steps in one launch
     (r"mk_quad_kernel<\d, [01], (true|false)>", 512, 1),  # one gate per workgroup (B <= CUs): one wave per
     (r"mk_quad_run_kernel<\d, [01]>", 512, 1),            # SIMD, so AGPRs may extend the register file
-    (r"mk_quad2_kernel<[234], [01], (true|false)>", 256, 2),  # two workgroups per CU (B <= 4 x CUs, dg <= 4)
+    (r"mk_quad2_kernel<[234], [01], false>", 256, 2),  # two workgroups per CU (B <= 4 x CUs, dg <= 4)
     (r"mk_quad2_run_kernel<[234], [01]>", 256, 2),
     (r"mk_step_kernel<4, 0, false, true>", 256, 2),      # config-4 step (dg = 4, d_i scratch; spill-free since
                                                           # the alternating reload order)
