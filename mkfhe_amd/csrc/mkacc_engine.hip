@@ -246,6 +246,10 @@ struct mkacc_ctx {
     // context's lifetime
     int env_lat = -1, env_latd = -1, env_dscr = -1, env_quad = -1;
     uint32_t* d_qimg = nullptr;   // mk_quad_kernel tables: TF, TI, TW (mkacc_quad.hpp), 3N pairs
+    uint32_t* d_psync = nullptr;  // mk_quadp_run_kernel flags, counters and sv slots (quad::psync_words)
+    size_t psync_words = 0;
+    bool psync_pending = false;   // a party-parallel launch since its timeout word was last read
+    uint32_t h_abort = 0;
     uint32_t dg = 0, nk = 0;
     Mod mod{};
     SddConsts sd{};
@@ -313,7 +317,8 @@ struct mkacc_ctx {
     uint32_t* d_wcvals = nullptr;
     uint32_t* d_wct = nullptr;     // host-pointer API staging
     uint64_t* d_wio = nullptr;
-    uint32_t* d_bad = nullptr;     // [0] input-range flag of the device batches (mkacc_sync), [1] device key upload
+    uint32_t* d_bad = nullptr;     // [0] input-range flag of the device batches (mkacc_sync), [1] device key upload,
+                                   // [2] party-parallel synchronisation timeout (mk_quadp_run_kernel)
     std::mutex mu;
 };
 
@@ -364,6 +369,15 @@ bool use_lat(const mkacc_ctx* c, size_t B) {
     return B <= (size_t)c->cus * (kLdsPerCu / lat_lds_bytes(c->p.k));
 }
 
+// The party-parallel form (mk_quadp_run_kernel: a workgroup per party, the steps after
+// the first) needs all B k workgroups resident, one per CU (a cooperative launch).  It
+// is the default wherever it fits: STD128_MKNTRU one gate 24.1 -> 17.1 ms, B = 128
+// 5.24 k -> 7.30 k gates/s; STD128_MKNTRU_3 one gate 319.5 -> 95.2 ms, B = 32 101 ->
+// 340 gates/s (profiles/r6/v16_ab_*).  MKACC_QUAD=1 keeps one workgroup per gate.
+bool use_quadp(const mkacc_ctx* c, size_t B) {
+    return c->p.k >= 2 && B * c->p.k <= (size_t)c->cus && c->p.k * c->p.n >= 2;
+}
+
 // Small batches of at most one gate per CU take mk_quad_kernel (every polynomial
 // spread over the four waves of the gate's workgroup, mkacc_quad.hpp) for every k and
 // dg: one STD128_MKNTRU gate 43.7 -> 24.2 ms against the split-digit kernel, B = 256
@@ -381,6 +395,7 @@ bool use_lat(const mkacc_ctx* c, size_t B) {
 int use_quad(const mkacc_ctx* c, size_t B) {
     if (c->wide || c->dg < 2 || c->dg > 5 || c->env_quad == 0) return 0;
     if (c->env_quad == 2) return c->dg <= 4 ? 2 : 0;
+    if (c->env_quad != 1 && use_quadp(c, B)) return 3;
     if (B <= (size_t)c->cus) return 1;
     return B <= 4 * (size_t)c->cus && c->dg <= 4 ? 2 : 0;
 }
@@ -389,7 +404,12 @@ int use_quad(const mkacc_ctx* c, size_t B) {
 // step's d_i ([dg][N]).
 size_t step_scratch_words(const mkacc_ctx* c) { return use_dscr(c) ? (size_t)c->dg * kN : 0; }
 
+int ensure_psync(mkacc_ctx* c, size_t B);
 int ensure_ws(mkacc_ctx* c, size_t B) {
+    if (use_quad(c, B) == 3) {
+        const int rc = ensure_psync(c, B);
+        if (rc) return rc;
+    }
     if (B <= c->ws_B) return MKACC_OK;
     if (c->d_acc0) HIP_TRY(hipFree(c->d_acc0));
     if (c->d_acc1) HIP_TRY(hipFree(c->d_acc1));
@@ -404,6 +424,31 @@ int ensure_ws(mkacc_ctx* c, size_t B) {
     if (const size_t sw = step_scratch_words(c)) HIP_TRY(hipMalloc(&c->d_dscr, B * sw * 4));
     c->ws_B = B;
     return MKACC_OK;
+}
+// the party-parallel kernel's synchronisation area for B gates
+int ensure_psync(mkacc_ctx* c, size_t B) {
+    const size_t w = quad::psync_words(B, c->p.k);
+    if (w <= c->psync_words) return MKACC_OK;
+    if (c->d_psync) HIP_TRY(hipFree(c->d_psync));
+    c->d_psync = nullptr;
+    c->psync_words = 0;
+    HIP_TRY(hipMalloc(&c->d_psync, w * 4));
+    c->psync_words = w;
+    return MKACC_OK;
+}
+// After the final synchronisation of an entry point: a party-parallel launch whose
+// waits timed out (d_bad[2], read back with the results by psync_enqueue) fails it.
+int psync_enqueue(mkacc_ctx* c) {
+    if (c->psync_pending) HIP_TRY(hipMemcpyAsync(&c->h_abort, c->d_bad + 2, 4, hipMemcpyDeviceToHost, c->stream));
+    return MKACC_OK;
+}
+int psync_result(mkacc_ctx* c) {
+    if (!c->psync_pending) return MKACC_OK;
+    c->psync_pending = false;
+    if (!c->h_abort) return MKACC_OK;
+    c->h_abort = 0;
+    HIP_TRY(hipMemset(c->d_bad + 2, 0, 4));
+    return fail(MKACC_E_DEVICE, "party-parallel step kernel: a synchronisation wait timed out (results are invalid)");
 }
 
 // The k*n accumulator steps over a batch whose monomial exponents are in
@@ -497,7 +542,18 @@ struct StepChain {
         r.t0 = t0;
         r.t1 = t1;
         r.key2off = c->nk == 2 ? (uint32_t)(c->dg * 2 * kN) : 0u;
-        if (quad)
+        if (quad == 3) {
+            // every workgroup of the batch resident at once: the cooperative launch refuses
+            // a grid the device cannot hold instead of leaving waits without a producer
+            if (hipMemsetAsync(c->d_psync, 0, quad::psync_counter_words(Bh, c->p.k) * 4, st) != hipSuccess)
+                return false;
+            QuadArgs qa{c->d_qimg, c->d_psync, c->d_bad + 2};
+            void* args[] = {(void*)&a, (void*)&r, (void*)&qa};
+            if (hipLaunchCooperativeKernel(fn, dim3((unsigned)(Bh * c->p.k)), dim3(64 * waves), args,
+                                           (unsigned)quad_lds(quad), st) != hipSuccess)
+                return false;
+            c->psync_pending = true;
+        } else if (quad)
             launch_ptr3(fn, dim3((unsigned)Bh), dim3(64 * waves), quad_lds(quad), st, a, r, QuadArgs{c->d_qimg});
         else
             launch_ptr2(fn, dim3((unsigned)Bh), dim3(64 * waves), split ? latd_lds_bytes() : lat_lds_bytes(waves), st, a,
@@ -1353,8 +1409,10 @@ int mkacc_create(const mkacc_params* pin, int device, mkacc_ctx** out) {
     c->env_latd = env_switch("MKACC_LATD");
     c->env_dscr = env_switch("MKACC_DSCR");
     {
-        const char* e = std::getenv("MKACC_QUAD");   // 0, 1 or 2 (two workgroups per CU, any B)
-        c->env_quad = e && *e ? (e[0] == '0' ? 0 : e[0] == '2' ? 2 : 1) : -1;
+        // 0 (no quad kernel), 1 (one workgroup per gate, no party-parallel form),
+        // 2 (two workgroups per CU, any B), 3 / unset (the policy of use_quad)
+        const char* e = std::getenv("MKACC_QUAD");
+        c->env_quad = e && *e ? (e[0] == '0' ? 0 : e[0] == '2' ? 2 : e[0] == '3' ? 3 : 1) : -1;
     }
     c->dg = dg;
     c->step_ver = step_version((int)dg);
@@ -1366,8 +1424,8 @@ int mkacc_create(const mkacc_params* pin, int device, mkacc_ctx** out) {
         HIP_TRY(hipSetDevice(device));
         HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
         HIP_TRY(create_slice_streams(c.get()));
-        HIP_TRY(hipMalloc(&c->d_bad, 8));   // [0] batch inputs, [1] device key upload
-        HIP_TRY(hipMemset(c->d_bad, 0, 8));
+        HIP_TRY(hipMalloc(&c->d_bad, 12));   // [0] batch inputs, [1] device key upload, [2] sync timeout
+        HIP_TRY(hipMemset(c->d_bad, 0, 12));
         const int rc = wide_setup(c.get());
         if (rc) {
             mkacc_destroy(c.release());
@@ -1407,8 +1465,8 @@ int mkacc_create(const mkacc_params* pin, int device, mkacc_ctx** out) {
     HIP_TRY(hipSetDevice(device));
     HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIP_TRY(create_slice_streams(c.get()));
-    HIP_TRY(hipMalloc(&c->d_bad, 8));   // [0] batch inputs, [1] device key upload
-    HIP_TRY(hipMemset(c->d_bad, 0, 8));
+    HIP_TRY(hipMalloc(&c->d_bad, 12));   // [0] batch inputs, [1] device key upload, [2] sync timeout
+    HIP_TRY(hipMemset(c->d_bad, 0, 12));
     // forward NTT table in the reference's order (transformnat-impl.h:705-760),
     // powers psi^e and psi^-e (e < 2N) for the inverse transform and the monomials
     const uint64_t Q = p.Q, psi = p.root, psii = modinv(psi, Q);
@@ -1491,7 +1549,8 @@ void mkacc_destroy(mkacc_ctx* c) {
                     (void*)c->d_wtwi, (void*)c->d_wpsi, (void*)c->d_ftwf, (void*)c->d_fpsi, (void*)c->d_rtis,
                     (void*)c->d_r2tab,
                     (void*)c->d_wkeys, (void*)c->d_wpkey, (void*)c->d_wacc0,
-                    (void*)c->d_wacc1, (void*)c->d_wcvals, (void*)c->d_wct, (void*)c->d_wio, (void*)c->d_bad})
+                    (void*)c->d_wacc1, (void*)c->d_wcvals, (void*)c->d_wct, (void*)c->d_wio, (void*)c->d_bad,
+                    (void*)c->d_psync})
         if (p) (void)hipFree(p);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     for (int j = 0; j < mkacc_ctx::kMaxStreams - 1; ++j) {
@@ -1543,7 +1602,8 @@ const char* mkacc_step_kernel_name(const mkacc_ctx* c, size_t B) {
     // small batches: the kernel that runs the steps after the first (all but one of
     // the k n steps; the first is one launch of mk_latd_kernel / mk_lat_kernel)
     if (const int qo = use_quad(c, B))
-        return qo == 2 ? (use_run(c, B) ? "mk_quad2_run_kernel" : "mk_quad2_kernel")
+        return qo == 3 ? "mk_quadp_run_kernel"
+               : qo == 2 ? (use_run(c, B) ? "mk_quad2_run_kernel" : "mk_quad2_kernel")
                        : (use_run(c, B) ? "mk_quad_run_kernel" : "mk_quad_kernel");
     if (use_lat(c, B)) {
         if (use_run(c, B)) return use_latd(c, B) ? "mk_latd_run_kernel" : "mk_lat_run_kernel";
@@ -1608,8 +1668,9 @@ int mkacc_eval_batch(mkacc_ctx* c, const uint32_t* ct, const uint32_t* acc_in, u
     int rc = launch_batch(c, c->d_ct, c->d_io, c->d_io, B);
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(acc_out, c->d_io, accw * 4, hipMemcpyDeviceToHost, c->stream));
+    if (const int prc = psync_enqueue(c)) return prc;
     HIP_TRY(hipStreamSynchronize(c->stream));
-    return MKACC_OK;
+    return psync_result(c);
 }
 
 int mkacc_eval_batch_device(mkacc_ctx* c, const uint32_t* d_ct, const uint32_t* d_in, uint32_t* d_out, size_t B) {
@@ -1839,8 +1900,9 @@ int gate_host(mkacc_ctx* c, const uint32_t* nand, const uint32_t* a1, const uint
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(out_a, c->d_gout, B * kno * 4, hipMemcpyDeviceToHost, c->stream));
     if (lwe) HIP_TRY(hipMemcpyAsync(out_b, c->d_gout + B * kno, B * 4, hipMemcpyDeviceToHost, c->stream));
+    if (const int prc = psync_enqueue(c)) return prc;
     HIP_TRY(hipStreamSynchronize(c->stream));
-    return MKACC_OK;
+    return psync_result(c);
 }
 }  // namespace
 
@@ -1914,7 +1976,9 @@ int mkacc_sync(mkacc_ctx* c) {
     HIP_TRY(hipSetDevice(c->device));
     uint32_t bad = 0;
     HIP_TRY(hipMemcpyAsync(&bad, c->d_bad, 4, hipMemcpyDeviceToHost, c->stream));
+    if (const int prc = psync_enqueue(c)) return prc;
     HIP_TRY(hipStreamSynchronize(c->stream));
+    if (const int rc = psync_result(c)) return rc;
     if (bad) {
         HIP_TRY(hipMemset(c->d_bad, 0, 4));
         return fail(MKACC_E_RANGE, "an input word passed to a device entry point was out of range "

@@ -551,6 +551,178 @@ __device__ __forceinline__ void quad_step(const StepArgs& a, const Ctx& s0, uint
     }
 }
 
+// ---- party-parallel steps (mk_quadp_run_kernel) ------------------------------------
+// A batch of B <= CUs / k gates runs B k workgroups, one per CU: workgroup g k + t runs
+// party t's pass of every step of gate g (its accumulator polynomial is touched by no
+// other workgroup), and the index party's workgroup also runs the step's f-part.  The
+// f-part needs sumV = sum over the parties of their sv shares; the other parties publish
+// theirs through a per-gate HBM ring of kSlots slots and run on into their next steps
+// (which need only their own polynomial), so a step's critical path is the index
+// party's pass plus the f-part: 2 (dg + 1) transforms instead of (k + 1)(dg + 1).
+// Synchronisation is per wave: wave q of the index workgroup reads only the slots wave
+// q of every other workgroup wrote (the same EVAL slots), so no workgroup barrier is
+// added.  The shares, flags and counters move with system-coherent accesses (sc0 sc1:
+// written through to memory, read past both cache levels) ordered by s_waitcnt, never
+// by whole-cache write-backs or invalidates: agent-scope release / acquire pairs
+// (buffer_wbl2 / buffer_inv) ran 18.4 ms per STD128_MKNTRU gate at B = 1 but tripled
+// the step at 256 workgroups, where every CU's waits flushed its XCD's L2
+// (profiles/r6/v15).  Every wait is bounded: a timeout sets *abort, after which no wave
+// waits again (the kernel drains, the engine reports MKACC_E_DEVICE).
+constexpr uint32_t kSlots = 4;
+constexpr uint32_t kSpinLimit = 1u << 20;   // polls of ~0.1-1 us: far beyond any step
+struct PSync {
+    uint32_t* flag;    // this gate's [k][4]: sv shares published by wave q of party t (steps)
+    uint32_t* used;    // this gate's [4]: steps whose shares wave q of the index party has read
+    __amdgpu_buffer_rsrc_t rsv;   // this gate's [kSlots][k][N] sv shares, C4 order
+    uint32_t* abort;
+    uint32_t gate, party;
+};
+// words of the synchronisation area for B gates of k parties: flags, counters, then
+// the 16-byte aligned slot ring
+__host__ __device__ constexpr size_t psync_counter_words(size_t B, size_t k) { return ((B * k * 4 + B * 4) + 3) & ~size_t(3); }
+__host__ __device__ constexpr size_t psync_words(size_t B, size_t k) {
+    return psync_counter_words(B, k) + B * kSlots * k * (size_t)kN;
+}
+__device__ __forceinline__ PSync make_psync(uint32_t* sync, uint32_t* abort, uint32_t B, uint32_t k) {
+    PSync p;
+    p.gate = __builtin_amdgcn_readfirstlane(blockIdx.x / k);
+    p.party = __builtin_amdgcn_readfirstlane(blockIdx.x - p.gate * k);
+    p.flag = sync + (size_t)p.gate * k * 4;
+    p.used = sync + (size_t)B * k * 4 + p.gate * 4;
+    p.rsv = make_rsrc(sync + psync_counter_words(B, k) + (size_t)p.gate * kSlots * k * kN, kSlots * k * kN * 4u);
+    p.abort = abort;
+    return p;
+}
+constexpr int kSysCoherent = 1 | 16;   // buffer cache policy sc0 | sc1
+// wait until *p >= want; false after a timeout here or elsewhere.  The memory clobbers
+// keep the caller's share loads after the loop (the hardware issues them after the
+// branch that saw the flag).
+__device__ __forceinline__ bool wait_at_least(const uint32_t* p, uint32_t want, uint32_t* abort) {
+    asm volatile("" ::: "memory");
+    bool ok = true;
+    for (uint32_t n = 0;; ++n) {
+        if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= want) break;
+        if (__hip_atomic_load(abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) { ok = false; break; }
+        if (n >= kSpinLimit) {
+            __hip_atomic_store(abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            ok = false;
+            break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+    asm volatile("" ::: "memory");
+    return ok;
+}
+// set a flag / counter once this wave's earlier stores (or the loads whose values the
+// caller consumed) have completed
+__device__ __forceinline__ void post(uint32_t* p, uint32_t v) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    asm volatile("" ::: "memory");
+}
+
+// one later step (rel = steps since the launch's first) of party ps.party of gate ps.gate
+template <int DG, int METHOD>
+__device__ __forceinline__ void quadp_step(const StepArgs& a, const Ctx& s0, uint32_t& xs, const PSync& ps,
+                                           uint32_t rel) {
+    constexpr bool C = true, FIRST = false;
+    constexpr bool kPf = MKACC_QUAD_PF;
+    Ctx s = s0;
+    const uint32_t l = s.l, q = s.q;
+    const uint32_t gate = ps.gate, t = ps.party;
+    const uint32_t c = __builtin_amdgcn_readfirstlane(a.cvals[gate]);
+    const uint32_t cneg = (2u * kN - c) & (2u * kN - 1u);
+    const uint32_t k = a.k, index = a.index;
+    const uint32_t polyB = kN * 4u;
+    const QMono mp = make_qmono(c, l, q);
+    const QMono mn = make_qmono(METHOD != XZW ? cneg : (cneg + kN) & (2u * kN - 1u), l, q);
+    const QRes rs{make_rsrc(a.acc_in + (size_t)gate * k * kN, k * polyB),
+                  make_rsrc(a.acc_out + (size_t)gate * k * kN, k * polyB),
+                  make_rsrc(a.key1, DG * 2 * polyB),
+                  make_rsrc(a.key2, DG * 2 * polyB),
+                  make_rsrc(a.keys, DG * 2 * polyB),
+                  make_rsrc(a.pkey, k * DG * polyB),
+                  l * 16u,
+                  q * 2048u};
+    const uint32_t Q = s.m.Q;
+    uint32_t sv[kR];
+#pragma unroll
+    for (int r = 0; r < kR; ++r) sv[r] = 0;
+    {   // party t's pass: acc_out[t] and its sv share
+        uint32_t x[kR], st[kR];
+        QKeys<DG, METHOD, FIRST> kk;
+        if (kPf) issue_keys<DG, METHOD, FIRST, false>(kk, rs, t);
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+            const u32x4 v = bload4(rs.rin, rs.vo, t * polyB + rs.so + (uint32_t)g * 1024u);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) st[4 * g + e] = v[e];
+        }
+#pragma unroll
+        for (int r = 0; r < kR; ++r) x[r] = mul_shoup_lazy(st[r], mp.at(s.psi, r), Q);   // xzw.cpp:336-338
+        vcc_fence();
+        uint32_t G[DG][kR];
+        digits_q<DG, C>(s, x, G, xs);
+        vcc_fence();
+        if (!kPf) issue_keys<DG, METHOD, FIRST, false>(kk, rs, t);
+        mac_q<DG, METHOD, FIRST, false>(s, rs, kk, G, st, sv, mp, mn, t);
+    }
+    const uint32_t slot = rel % kSlots;
+    if (t != index) {
+        // publish the share once the index party has read what the slot held
+        if (rel + 1u > kSlots) wait_at_least(ps.used + q, rel + 1u - kSlots, ps.abort);
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4{sv[4 * g], sv[4 * g + 1], sv[4 * g + 2], sv[4 * g + 3]},
+                                                   ps.rsv, rs.vo, (slot * k + t) * polyB + rs.so + (uint32_t)g * 1024u,
+                                                   kSysCoherent);
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_nop 1");   // store-data hazard (bstore4)
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        post(ps.flag + t * 4u + q, rel + 1u);
+        return;
+    }
+    // the index party: sumV = its own share + the others', then the f-part
+    uint32_t x[kR];
+#pragma unroll
+    for (int r = 0; r < kR; ++r) x[r] = sv[r];
+#pragma unroll 1
+    for (uint32_t o = 1; o < k; ++o) {
+        const uint32_t u = index + o < k ? index + o : index + o - k;
+        wait_at_least(ps.flag + u * 4u + q, rel + 1u, ps.abort);
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(
+                ps.rsv, rs.vo, (slot * k + u) * polyB + rs.so + (uint32_t)g * 1024u, kSysCoherent);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const uint32_t y = x[4 * g + e] + v[e];   // shares and sums in [0, 2Q)
+                x[4 * g + e] = min(y, y - 2u * Q);
+            }
+        }
+    }
+    vcc_fence();
+    post(ps.used + q, rel + 1u);   // the shares have landed: the slots are free
+    {
+        uint32_t st[kR];
+        QKeys<DG, METHOD, FIRST> kk;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's acc_out[index] stores
+        if (kPf) issue_keys<DG, METHOD, FIRST, true>(kk, rs, index);
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+            const u32x4 v = bload4(rs.rout, rs.vo, index * polyB + rs.so + (uint32_t)g * 1024u);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) st[4 * g + e] = v[e];
+        }
+        uint32_t G[DG][kR];
+        digits_q<DG, C>(s, x, G, xs);
+        vcc_fence();
+        if (!kPf) issue_keys<DG, METHOD, FIRST, true>(kk, rs, index);
+        mac_q<DG, METHOD, FIRST, true>(s, rs, kk, G, st, sv, mp, mn, index);
+    }
+}
+
 template <bool LDSTAB>
 __device__ __forceinline__ Ctx make_ctx(const StepArgs& a, uint32_t* smem, const uint32_t* qimg) {
     Ctx s;
@@ -577,6 +749,8 @@ __device__ __forceinline__ Ctx make_ctx(const StepArgs& a, uint32_t* smem, const
 
 struct QuadArgs {
     const uint32_t* qimg;   // TF, TI, TW tables (mkacc_ctx::d_qimg), 3N pairs
+    uint32_t* sync;         // mk_quadp_run_kernel: flags, counters and sv slots (quad::psync_words)
+    uint32_t* abort;        // mk_quadp_run_kernel: non-zero after a synchronisation timeout
 };
 
 // one accumulator step (the first, KDM, or any other) for B gates, one workgroup each.
@@ -627,6 +801,22 @@ __global__ __launch_bounds__(256, 2) void mk_quad2_run_kernel(StepArgs a, LatdRu
     quad_run<DG, METHOD, 2>(a, r, qa, smem);
 }
 
+// steps [t0, t1) party-parallel: B k workgroups, all resident (cooperative launch)
+template <int DG, int METHOD>
+__global__ __launch_bounds__(256, 1) void mk_quadp_run_kernel(StepArgs a, LatdRun r, QuadArgs qa) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    quad::load_tables<true>(smem, a.img, qa.qimg);
+    const quad::Ctx s = quad::make_ctx<true>(a, smem, qa.qimg);
+    const quad::PSync ps = quad::make_psync(qa.sync, qa.abort, a.B, a.k);
+    uint32_t xs = 0;
+#pragma unroll 1
+    for (uint32_t t = r.t0; t < r.t1; ++t) {
+        quad::quadp_step<DG, METHOD>(run_args(a, r, t), s, xs, ps, t - r.t0);
+        vcc_fence();   // the loop branch follows the step's last reductions
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+}
+
 template <int DG>
 const void* pick_quad(int method, bool first, int occ) {
     if (occ == 2) {
@@ -644,6 +834,7 @@ const void* pick_quad(int method, bool first, int occ) {
 }
 template <int DG>
 const void* pick_quad_run(int method, int occ) {
+    if (occ == 3) return method == XZW ? (const void*)mk_quadp_run_kernel<DG, XZW> : (const void*)mk_quadp_run_kernel<DG, XZW_B>;
     if (occ == 2) {
         if constexpr (DG > 4) {
             return nullptr;

@@ -99,15 +99,18 @@ def test_gate_tail_mntru(mk_gpu, oracle):
 @pytest.mark.gpu
 @pytest.mark.parametrize("k,n,logB,lat", [(2, 4, 9, ""), (2, 3, 7, ""), (3, 2, 6, ""), (8, 2, 6, "1"), (8, 2, 6, "0"),
                                           (8, 2, 9, "1"), (8, 2, 9, "0"), (2, 3, 7, "q"), (8, 2, 6, "q"),
-                                          (16, 2, 5, "q")])
+                                          (16, 2, 5, "q"), (2, 3, 7, "q1"), (8, 2, 6, "q1")])
 def test_nand_gate_mntru(mk_gpu, oracle, k, n, logB, lat, monkeypatch):
     mk = mk_gpu
-    if lat:
+    if lat and lat[0] != "q":
         monkeypatch.setenv("MKACC_LAT", lat)
-    if lat != "q":
-        monkeypatch.setenv("MKACC_QUAD", "0")   # B = 5 would take mk_quad_kernel
+        monkeypatch.setenv("MKACC_QUAD", "0")   # B = 5 would take the quad kernels
+    elif lat == "q1":
+        monkeypatch.setenv("MKACC_QUAD", "1")   # one workgroup per gate (no party-parallel form)
+    elif lat == "q":
+        monkeypatch.delenv("MKACC_LAT", raising=False)   # default: party-parallel, B k <= CUs
     else:
-        monkeypatch.delenv("MKACC_LAT", raising=False)
+        monkeypatch.setenv("MKACC_QUAD", "0")
     B = 5
     orc, eng, evk, pkey, ksk2, q, qKS, baseKS = _mntru_setup(mk, oracle, k, n, 1 << logB, B, seed=k * 10 + n)
     ct1 = oracle.fill_uniform(B * k * n, q, 31).reshape(B, k, n)
@@ -149,10 +152,11 @@ def test_gate_tail_mklwe(mk_gpu, oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("k,n,quad", [(2, 4, "0"), (4, 2, "0"), (8, 2, "0"), (2, 4, "1"), (4, 2, "1"), (16, 2, "1")])
+@pytest.mark.parametrize("k,n,quad", [(2, 4, "0"), (4, 2, "0"), (8, 2, "0"), (2, 4, "1"), (4, 2, "1"), (16, 2, "1"),
+                                      (2, 4, "3"), (16, 2, "3")])
 def test_nand_gate_mklwe(mk_gpu, oracle, k, n, quad, monkeypatch):
     mk = mk_gpu
-    monkeypatch.setenv("MKACC_QUAD", quad)   # "1": mk_quad_kernel (B = 6 gates, one per workgroup)
+    monkeypatch.setenv("MKACC_QUAD", quad)   # "1": mk_quad_kernel (B = 6 gates, one per workgroup); "3": party-parallel
     B = 6
     orc, eng, evk, pkey, A, Bk, q, qKS, baseKS = _mklwe_setup(mk, oracle, k, n, 1 << 9, seed=k * 10 + n + 50)
     a1 = oracle.fill_uniform(B * k * n, q, 61).reshape(B, k, n)

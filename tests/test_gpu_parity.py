@@ -347,14 +347,17 @@ def test_small_batch_run_kernel_at_its_residency_limit(mk, oracle, k, B, monkeyp
 QUAD_CASES = [c for c in CASES]
 
 
-@pytest.mark.parametrize("occ", ["1", "2"])
+@pytest.mark.parametrize("occ", ["1", "2", "3"])
 @pytest.mark.parametrize("case", QUAD_CASES,
                          ids=[f"{c[0]}-k{c[1]}-n{c[2]}-logB{c[4].bit_length() - 1}" for c in QUAD_CASES])
 def test_evalacc_quad_kernel(mk, oracle, case, occ, monkeypatch):
     """mk_quad_kernel (one gate per workgroup, every polynomial spread over its four
     waves, mkacc_quad.hpp; MKACC_QUAD=1) equals the oracle for both methods, k = 1..16,
     dg = 2..5, with the monomial edge cases c = 0, 2N - 1 (and 2N for XZW_B): the first
-    step in its own launch, the others in one mk_quad_run_kernel launch."""
+    step in its own launch, the others in one mk_quad_run_kernel launch.  occ "2": the
+    two-workgroups-per-CU form; "3": the party-parallel form (a workgroup per party,
+    mk_quadp_run_kernel; k = 1 keeps mk_quad_run_kernel), whose small n switches the
+    index party every few steps and wraps the sv slot ring."""
     meth, k, n, q, baseG, B = case
     if occ == "2" and baseG == 1 << 5:
         pytest.skip("the two-workgroups-per-CU form is built for dg <= 4")
@@ -370,24 +373,27 @@ def test_evalacc_quad_kernel(mk, oracle, case, occ, monkeypatch):
         ct[0, 0, n - 1] = 4095
     exp = orc.evalacc_batch(evk, pkey, ct, acc, 8)
     eng = mk.MKAccumulatorEngine(mk.make_params(em, k, n, 2048, Q_MK, q, baseG))
-    pre = "mk_quad2" if occ == "2" else "mk_quad"
+    pre = {"2": "mk_quad2", "3": "mk_quadp" if k > 1 else "mk_quad"}.get(occ, "mk_quad")
     assert eng.step_kernel_name(B + 2) == (pre + "_run_kernel" if k * n > 1 else pre + "_kernel")
     eng.upload_keys(evk.astype(np.uint32), pkey.astype(np.uint32))
     got = eng.eval_batch(ct.astype(np.uint32), acc.astype(np.uint32))
     assert np.array_equal(got, exp.astype(np.uint32))
 
 
-@pytest.mark.parametrize("name,B", [("STD128_MKNTRU", 3), ("STD100_MKNTRU_LWE", 2), ("STD100_MKNTRU_LWE_2", 256)])
-def test_evalacc_quad_kernel_full_paramsets(mk, oracle, name, B, monkeypatch):
-    """The quad kernel at full n (1530 / 1000 / 2000 steps in one launch), up to one
-    gate per CU, against the oracle on a spread sample."""
-    monkeypatch.setenv("MKACC_QUAD", "1")
+@pytest.mark.parametrize("name,B,occ", [("STD128_MKNTRU", 3, "1"), ("STD100_MKNTRU_LWE", 2, "1"),
+                                        ("STD100_MKNTRU_LWE_2", 256, "1"), ("STD128_MKNTRU", 3, "3"),
+                                        ("STD100_MKNTRU_LWE_2", 64, "3"), ("STD128_MKNTRU_3", 1, "3")])
+def test_evalacc_quad_kernel_full_paramsets(mk, oracle, name, B, occ, monkeypatch):
+    """The quad kernel at full n (1530 / 1000 / 2000 / 6120 steps in one launch), up to
+    one gate per CU, against the oracle on a spread sample; occ "3" is the party-parallel
+    form (B = 64 at k = 4: 256 workgroups, one on every CU)."""
+    monkeypatch.setenv("MKACC_QUAD", occ)
     p = mk.paramset(name)
     om = oracle.XZW if p.method == mk.MKNTRU else oracle.XZW_B
     orc, evk, pkey, ct, acc = make_case(oracle, om, p.k, p.n, p.q, p.baseG, B, seed=p.n + B)
     acc[:] = orc.mntru_testvector(4)
     eng = mk.MKAccumulatorEngine(p)
-    assert eng.step_kernel_name(B) == "mk_quad_run_kernel"
+    assert eng.step_kernel_name(B) == ("mk_quadp_run_kernel" if occ == "3" else "mk_quad_run_kernel")
     eng.upload_keys(evk.astype(np.uint32), pkey.astype(np.uint32))
     got = eng.eval_batch(ct.astype(np.uint32), acc.astype(np.uint32))
     pick = sorted({0, B // 2, B - 1})
