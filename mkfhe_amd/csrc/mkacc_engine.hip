@@ -375,7 +375,8 @@ bool use_lat(const mkacc_ctx* c, size_t B) {
 // 5.24 k -> 7.30 k gates/s; STD128_MKNTRU_3 one gate 319.5 -> 95.2 ms, B = 32 101 ->
 // 340 gates/s (profiles/r6/v16_ab_*).  MKACC_QUAD=1 keeps one workgroup per gate.
 bool use_quadp(const mkacc_ctx* c, size_t B) {
-    return c->p.k >= 2 && B * c->p.k <= (size_t)c->cus && c->p.k * c->p.n >= 2;
+    // shares carry their step tag in bits 28..31: residues below 2Q < 2^28
+    return c->p.k >= 2 && B * c->p.k <= (size_t)c->cus && c->p.k * c->p.n >= 2 && c->p.Q < (1ull << 27);
 }
 
 // Small batches of at most one gate per CU take mk_quad_kernel (every polynomial
@@ -545,8 +546,9 @@ struct StepChain {
         if (quad == 3) {
             // every workgroup of the batch resident at once: the cooperative launch refuses
             // a grid the device cannot hold instead of leaving waits without a producer
-            if (hipMemsetAsync(c->d_psync, 0, quad::psync_counter_words(Bh, c->p.k) * 4, st) != hipSuccess)
-                return false;
+            const uint32_t v4 = (uint32_t)(quad::psync_words(Bh, c->p.k) / 4);
+            hipLaunchKernelGGL(psync_clear_kernel, dim3(std::min<uint32_t>((v4 + 255) / 256, 1024u)), dim3(256), 0, st,
+                               c->d_psync, v4);
             QuadArgs qa{c->d_qimg, c->d_psync, c->d_bad + 2};
             void* args[] = {(void*)&a, (void*)&r, (void*)&qa};
             if (hipLaunchCooperativeKernel(fn, dim3((unsigned)(Bh * c->p.k)), dim3(64 * waves), args,

@@ -561,50 +561,64 @@ __device__ __forceinline__ void quad_step(const StepArgs& a, const Ctx& s0, uint
 // party's pass plus the f-part: 2 (dg + 1) transforms instead of (k + 1)(dg + 1).
 // Synchronisation is per wave: wave q of the index workgroup reads only the slots wave
 // q of every other workgroup wrote (the same EVAL slots), so no workgroup barrier is
-// added.  The shares, flags and counters move with system-coherent accesses (sc0 sc1:
-// written through to memory, read past both cache levels) ordered by s_waitcnt, never
-// by whole-cache write-backs or invalidates: agent-scope release / acquire pairs
+// added.  Shares and counters move with system-coherent accesses (sc0 sc1: written
+// through to memory, read past both cache levels) ordered by s_waitcnt, never by
+// whole-cache write-backs or invalidates: agent-scope release / acquire pairs
 // (buffer_wbl2 / buffer_inv) ran 18.4 ms per STD128_MKNTRU gate at B = 1 but tripled
 // the step at 256 workgroups, where every CU's waits flushed its XCD's L2
-// (profiles/r6/v15).  Every wait is bounded: a timeout sets *abort, after which no wave
-// waits again (the kernel drains, the engine reports MKACC_E_DEVICE).
+// (profiles/r6/v15).  A share carries its step in the free top bits of every word
+// (a residue below 2Q < 2^28; tag 1 + rel mod 8, a zeroed slot never matches), so the
+// index party loads the shares without a flag round trip -- the first batch before its
+// own pass, checked after it -- and reloads only what is not there yet.  One counter
+// per wave, `used`, orders the ring: the index party's wave q posts rel + 1 once it has
+// taken step rel's shares and written its own share of rel to its slot (every party
+// writes every step's slot, so no slot keeps a share from 8 steps back); a writer
+// waits for used >= rel + 1 - kSlots before reusing a slot, and a party that takes over
+// as index waits for the same before (re)loading, so every slot it reads holds step rel
+// or rel - kSlots, whose tags differ (tools/quadp_protocol.py checks this under random
+// schedules, and that each of the three rules is needed).  Every wait is bounded: a timeout sets *abort, after which no wave waits
+// again (the kernel drains, the engine reports MKACC_E_DEVICE).
 constexpr uint32_t kSlots = 4;
-constexpr uint32_t kSpinLimit = 1u << 20;   // polls of ~0.1-1 us: far beyond any step
+constexpr uint32_t kBatch = 4;              // shares per load batch of the index party
+constexpr uint32_t kSpinLimit = 1u << 20;   // polls of ~1 us: far beyond any step
+constexpr int kSysCoherent = 1 | 16;        // buffer cache policy sc0 | sc1
 struct PSync {
-    uint32_t* flag;    // this gate's [k][4]: sv shares published by wave q of party t (steps)
-    uint32_t* used;    // this gate's [4]: steps whose shares wave q of the index party has read
-    __amdgpu_buffer_rsrc_t rsv;   // this gate's [kSlots][k][N] sv shares, C4 order
+    uint32_t* used;    // this gate's [4]: steps whose shares wave q of the index party has taken
+    __amdgpu_buffer_rsrc_t rsv;   // this gate's [kSlots][k][N] tagged sv shares, C4 order
     uint32_t* abort;
     uint32_t gate, party;
 };
-// words of the synchronisation area for B gates of k parties: flags, counters, then
-// the 16-byte aligned slot ring
-__host__ __device__ constexpr size_t psync_counter_words(size_t B, size_t k) { return ((B * k * 4 + B * 4) + 3) & ~size_t(3); }
+// words of the synchronisation area for B gates of k parties: the counters, then the
+// 16-byte aligned slot ring (all zeroed before every launch)
+__host__ __device__ constexpr size_t psync_counter_words(size_t B) { return (B * 4 + 3) & ~size_t(3); }
 __host__ __device__ constexpr size_t psync_words(size_t B, size_t k) {
-    return psync_counter_words(B, k) + B * kSlots * k * (size_t)kN;
+    return psync_counter_words(B) + B * kSlots * k * (size_t)kN;
 }
 __device__ __forceinline__ PSync make_psync(uint32_t* sync, uint32_t* abort, uint32_t B, uint32_t k) {
     PSync p;
     p.gate = __builtin_amdgcn_readfirstlane(blockIdx.x / k);
     p.party = __builtin_amdgcn_readfirstlane(blockIdx.x - p.gate * k);
-    p.flag = sync + (size_t)p.gate * k * 4;
-    p.used = sync + (size_t)B * k * 4 + p.gate * 4;
-    p.rsv = make_rsrc(sync + psync_counter_words(B, k) + (size_t)p.gate * kSlots * k * kN, kSlots * k * kN * 4u);
+    p.used = sync + p.gate * 4;
+    p.rsv = make_rsrc(sync + psync_counter_words(B) + (size_t)p.gate * kSlots * k * kN, kSlots * k * kN * 4u);
     p.abort = abort;
     return p;
 }
-constexpr int kSysCoherent = 1 | 16;   // buffer cache policy sc0 | sc1
-// wait until *p >= want; false after a timeout here or elsewhere.  The memory clobbers
-// keep the caller's share loads after the loop (the hardware issues them after the
-// branch that saw the flag).
+__device__ __forceinline__ uint32_t share_tag(uint32_t rel) { return (rel & 7u) + 1u; }
+__device__ __forceinline__ bool aborted(uint32_t* abort) {
+    return __hip_atomic_load(abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
+}
+__device__ __forceinline__ void set_abort(uint32_t* abort) {
+    __hip_atomic_store(abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// wait until *p >= want; false after a timeout here or elsewhere
 __device__ __forceinline__ bool wait_at_least(const uint32_t* p, uint32_t want, uint32_t* abort) {
     asm volatile("" ::: "memory");
     bool ok = true;
     for (uint32_t n = 0;; ++n) {
         if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= want) break;
-        if (__hip_atomic_load(abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) { ok = false; break; }
+        if (aborted(abort)) { ok = false; break; }
         if (n >= kSpinLimit) {
-            __hip_atomic_store(abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            set_abort(abort);
             ok = false;
             break;
         }
@@ -613,18 +627,87 @@ __device__ __forceinline__ bool wait_at_least(const uint32_t* p, uint32_t want, 
     asm volatile("" ::: "memory");
     return ok;
 }
-// set a flag / counter once this wave's earlier stores (or the loads whose values the
-// caller consumed) have completed
+// set a counter once the loads whose values the caller consumed have completed
 __device__ __forceinline__ void post(uint32_t* p, uint32_t v) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     asm volatile("" ::: "memory");
 }
+// the index party's loads of shares o0 .. o0 + nb - 1 (party index + o) of this step
+struct ShareBatch {
+    u32x4 v[kBatch][2];
+};
+__device__ __forceinline__ void load_shares(ShareBatch& sb, const PSync& ps, uint32_t slot, uint32_t k,
+                                            uint32_t index, uint32_t o0, uint32_t nb, uint32_t vo, uint32_t so) {
+    const uint32_t polyB = kN * 4u;
+#pragma unroll
+    for (uint32_t b = 0; b < kBatch; ++b) {
+        if (b < nb) {
+            const uint32_t o = o0 + b, u = index + o < k ? index + o : index + o - k;
+#pragma unroll
+            for (int g = 0; g < 2; ++g)
+                sb.v[b][g] = __builtin_amdgcn_raw_buffer_load_b128(ps.rsv, vo, (slot * k + u) * polyB + so +
+                                                                   (uint32_t)g * 1024u, kSysCoherent);
+        }
+    }
+}
+// check the batch's tags (reloading until every word of the wave carries this step's),
+// then add its shares into sum ([0, 2Q))
+__device__ __forceinline__ void take_shares(ShareBatch& sb, const PSync& ps, uint32_t slot, uint32_t k,
+                                            uint32_t index, uint32_t o0, uint32_t nb, uint32_t vo, uint32_t so,
+                                            uint32_t tag, uint32_t Q, uint32_t (&sum)[kR]) {
+    for (uint32_t n = 0;; ++n) {
+        bool ok = true;
+#pragma unroll
+        for (uint32_t b = 0; b < kBatch; ++b)
+            if (b < nb)
+#pragma unroll
+                for (int g = 0; g < 2; ++g)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) ok = ok && (sb.v[b][g][e] >> 28) == tag;
+        if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;   // wave-uniform
+        if (aborted(ps.abort)) break;
+        if (n >= kSpinLimit) {
+            set_abort(ps.abort);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+        asm volatile("" ::: "memory");
+        load_shares(sb, ps, slot, k, index, o0, nb, vo, so);
+    }
+#pragma unroll
+    for (uint32_t b = 0; b < kBatch; ++b)
+        if (b < nb)
+#pragma unroll
+            for (int g = 0; g < 2; ++g)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const uint32_t y = sum[4 * g + e] + (sb.v[b][g][e] & 0x0fffffffu);
+                    sum[4 * g + e] = min(y, y - 2u * Q);
+                }
+}
 
-// one later step (rel = steps since the launch's first) of party ps.party of gate ps.gate
+// publish this wave's tagged share of step rel in its slot (system-coherent stores)
+__device__ __forceinline__ void put_share(const PSync& ps, const uint32_t (&sv)[kR], uint32_t slot, uint32_t k,
+                                          uint32_t t, uint32_t tag, uint32_t vo, uint32_t so) {
+    const uint32_t polyB = kN * 4u, tg = tag << 28;
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+        __builtin_amdgcn_raw_buffer_store_b128(
+            u32x4{sv[4 * g] | tg, sv[4 * g + 1] | tg, sv[4 * g + 2] | tg, sv[4 * g + 3] | tg}, ps.rsv, vo,
+            (slot * k + t) * polyB + so + (uint32_t)g * 1024u, kSysCoherent);
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_nop 1");   // store-data hazard (bstore4)
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// one later step (rel = steps since the launch's first) of party ps.party of gate ps.gate;
+// takeover: the index party of this step was not the previous step's
 template <int DG, int METHOD>
 __device__ __forceinline__ void quadp_step(const StepArgs& a, const Ctx& s0, uint32_t& xs, const PSync& ps,
-                                           uint32_t rel) {
+                                           uint32_t rel, bool takeover) {
     constexpr bool C = true, FIRST = false;
     constexpr bool kPf = MKACC_QUAD_PF;
     Ctx s = s0;
@@ -645,19 +728,29 @@ __device__ __forceinline__ void quadp_step(const StepArgs& a, const Ctx& s0, uin
                   l * 16u,
                   q * 2048u};
     const uint32_t Q = s.m.Q;
+    const uint32_t slot = rel % kSlots, tag = share_tag(rel);
+    const bool is_index = t == index;
+    ShareBatch sb;
+    const uint32_t nb0 = is_index ? min(k - 1u, kBatch) : 0u;
     uint32_t sv[kR];
 #pragma unroll
     for (int r = 0; r < kR; ++r) sv[r] = 0;
     {   // party t's pass: acc_out[t] and its sv share
         uint32_t x[kR], st[kR];
         QKeys<DG, METHOD, FIRST> kk;
-        if (kPf) issue_keys<DG, METHOD, FIRST, false>(kk, rs, t);
+        // loads in the order they are needed (vector loads return in order): the party's
+        // accumulator for the rotation, then -- the index party -- the first batch of the
+        // others' shares, in flight across the pass, then the keys for the MAC
 #pragma unroll
         for (int g = 0; g < 2; ++g) {
             const u32x4 v = bload4(rs.rin, rs.vo, t * polyB + rs.so + (uint32_t)g * 1024u);
 #pragma unroll
             for (int e = 0; e < 4; ++e) st[4 * g + e] = v[e];
         }
+        asm volatile("" ::: "memory");
+        if (is_index) load_shares(sb, ps, slot, k, index, 1u, nb0, rs.vo, rs.so);
+        asm volatile("" ::: "memory");
+        if (kPf) issue_keys<DG, METHOD, FIRST, false>(kk, rs, t);
 #pragma unroll
         for (int r = 0; r < kR; ++r) x[r] = mul_shoup_lazy(st[r], mp.at(s.psi, r), Q);   // xzw.cpp:336-338
         vcc_fence();
@@ -667,43 +760,32 @@ __device__ __forceinline__ void quadp_step(const StepArgs& a, const Ctx& s0, uin
         if (!kPf) issue_keys<DG, METHOD, FIRST, false>(kk, rs, t);
         mac_q<DG, METHOD, FIRST, false>(s, rs, kk, G, st, sv, mp, mn, t);
     }
-    const uint32_t slot = rel % kSlots;
-    if (t != index) {
-        // publish the share once the index party has read what the slot held
+    if (!is_index) {
+        // publish the tagged share once the index party has taken what the slot held
         if (rel + 1u > kSlots) wait_at_least(ps.used + q, rel + 1u - kSlots, ps.abort);
-#pragma unroll
-        for (int g = 0; g < 2; ++g) {
-            __builtin_amdgcn_raw_buffer_store_b128(u32x4{sv[4 * g], sv[4 * g + 1], sv[4 * g + 2], sv[4 * g + 3]},
-                                                   ps.rsv, rs.vo, (slot * k + t) * polyB + rs.so + (uint32_t)g * 1024u,
-                                                   kSysCoherent);
-            __builtin_amdgcn_sched_barrier(0);
-            asm volatile("s_nop 1");   // store-data hazard (bstore4)
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        post(ps.flag + t * 4u + q, rel + 1u);
+        put_share(ps, sv, slot, k, t, tag, rs.vo, rs.so);
         return;
     }
-    // the index party: sumV = its own share + the others', then the f-part
+    // the index party: sumV = its own share + the others', then the f-part.  Taking over
+    // from another party, it first waits for the ring to hold nothing older than rel - kSlots
+    // (as index of the previous step it posted used = rel itself)
+    if (takeover) {
+        // the batch loaded before the pass may hold a share from 2 kSlots steps back
+        // (same tag): load it again once the ring is known to be recent
+        if (rel + 1u > kSlots) wait_at_least(ps.used + q, rel + 1u - kSlots, ps.abort);
+        load_shares(sb, ps, slot, k, index, 1u, nb0, rs.vo, rs.so);
+    }
     uint32_t x[kR];
 #pragma unroll
     for (int r = 0; r < kR; ++r) x[r] = sv[r];
+    take_shares(sb, ps, slot, k, index, 1u, nb0, rs.vo, rs.so, tag, Q, x);
 #pragma unroll 1
-    for (uint32_t o = 1; o < k; ++o) {
-        const uint32_t u = index + o < k ? index + o : index + o - k;
-        wait_at_least(ps.flag + u * 4u + q, rel + 1u, ps.abort);
-#pragma unroll
-        for (int g = 0; g < 2; ++g) {
-            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(
-                ps.rsv, rs.vo, (slot * k + u) * polyB + rs.so + (uint32_t)g * 1024u, kSysCoherent);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const uint32_t y = x[4 * g + e] + v[e];   // shares and sums in [0, 2Q)
-                x[4 * g + e] = min(y, y - 2u * Q);
-            }
-        }
+    for (uint32_t o0 = 1u + kBatch; o0 < k; o0 += kBatch) {
+        const uint32_t nb = min(k - o0, kBatch);
+        load_shares(sb, ps, slot, k, index, o0, nb, rs.vo, rs.so);
+        take_shares(sb, ps, slot, k, index, o0, nb, rs.vo, rs.so, tag, Q, x);
     }
     vcc_fence();
-    post(ps.used + q, rel + 1u);   // the shares have landed: the slots are free
     {
         uint32_t st[kR];
         QKeys<DG, METHOD, FIRST> kk;
@@ -715,14 +797,34 @@ __device__ __forceinline__ void quadp_step(const StepArgs& a, const Ctx& s0, uin
 #pragma unroll
             for (int e = 0; e < 4; ++e) st[4 * g + e] = v[e];
         }
+        // every party writes every step's slot: its own share, issued behind the f-part's
+        // loads (vmcnt counts stores too, in order) so no wait before the MAC covers the
+        // write-through store
+        put_share(ps, sv, slot, k, t, tag, rs.vo, rs.so);
         uint32_t G[DG][kR];
         digits_q<DG, C>(s, x, G, xs);
         vcc_fence();
         if (!kPf) issue_keys<DG, METHOD, FIRST, true>(kk, rs, index);
         mac_q<DG, METHOD, FIRST, true>(s, rs, kk, G, st, sv, mp, mn, index);
     }
+    // the shares have landed and its own is written (long since, behind the f-part: the
+    // wait for the write-through store is off the critical path)
+    post(ps.used + q, rel + 1u);
 }
 
+}  // namespace quad
+
+// Zeroes the synchronisation area before a party-parallel launch with system-coherent
+// stores: a zeroed slot must read as "no share" through the whole launch, and an
+// ordinary fill could leave dirty L2 lines whose later write-back lands on top of a
+// share written through to memory (the shares bypass the L2s).
+__global__ void psync_clear_kernel(uint32_t* p, uint32_t vec4s) {
+    const __amdgpu_buffer_rsrc_t r = make_rsrc(p, vec4s * 16u);
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < vec4s; i += gridDim.x * blockDim.x)
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, r, i * 16u, 0, quad::kSysCoherent);
+}
+
+namespace quad {
 template <bool LDSTAB>
 __device__ __forceinline__ Ctx make_ctx(const StepArgs& a, uint32_t* smem, const uint32_t* qimg) {
     Ctx s;
@@ -811,7 +913,8 @@ __global__ __launch_bounds__(256, 1) void mk_quadp_run_kernel(StepArgs a, LatdRu
     uint32_t xs = 0;
 #pragma unroll 1
     for (uint32_t t = r.t0; t < r.t1; ++t) {
-        quad::quadp_step<DG, METHOD>(run_args(a, r, t), s, xs, ps, t - r.t0);
+        // the index party changes at t = u n (run_args: index = t / n)
+        quad::quadp_step<DG, METHOD>(run_args(a, r, t), s, xs, ps, t - r.t0, t % r.n == 0u);
         vcc_fence();   // the loop branch follows the step's last reductions
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
