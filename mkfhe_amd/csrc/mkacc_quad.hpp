@@ -571,8 +571,8 @@ __device__ __forceinline__ void quad_step(const StepArgs& a, const Ctx& s0, uint
 // index party loads the shares without a flag round trip -- the first batch before its
 // own pass, checked after it -- and reloads only what is not there yet.  One counter
 // per wave, `used`, orders the ring: the index party's wave q posts rel + 1 once it has
-// taken step rel's shares and written its own share of rel to its slot (every party
-// writes every step's slot, so no slot keeps a share from 8 steps back); a writer
+// taken step rel's shares (and, in the last kSlots steps of its turn as index, written
+// its own share of rel to its slot, so no slot keeps a share from 8 steps back); a writer
 // waits for used >= rel + 1 - kSlots before reusing a slot, and a party that takes over
 // as index waits for the same before (re)loading, so every slot it reads holds step rel
 // or rel - kSlots, whose tags differ (tools/quadp_protocol.py checks this under random
@@ -704,10 +704,11 @@ __device__ __forceinline__ void put_share(const PSync& ps, const uint32_t (&sv)[
 }
 
 // one later step (rel = steps since the launch's first) of party ps.party of gate ps.gate;
-// takeover: the index party of this step was not the previous step's
+// takeover: the index party of this step was not the previous step's; last: this step
+// is one of the last kSlots of the index party's turn
 template <int DG, int METHOD>
 __device__ __forceinline__ void quadp_step(const StepArgs& a, const Ctx& s0, uint32_t& xs, const PSync& ps,
-                                           uint32_t rel, bool takeover) {
+                                           uint32_t rel, bool takeover, bool last) {
     constexpr bool C = true, FIRST = false;
     constexpr bool kPf = MKACC_QUAD_PF;
     Ctx s = s0;
@@ -797,10 +798,11 @@ __device__ __forceinline__ void quadp_step(const StepArgs& a, const Ctx& s0, uin
 #pragma unroll
             for (int e = 0; e < 4; ++e) st[4 * g + e] = v[e];
         }
-        // every party writes every step's slot: its own share, issued behind the f-part's
-        // loads (vmcnt counts stores too, in order) so no wait before the MAC covers the
+        // the index party refreshes its slots in the last kSlots steps of its turn (a share
+        // of its last turn as writer could alias the tag later): issued behind the f-part's
+        // loads (vmcnt counts stores too, in order), so no wait before the MAC covers the
         // write-through store
-        put_share(ps, sv, slot, k, t, tag, rs.vo, rs.so);
+        if (last) put_share(ps, sv, slot, k, t, tag, rs.vo, rs.so);
         uint32_t G[DG][kR];
         digits_q<DG, C>(s, x, G, xs);
         vcc_fence();
@@ -914,7 +916,8 @@ __global__ __launch_bounds__(256, 1) void mk_quadp_run_kernel(StepArgs a, LatdRu
 #pragma unroll 1
     for (uint32_t t = r.t0; t < r.t1; ++t) {
         // the index party changes at t = u n (run_args: index = t / n)
-        quad::quadp_step<DG, METHOD>(run_args(a, r, t), s, xs, ps, t - r.t0, t % r.n == 0u);
+        quad::quadp_step<DG, METHOD>(run_args(a, r, t), s, xs, ps, t - r.t0, t % r.n == 0u,
+                                     (t + quad::kSlots) / r.n != t / r.n);
         vcc_fence();   // the loop branch follows the step's last reductions
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }

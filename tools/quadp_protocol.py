@@ -11,11 +11,12 @@ step a party runs its pass, then:
     flight across the pass); on taking over from another party, waits for used >= rel +
     1 - SLOTS and loads them again; takes the shares of rel, accepting a slot only when
     its tag equals 1 + rel mod 8 (zeroed slots never match) and reloading the others;
-    writes its own share to its slot; posts used = rel + 1; goes on to rel + 1.
+    in the last SLOTS steps of its turn writes its own share to its slot; posts used =
+    rel + 1; goes on to rel + 1.
 
 Random schedules (one enabled action at a time) must finish every step, never accept
 a share of another step (a tag alias), and keep `used` monotonic.  The same model
-with the index's own slot write, the takeover wait or the reload after it removed
+with the index's own slot writes, the takeover wait or the reload after it removed
 finds the stale-share failures that the first GPU runs of the tagged ring hit.
 
     python tools/quadp_protocol.py      # all checks; exit status 0 when clean
@@ -79,7 +80,7 @@ def run(k: int, n: int, seed: int, own_write: bool = True, takeover_wait: bool =
                     return f"k={k} n={n} seed={seed}: step {r} took shares of steps {got}"
                 if used > r + 1:
                     return f"k={k} n={n} seed={seed}: used went back from {used} to {r + 1}"
-                if own_write:
+                if own_write and index(r + SLOTS) != w:
                     slot[(r % SLOTS, w)] = r
                 used = r + 1
             rel[w] += 1
