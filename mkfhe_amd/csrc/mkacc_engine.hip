@@ -369,15 +369,28 @@ bool use_lat(const mkacc_ctx* c, size_t B) {
     return B <= (size_t)c->cus * (kLdsPerCu / lat_lds_bytes(c->p.k));
 }
 
-// The party-parallel form (mk_quadp_run_kernel: a workgroup per party, the steps after
-// the first) needs all B k workgroups resident, one per CU (a cooperative launch).  It
-// is the default wherever it fits: STD128_MKNTRU one gate 24.1 -> 17.1 ms, B = 128
-// 5.24 k -> 7.30 k gates/s; STD128_MKNTRU_3 one gate 319.5 -> 95.2 ms, B = 32 101 ->
-// 340 gates/s (profiles/r6/v16_ab_*).  MKACC_QUAD=1 keeps one workgroup per gate.
-bool use_quadp(const mkacc_ctx* c, size_t B) {
+// The party-parallel form (mk_quadp_run_kernel: each gate's parties spread over G >= 2
+// workgroups, one per CU, the steps after the first) needs all B G workgroups resident
+// (a cooperative launch): G = k where B k <= CUs, fewer -- ceil(k / G) parties each --
+// for larger batches up to CUs / 2 gates.  It is the default wherever it fits:
+// STD128_MKNTRU one gate 24.1 -> 17.1 ms, B = 128 5.24 k -> 7.30 k gates/s;
+// STD128_MKNTRU_3 one gate 319.5 -> 95.2 ms, B = 32 101 -> 340 gates/s
+// (profiles/r6/v16_ab_*).  MKACC_QUAD=1 keeps one workgroup per gate.
+struct QuadpShape {
+    uint32_t groups = 0, ppw = 0;   // workgroups per gate, parties per workgroup
+};
+QuadpShape quadp_shape(const mkacc_ctx* c, size_t B) {
+    const uint32_t k = c->p.k;
     // shares carry their step tag in bits 28..31: residues below 2Q < 2^28
-    return c->p.k >= 2 && B * c->p.k <= (size_t)c->cus && c->p.k * c->p.n >= 2 && c->p.Q < (1ull << 27);
+    if (k < 2 || B == 0 || k * c->p.n < 2 || c->p.Q >= (1ull << 27)) return {};
+    const size_t gmax = std::min<size_t>(k, (size_t)c->cus / B);
+    if (gmax < 2) return {};
+    QuadpShape sh;
+    sh.ppw = (uint32_t)((k + gmax - 1) / gmax);
+    sh.groups = (k + sh.ppw - 1) / sh.ppw;
+    return sh;
 }
+bool use_quadp(const mkacc_ctx* c, size_t B) { return quadp_shape(c, B).groups >= 2; }
 
 // Small batches of at most one gate per CU take mk_quad_kernel (every polynomial
 // spread over the four waves of the gate's workgroup, mkacc_quad.hpp) for every k and
@@ -428,7 +441,7 @@ int ensure_ws(mkacc_ctx* c, size_t B) {
 }
 // the party-parallel kernel's synchronisation area for B gates
 int ensure_psync(mkacc_ctx* c, size_t B) {
-    const size_t w = quad::psync_words(B, c->p.k);
+    const size_t w = quad::psync_words(B, quadp_shape(c, B).groups);
     if (w <= c->psync_words) return MKACC_OK;
     if (c->d_psync) HIP_TRY(hipFree(c->d_psync));
     c->d_psync = nullptr;
@@ -546,12 +559,13 @@ struct StepChain {
         if (quad == 3) {
             // every workgroup of the batch resident at once: the cooperative launch refuses
             // a grid the device cannot hold instead of leaving waits without a producer
-            const uint32_t v4 = (uint32_t)(quad::psync_words(Bh, c->p.k) / 4);
+            const QuadpShape sh = quadp_shape(c, Bh);
+            const uint32_t v4 = (uint32_t)(quad::psync_words(Bh, sh.groups) / 4);
             hipLaunchKernelGGL(psync_clear_kernel, dim3(std::min<uint32_t>((v4 + 255) / 256, 1024u)), dim3(256), 0, st,
                                c->d_psync, v4);
-            QuadArgs qa{c->d_qimg, c->d_psync, c->d_bad + 2};
+            QuadArgs qa{c->d_qimg, c->d_psync, c->d_bad + 2, sh.groups, sh.ppw};
             void* args[] = {(void*)&a, (void*)&r, (void*)&qa};
-            if (hipLaunchCooperativeKernel(fn, dim3((unsigned)(Bh * c->p.k)), dim3(64 * waves), args,
+            if (hipLaunchCooperativeKernel(fn, dim3((unsigned)(Bh * sh.groups)), dim3(64 * waves), args,
                                            (unsigned)quad_lds(quad), st) != hipSuccess)
                 return false;
             c->psync_pending = true;

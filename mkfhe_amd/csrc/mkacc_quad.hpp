@@ -583,23 +583,27 @@ constexpr uint32_t kBatch = 4;              // shares per load batch of the inde
 constexpr uint32_t kSpinLimit = 1u << 20;   // polls of ~1 us: far beyond any step
 constexpr int kSysCoherent = 1 | 16;        // buffer cache policy sc0 | sc1
 struct PSync {
-    uint32_t* used;    // this gate's [4]: steps whose shares wave q of the index party has taken
-    __amdgpu_buffer_rsrc_t rsv;   // this gate's [kSlots][k][N] tagged sv shares, C4 order
+    uint32_t* used;    // this gate's [4]: steps whose shares wave q of the index workgroup has taken
+    __amdgpu_buffer_rsrc_t rsv;   // this gate's [kSlots][groups][N] tagged sv shares, C4 order
     uint32_t* abort;
-    uint32_t gate, party;
+    uint32_t gate, wg;            // this workgroup's gate and its place among the gate's
+    uint32_t groups, ppw;         // workgroups per gate; parties per workgroup (wg owns
+                                  // parties wg ppw .. wg ppw + ppw - 1)
 };
-// words of the synchronisation area for B gates of k parties: the counters, then the
+// words of the synchronisation area for B gates of G workgroups: the counters, then the
 // 16-byte aligned slot ring (all zeroed before every launch)
 __host__ __device__ constexpr size_t psync_counter_words(size_t B) { return (B * 4 + 3) & ~size_t(3); }
-__host__ __device__ constexpr size_t psync_words(size_t B, size_t k) {
-    return psync_counter_words(B) + B * kSlots * k * (size_t)kN;
+__host__ __device__ constexpr size_t psync_words(size_t B, size_t G) {
+    return psync_counter_words(B) + B * kSlots * G * (size_t)kN;
 }
-__device__ __forceinline__ PSync make_psync(uint32_t* sync, uint32_t* abort, uint32_t B, uint32_t k) {
+__device__ __forceinline__ PSync make_psync(uint32_t* sync, uint32_t* abort, uint32_t B, uint32_t G, uint32_t ppw) {
     PSync p;
-    p.gate = __builtin_amdgcn_readfirstlane(blockIdx.x / k);
-    p.party = __builtin_amdgcn_readfirstlane(blockIdx.x - p.gate * k);
+    p.gate = __builtin_amdgcn_readfirstlane(blockIdx.x / G);
+    p.wg = __builtin_amdgcn_readfirstlane(blockIdx.x - p.gate * G);
+    p.groups = G;
+    p.ppw = ppw;
     p.used = sync + p.gate * 4;
-    p.rsv = make_rsrc(sync + psync_counter_words(B) + (size_t)p.gate * kSlots * k * kN, kSlots * k * kN * 4u);
+    p.rsv = make_rsrc(sync + psync_counter_words(B) + (size_t)p.gate * kSlots * G * kN, kSlots * G * kN * 4u);
     p.abort = abort;
     return p;
 }
@@ -703,9 +707,10 @@ __device__ __forceinline__ void put_share(const PSync& ps, const uint32_t (&sv)[
     }
 }
 
-// one later step (rel = steps since the launch's first) of party ps.party of gate ps.gate;
-// takeover: the index party of this step was not the previous step's; last: this step
-// is one of the last kSlots of the index party's turn
+// one later step (rel = steps since the launch's first) of workgroup ps.wg of gate
+// ps.gate: the passes of its parties (the index party's last), then -- the index
+// workgroup -- the f-part.  takeover: the index workgroup of this step was not the
+// previous step's; last: this step is one of the last kSlots of the index workgroup's turn
 template <int DG, int METHOD>
 __device__ __forceinline__ void quadp_step(const StepArgs& a, const Ctx& s0, uint32_t& xs, const PSync& ps,
                                            uint32_t rel, bool takeover, bool last) {
@@ -713,7 +718,7 @@ __device__ __forceinline__ void quadp_step(const StepArgs& a, const Ctx& s0, uin
     constexpr bool kPf = MKACC_QUAD_PF;
     Ctx s = s0;
     const uint32_t l = s.l, q = s.q;
-    const uint32_t gate = ps.gate, t = ps.party;
+    const uint32_t gate = ps.gate, w = ps.wg, G = ps.groups;
     const uint32_t c = __builtin_amdgcn_readfirstlane(a.cvals[gate]);
     const uint32_t cneg = (2u * kN - c) & (2u * kN - 1u);
     const uint32_t k = a.k, index = a.index;
@@ -730,61 +735,66 @@ __device__ __forceinline__ void quadp_step(const StepArgs& a, const Ctx& s0, uin
                   q * 2048u};
     const uint32_t Q = s.m.Q;
     const uint32_t slot = rel % kSlots, tag = share_tag(rel);
-    const bool is_index = t == index;
+    const uint32_t lo = w * ps.ppw, cnt = min(k, lo + ps.ppw) - lo, iw = index / ps.ppw;
+    const bool is_index = w == iw;
+    // pass order lo + (base - lo + j) mod cnt, j = 1 .. cnt: the index party last
+    const uint32_t base = is_index ? index : lo + cnt - 1u;
     ShareBatch sb;
-    const uint32_t nb0 = is_index ? min(k - 1u, kBatch) : 0u;
-    uint32_t sv[kR];
+    const uint32_t nb0 = is_index ? min(G - 1u, kBatch) : 0u;
+    uint32_t sv[kR];   // the workgroup's share: redc-summed over its parties' passes (mac_q)
 #pragma unroll
     for (int r = 0; r < kR; ++r) sv[r] = 0;
-    {   // party t's pass: acc_out[t] and its sv share
+#pragma unroll 1
+    for (uint32_t j = 1; j <= cnt; ++j) {   // party u's pass: acc_out[u] and its sv share
+        const uint32_t o = base - lo + j, u = __builtin_amdgcn_readfirstlane(lo + (o < cnt ? o : o % cnt));
         uint32_t x[kR], st[kR];
         QKeys<DG, METHOD, FIRST> kk;
         // loads in the order they are needed (vector loads return in order): the party's
         // accumulator for the rotation, then -- the index party -- the first batch of the
-        // others' shares, in flight across the pass, then the keys for the MAC
+        // other workgroups' shares, in flight across the pass, then the keys for the MAC
 #pragma unroll
         for (int g = 0; g < 2; ++g) {
-            const u32x4 v = bload4(rs.rin, rs.vo, t * polyB + rs.so + (uint32_t)g * 1024u);
+            const u32x4 v = bload4(rs.rin, rs.vo, u * polyB + rs.so + (uint32_t)g * 1024u);
 #pragma unroll
             for (int e = 0; e < 4; ++e) st[4 * g + e] = v[e];
         }
         asm volatile("" ::: "memory");
-        if (is_index) load_shares(sb, ps, slot, k, index, 1u, nb0, rs.vo, rs.so);
+        if (is_index && j == cnt) load_shares(sb, ps, slot, G, iw, 1u, nb0, rs.vo, rs.so);
         asm volatile("" ::: "memory");
-        if (kPf) issue_keys<DG, METHOD, FIRST, false>(kk, rs, t);
+        if (kPf) issue_keys<DG, METHOD, FIRST, false>(kk, rs, u);
 #pragma unroll
         for (int r = 0; r < kR; ++r) x[r] = mul_shoup_lazy(st[r], mp.at(s.psi, r), Q);   // xzw.cpp:336-338
         vcc_fence();
-        uint32_t G[DG][kR];
-        digits_q<DG, C>(s, x, G, xs);
+        uint32_t Gd[DG][kR];
+        digits_q<DG, C>(s, x, Gd, xs);
         vcc_fence();
-        if (!kPf) issue_keys<DG, METHOD, FIRST, false>(kk, rs, t);
-        mac_q<DG, METHOD, FIRST, false>(s, rs, kk, G, st, sv, mp, mn, t);
+        if (!kPf) issue_keys<DG, METHOD, FIRST, false>(kk, rs, u);
+        mac_q<DG, METHOD, FIRST, false>(s, rs, kk, Gd, st, sv, mp, mn, u);
     }
     if (!is_index) {
-        // publish the tagged share once the index party has taken what the slot held
+        // publish the tagged share once the index workgroup has taken what the slot held
         if (rel + 1u > kSlots) wait_at_least(ps.used + q, rel + 1u - kSlots, ps.abort);
-        put_share(ps, sv, slot, k, t, tag, rs.vo, rs.so);
+        put_share(ps, sv, slot, G, w, tag, rs.vo, rs.so);
         return;
     }
-    // the index party: sumV = its own share + the others', then the f-part.  Taking over
-    // from another party, it first waits for the ring to hold nothing older than rel - kSlots
-    // (as index of the previous step it posted used = rel itself)
+    // the index workgroup: sumV = its own share + the others', then the f-part.  Taking
+    // over from another workgroup, it first waits for the ring to hold nothing older than
+    // rel - kSlots (as index of the previous step it posted used = rel itself)
     if (takeover) {
         // the batch loaded before the pass may hold a share from 2 kSlots steps back
         // (same tag): load it again once the ring is known to be recent
         if (rel + 1u > kSlots) wait_at_least(ps.used + q, rel + 1u - kSlots, ps.abort);
-        load_shares(sb, ps, slot, k, index, 1u, nb0, rs.vo, rs.so);
+        load_shares(sb, ps, slot, G, iw, 1u, nb0, rs.vo, rs.so);
     }
     uint32_t x[kR];
 #pragma unroll
     for (int r = 0; r < kR; ++r) x[r] = sv[r];
-    take_shares(sb, ps, slot, k, index, 1u, nb0, rs.vo, rs.so, tag, Q, x);
+    take_shares(sb, ps, slot, G, iw, 1u, nb0, rs.vo, rs.so, tag, Q, x);
 #pragma unroll 1
-    for (uint32_t o0 = 1u + kBatch; o0 < k; o0 += kBatch) {
-        const uint32_t nb = min(k - o0, kBatch);
-        load_shares(sb, ps, slot, k, index, o0, nb, rs.vo, rs.so);
-        take_shares(sb, ps, slot, k, index, o0, nb, rs.vo, rs.so, tag, Q, x);
+    for (uint32_t o0 = 1u + kBatch; o0 < G; o0 += kBatch) {
+        const uint32_t nb = min(G - o0, kBatch);
+        load_shares(sb, ps, slot, G, iw, o0, nb, rs.vo, rs.so);
+        take_shares(sb, ps, slot, G, iw, o0, nb, rs.vo, rs.so, tag, Q, x);
     }
     vcc_fence();
     {
@@ -798,16 +808,16 @@ __device__ __forceinline__ void quadp_step(const StepArgs& a, const Ctx& s0, uin
 #pragma unroll
             for (int e = 0; e < 4; ++e) st[4 * g + e] = v[e];
         }
-        // the index party refreshes its slots in the last kSlots steps of its turn (a share
-        // of its last turn as writer could alias the tag later): issued behind the f-part's
-        // loads (vmcnt counts stores too, in order), so no wait before the MAC covers the
-        // write-through store
-        if (last) put_share(ps, sv, slot, k, t, tag, rs.vo, rs.so);
-        uint32_t G[DG][kR];
-        digits_q<DG, C>(s, x, G, xs);
+        // the index workgroup refreshes its slots in the last kSlots steps of its turn (a
+        // share of its last turn as writer could alias the tag later): issued behind the
+        // f-part's loads (vmcnt counts stores too, in order), so no wait before the MAC
+        // covers the write-through store
+        if (last) put_share(ps, sv, slot, G, w, tag, rs.vo, rs.so);
+        uint32_t Gd[DG][kR];
+        digits_q<DG, C>(s, x, Gd, xs);
         vcc_fence();
         if (!kPf) issue_keys<DG, METHOD, FIRST, true>(kk, rs, index);
-        mac_q<DG, METHOD, FIRST, true>(s, rs, kk, G, st, sv, mp, mn, index);
+        mac_q<DG, METHOD, FIRST, true>(s, rs, kk, Gd, st, sv, mp, mn, index);
     }
     // the shares have landed and its own is written (long since, behind the f-part: the
     // wait for the write-through store is off the critical path)
@@ -853,8 +863,9 @@ __device__ __forceinline__ Ctx make_ctx(const StepArgs& a, uint32_t* smem, const
 
 struct QuadArgs {
     const uint32_t* qimg;   // TF, TI, TW tables (mkacc_ctx::d_qimg), 3N pairs
-    uint32_t* sync;         // mk_quadp_run_kernel: flags, counters and sv slots (quad::psync_words)
+    uint32_t* sync;         // mk_quadp_run_kernel: counters and sv slots (quad::psync_words)
     uint32_t* abort;        // mk_quadp_run_kernel: non-zero after a synchronisation timeout
+    uint32_t groups, ppw;   // mk_quadp_run_kernel: workgroups per gate, parties per workgroup
 };
 
 // one accumulator step (the first, KDM, or any other) for B gates, one workgroup each.
@@ -911,13 +922,14 @@ __global__ __launch_bounds__(256, 1) void mk_quadp_run_kernel(StepArgs a, LatdRu
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     quad::load_tables<true>(smem, a.img, qa.qimg);
     const quad::Ctx s = quad::make_ctx<true>(a, smem, qa.qimg);
-    const quad::PSync ps = quad::make_psync(qa.sync, qa.abort, a.B, a.k);
+    const quad::PSync ps = quad::make_psync(qa.sync, qa.abort, a.B, qa.groups, qa.ppw);
     uint32_t xs = 0;
 #pragma unroll 1
     for (uint32_t t = r.t0; t < r.t1; ++t) {
-        // the index party changes at t = u n (run_args: index = t / n)
-        quad::quadp_step<DG, METHOD>(run_args(a, r, t), s, xs, ps, t - r.t0, t % r.n == 0u,
-                                     (t + quad::kSlots) / r.n != t / r.n);
+        // the index workgroup of step t is (t / n) / ppw (run_args: index = t / n)
+        const uint32_t iw = t / r.n / ps.ppw;
+        quad::quadp_step<DG, METHOD>(run_args(a, r, t), s, xs, ps, t - r.t0, (t - 1u) / r.n / ps.ppw != iw,
+                                     (t + quad::kSlots) / r.n / ps.ppw != iw);
         vcc_fence();   // the loop branch follows the step's last reductions
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }

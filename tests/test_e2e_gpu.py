@@ -185,7 +185,7 @@ def test_config3_four_party_mklwe_gates_decrypt_correctly(oracle, monkeypatch):
 @pytest.mark.parametrize("ps,method,seed", [("STD100_MKNTRU_4", 0, 1804), ("STD128_MKNTRU_LWE_4", 2, 1702)])
 def test_sixteen_party_gates(oracle, ps, method, seed):
     """The reference's k = 16 rows (binfhecontext.cpp:129-144) with real seeded keys: a
-    128-gate batch (one gate per workgroup, mk_quad_kernel).  MK-LWE k = 16: the first
+    128-gate batch (the party-parallel kernel, two workgroups of eight parties per gate).  MK-LWE k = 16: the first
     and last gate equal the CPU oracle's full gates bit for bit and every gate decrypts
     to NAND.  MK-NTRU k = 16 (STD100_MKNTRU_4) is the set whose noise shows in the
     restated scheme itself: over the oracle's own gates, 67 of 80 sampled gates on five
@@ -201,7 +201,7 @@ def test_sixteen_party_gates(oracle, ps, method, seed):
     rng = np.random.default_rng(seed)
     B = 128
     m1, m2 = rng.integers(0, 2, B), rng.integers(0, 2, B)
-    assert cc.engine().step_kernel_name(B) == "mk_quad_run_kernel"
+    assert cc.engine().step_kernel_name(B) == "mk_quadp_run_kernel"   # 2 workgroups of 8 parties per gate
     p, bk = cc.params, cc.BTKey
     k, n, _, dg, nk, dks = K.dims(p)
     if method == 0:

@@ -380,6 +380,39 @@ def test_evalacc_quad_kernel(mk, oracle, case, occ, monkeypatch):
     assert np.array_equal(got, exp.astype(np.uint32))
 
 
+# the party-parallel form with several parties per workgroup (B > CUs / k): G = ceil(k /
+# ceil(k / min(k, CUs / B))) workgroups per gate on a 256-CU MI355X
+QUADP_GROUPED = [
+    # method, k, n, q, baseG, B
+    ("XZW", 8, 3, 45181, 1 << 6, 64),      # G = 4, two parties each (config 4 shape, dg = 4)
+    ("XZW_B", 16, 2, 32749, 1 << 7, 40),   # G = 6: five workgroups of 3 parties, one of 1
+    ("XZW", 5, 3, 45181, 1 << 9, 100),     # G = 2: 3 + 2 parties
+    ("XZW_B", 4, 4, 32749, 1 << 9, 128),   # G = 2 (STD100_MKNTRU_LWE_2 shape)
+    ("XZW", 2, 5, 45181, 1 << 7, 128),     # G = k = 2 at B = CUs / 2
+]
+
+
+@pytest.mark.parametrize("case", QUADP_GROUPED, ids=[f"{c[0]}-k{c[1]}-n{c[2]}-B{c[5]}" for c in QUADP_GROUPED])
+def test_evalacc_quadp_grouped(mk, oracle, case):
+    """mk_quadp_run_kernel where a workgroup owns several parties (its passes run one
+    after the other, the index party's last, and it publishes one summed share): every
+    gate of the batch equals the oracle; small n turns the index workgroup over every
+    few steps, including turns shorter than the four-slot ring."""
+    meth, k, n, q, baseG, B = case
+    om = oracle.XZW if meth == "XZW" else oracle.XZW_B
+    em = mk.MKNTRU if meth == "XZW" else mk.MKNTRU_LWE
+    orc, evk, pkey, ct, acc = make_case(oracle, om, k, n, q, baseG, B, seed=k * 7 + n + B)
+    ct[0, 0, 0] = 0
+    ct[-1, k - 1, n - 1] = q - 1 if om == oracle.XZW else 4096
+    exp = orc.evalacc_batch(evk, pkey, ct, acc, 8)
+    eng = mk.MKAccumulatorEngine(mk.make_params(em, k, n, 2048, Q_MK, q, baseG))
+    assert eng.step_kernel_name(B) == "mk_quadp_run_kernel"
+    eng.upload_keys(evk.astype(np.uint32), pkey.astype(np.uint32))
+    got = eng.eval_batch(ct.astype(np.uint32), acc.astype(np.uint32))
+    bad = [b for b in range(B) if not np.array_equal(got[b], exp[b].astype(np.uint32))]
+    assert not bad, bad[:8]
+
+
 @pytest.mark.parametrize("name,B,occ", [("STD128_MKNTRU", 3, "1"), ("STD100_MKNTRU_LWE", 2, "1"),
                                         ("STD100_MKNTRU_LWE_2", 256, "1"), ("STD128_MKNTRU", 3, "3"),
                                         ("STD100_MKNTRU_LWE_2", 64, "3"), ("STD128_MKNTRU_3", 1, "3")])

@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
 """Model check of the party-parallel kernel's share ring (mkacc_quad.hpp, quadp_step).
 
-One gate, k workgroups (parties), steps rel = 0 .. k n - 2 of one launch; the index
-party of step rel is (rel + 1) // n (run_args: index = t / n with t = rel + 1).  Per
-step a party runs its pass, then:
+One gate, k parties on G = ceil(k / ppw) workgroups (workgroup w owns parties
+w ppw .. w ppw + ppw - 1), steps rel = 0 .. k n - 2 of one launch; the index party of
+step rel is (rel + 1) // n (run_args: index = t / n with t = rel + 1) and the index
+workgroup the one owning it.  Per step a workgroup runs its parties' passes, then:
 
   * not the index: waits for used >= rel + 1 - SLOTS, writes its tagged share of rel
     to slot rel % SLOTS, goes on to rel + 1;
@@ -30,26 +31,27 @@ SLOTS, TAGS = 4, 8
 
 
 def run(k: int, n: int, seed: int, own_write: bool = True, takeover_wait: bool = True,
-        reload: bool = True) -> str | None:
+        reload: bool = True, ppw: int = 1) -> str | None:
     rnd = random.Random(seed)
     steps = k * n - 1
-    slot = {}                                 # (slot, party) -> step written
+    slot = {}                                 # (slot, workgroup) -> step written
     used = 0
-    rel = [0] * k
-    phase = ["pass"] * k
-    seen: list[list] = [[] for _ in range(k)]   # the index party's loaded slots
+    groups = -(-k // ppw)
+    rel = [0] * groups
+    phase = ["pass"] * groups
+    seen: list[list] = [[] for _ in range(groups)]   # the index workgroup's loaded slots
 
     def load(w: int, r: int) -> list:
-        return [slot.get((r % SLOTS, u)) for u in range(k) if u != w]
+        return [slot.get((r % SLOTS, u)) for u in range(groups) if u != w]
 
     def index(r: int) -> int:
-        return (r + 1) // n
+        return ((r + 1) // n) // ppw
 
     while True:
         if all(r >= steps for r in rel):
             return None
         moved = False
-        for w in rnd.sample(range(k), k):
+        for w in rnd.sample(range(groups), groups):
             r = rel[w]
             if r >= steps:
                 continue
@@ -91,22 +93,23 @@ def run(k: int, n: int, seed: int, own_write: bool = True, takeover_wait: bool =
             return f"k={k} n={n} seed={seed}: deadlock at steps {rel}, used {used}"
 
 
-def check(seeds: int = 200, **kw) -> list[str]:
+def check(seeds: int = 200, ppws=(1,), **kw) -> list[str]:
     bad = []
     for k in (2, 3, 4, 5, 8, 16):
         for n in (1, 2, 3, 4, 5, 8, 9, 17, 40):
-            if k * n < 2:
-                continue
-            for seed in range(seeds):
-                err = run(k, n, seed, **kw)
-                if err:
-                    bad.append(err)
-                    break
+            for ppw in ppws:
+                if k * n < 2 or -(-k // ppw) < 2:
+                    continue
+                for seed in range(seeds):
+                    err = run(k, n, seed, ppw=ppw, **kw)
+                    if err:
+                        bad.append(err)
+                        break
     return bad
 
 
 def main() -> int:
-    bad = check()
+    bad = check(ppws=(1, 2, 3, 4))
     print(f"quadp share ring: {'clean' if not bad else bad[:3]}")
     weak = [check(seeds=60, own_write=False), check(seeds=60, takeover_wait=False), check(seeds=60, reload=False)]
     print("failing shapes without the index's own slot write / the takeover wait / the reload after it:",
