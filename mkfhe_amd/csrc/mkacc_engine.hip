@@ -155,7 +155,9 @@ const void* quadrun_fn(int dg, int method, int occ) {
         default: return nullptr;
     }
 }
-size_t quad_lds(int occ) { return occ == 2 ? quad::kLdsBytes2 : quad::kLdsBytes; }
+// quad modes (use_quad): 1 one workgroup per gate, 2 the same two per CU, 3 party-parallel,
+// 4 party-parallel two per CU; modes 2 and 4 keep the twiddle tables in HBM
+size_t quad_lds(int mode) { return mode == 2 || mode == 4 ? quad::kLdsBytes2 : quad::kLdsBytes; }
 const void* lat_fn(int dg, int method, bool first) {
     switch (dg) {
         case 2: return mkacc_tu::lat_dg2(method, first);
@@ -379,18 +381,20 @@ bool use_lat(const mkacc_ctx* c, size_t B) {
 struct QuadpShape {
     uint32_t groups = 0, ppw = 0;   // workgroups per gate, parties per workgroup
 };
-QuadpShape quadp_shape(const mkacc_ctx* c, size_t B) {
+// occ: workgroups per CU (2: mk_quadp2_run_kernel, dg <= 4)
+QuadpShape quadp_shape(const mkacc_ctx* c, size_t B, int occ = 1) {
     const uint32_t k = c->p.k;
     // shares carry their step tag in bits 28..31: residues below 2Q < 2^28
     if (k < 2 || B == 0 || k * c->p.n < 2 || c->p.Q >= (1ull << 27)) return {};
-    const size_t gmax = std::min<size_t>(k, (size_t)c->cus / B);
+    if (occ == 2 && c->dg > 4) return {};
+    const size_t gmax = std::min<size_t>(k, (size_t)occ * c->cus / B);
     if (gmax < 2) return {};
     QuadpShape sh;
     sh.ppw = (uint32_t)((k + gmax - 1) / gmax);
     sh.groups = (k + sh.ppw - 1) / sh.ppw;
     return sh;
 }
-bool use_quadp(const mkacc_ctx* c, size_t B) { return quadp_shape(c, B).groups >= 2; }
+bool use_quadp(const mkacc_ctx* c, size_t B, int occ = 1) { return quadp_shape(c, B, occ).groups >= 2; }
 
 // Small batches of at most one gate per CU take mk_quad_kernel (every polynomial
 // spread over the four waves of the gate's workgroup, mkacc_quad.hpp) for every k and
@@ -410,6 +414,7 @@ int use_quad(const mkacc_ctx* c, size_t B) {
     if (c->wide || c->dg < 2 || c->dg > 5 || c->env_quad == 0) return 0;
     if (c->env_quad == 2) return c->dg <= 4 ? 2 : 0;
     if (c->env_quad != 1 && use_quadp(c, B)) return 3;
+    if (c->env_quad == 4 && use_quadp(c, B, 2)) return 4;
     if (B <= (size_t)c->cus) return 1;
     return B <= 4 * (size_t)c->cus && c->dg <= 4 ? 2 : 0;
 }
@@ -420,7 +425,7 @@ size_t step_scratch_words(const mkacc_ctx* c) { return use_dscr(c) ? (size_t)c->
 
 int ensure_psync(mkacc_ctx* c, size_t B);
 int ensure_ws(mkacc_ctx* c, size_t B) {
-    if (use_quad(c, B) == 3) {
+    if (use_quad(c, B) >= 3) {
         const int rc = ensure_psync(c, B);
         if (rc) return rc;
     }
@@ -441,7 +446,8 @@ int ensure_ws(mkacc_ctx* c, size_t B) {
 }
 // the party-parallel kernel's synchronisation area for B gates
 int ensure_psync(mkacc_ctx* c, size_t B) {
-    const size_t w = quad::psync_words(B, quadp_shape(c, B).groups);
+    const int mode = use_quad(c, B);
+    const size_t w = quad::psync_words(B, quadp_shape(c, B, mode == 4 ? 2 : 1).groups);
     if (w <= c->psync_words) return MKACC_OK;
     if (c->d_psync) HIP_TRY(hipFree(c->d_psync));
     c->d_psync = nullptr;
@@ -511,7 +517,7 @@ struct StepChain {
         if (quad) {
             // the first (KDM) step, once per gate, runs the one-workgroup-per-CU form for
             // either occupancy: its four key words per digit do not fit 256 VGPRs at dg = 4
-            const int occ = first ? 1 : quad;
+            const int occ = first ? 1 : quad;   // modes 3 and 4 have no step kernel of their own
             const void* fn = quad_fn((int)c->dg, c->method_class, first, occ);
             if (!fn) return false;
             launch_ptr2(fn, dim3((unsigned)Bh), dim3(64 * quad::kWaves), quad_lds(occ), st, a, QuadArgs{c->d_qimg});
@@ -556,10 +562,10 @@ struct StepChain {
         r.t0 = t0;
         r.t1 = t1;
         r.key2off = c->nk == 2 ? (uint32_t)(c->dg * 2 * kN) : 0u;
-        if (quad == 3) {
+        if (quad >= 3) {
             // every workgroup of the batch resident at once: the cooperative launch refuses
             // a grid the device cannot hold instead of leaving waits without a producer
-            const QuadpShape sh = quadp_shape(c, Bh);
+            const QuadpShape sh = quadp_shape(c, Bh, quad == 4 ? 2 : 1);
             const uint32_t v4 = (uint32_t)(quad::psync_words(Bh, sh.groups) / 4);
             hipLaunchKernelGGL(psync_clear_kernel, dim3(std::min<uint32_t>((v4 + 255) / 256, 1024u)), dim3(256), 0, st,
                                c->d_psync, v4);
@@ -1426,9 +1432,10 @@ int mkacc_create(const mkacc_params* pin, int device, mkacc_ctx** out) {
     c->env_dscr = env_switch("MKACC_DSCR");
     {
         // 0 (no quad kernel), 1 (one workgroup per gate, no party-parallel form),
-        // 2 (two workgroups per CU, any B), 3 / unset (the policy of use_quad)
+        // 2 (two workgroups per CU, any B), 3 / unset (the policy of use_quad), 4 (the
+        // policy with the two-per-CU party-parallel form up to CUs gates)
         const char* e = std::getenv("MKACC_QUAD");
-        c->env_quad = e && *e ? (e[0] == '0' ? 0 : e[0] == '2' ? 2 : e[0] == '3' ? 3 : 1) : -1;
+        c->env_quad = e && *e ? (e[0] == '0' ? 0 : e[0] == '2' ? 2 : e[0] == '3' ? 3 : e[0] == '4' ? 4 : 1) : -1;
     }
     c->dg = dg;
     c->step_ver = step_version((int)dg);
@@ -1618,7 +1625,8 @@ const char* mkacc_step_kernel_name(const mkacc_ctx* c, size_t B) {
     // small batches: the kernel that runs the steps after the first (all but one of
     // the k n steps; the first is one launch of mk_latd_kernel / mk_lat_kernel)
     if (const int qo = use_quad(c, B))
-        return qo == 3 ? "mk_quadp_run_kernel"
+        return qo == 4   ? "mk_quadp2_run_kernel"
+               : qo == 3 ? "mk_quadp_run_kernel"
                : qo == 2 ? (use_run(c, B) ? "mk_quad2_run_kernel" : "mk_quad2_kernel")
                        : (use_run(c, B) ? "mk_quad_run_kernel" : "mk_quad_kernel");
     if (use_lat(c, B)) {

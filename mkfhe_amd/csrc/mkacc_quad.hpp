@@ -579,7 +579,7 @@ __device__ __forceinline__ void quad_step(const StepArgs& a, const Ctx& s0, uint
 // schedules, and that each of the three rules is needed).  Every wait is bounded: a timeout sets *abort, after which no wave waits
 // again (the kernel drains, the engine reports MKACC_E_DEVICE).
 constexpr uint32_t kSlots = 4;
-constexpr uint32_t kBatch = 4;              // shares per load batch of the index party
+constexpr uint32_t kBatch = 4;              // shares per load batch of the index workgroup
 constexpr uint32_t kSpinLimit = 1u << 20;   // polls of ~1 us: far beyond any step
 constexpr int kSysCoherent = 1 | 16;        // buffer cache policy sc0 | sc1
 struct PSync {
@@ -638,14 +638,16 @@ __device__ __forceinline__ void post(uint32_t* p, uint32_t v) {
     asm volatile("" ::: "memory");
 }
 // the index party's loads of shares o0 .. o0 + nb - 1 (party index + o) of this step
+template <uint32_t NB>
 struct ShareBatch {
-    u32x4 v[kBatch][2];
+    u32x4 v[NB][2];
 };
-__device__ __forceinline__ void load_shares(ShareBatch& sb, const PSync& ps, uint32_t slot, uint32_t k,
+template <uint32_t NB>
+__device__ __forceinline__ void load_shares(ShareBatch<NB>& sb, const PSync& ps, uint32_t slot, uint32_t k,
                                             uint32_t index, uint32_t o0, uint32_t nb, uint32_t vo, uint32_t so) {
     const uint32_t polyB = kN * 4u;
 #pragma unroll
-    for (uint32_t b = 0; b < kBatch; ++b) {
+    for (uint32_t b = 0; b < NB; ++b) {
         if (b < nb) {
             const uint32_t o = o0 + b, u = index + o < k ? index + o : index + o - k;
 #pragma unroll
@@ -657,13 +659,14 @@ __device__ __forceinline__ void load_shares(ShareBatch& sb, const PSync& ps, uin
 }
 // check the batch's tags (reloading until every word of the wave carries this step's),
 // then add its shares into sum ([0, 2Q))
-__device__ __forceinline__ void take_shares(ShareBatch& sb, const PSync& ps, uint32_t slot, uint32_t k,
+template <uint32_t NB>
+__device__ __forceinline__ void take_shares(ShareBatch<NB>& sb, const PSync& ps, uint32_t slot, uint32_t k,
                                             uint32_t index, uint32_t o0, uint32_t nb, uint32_t vo, uint32_t so,
                                             uint32_t tag, uint32_t Q, uint32_t (&sum)[kR]) {
     for (uint32_t n = 0;; ++n) {
         bool ok = true;
 #pragma unroll
-        for (uint32_t b = 0; b < kBatch; ++b)
+        for (uint32_t b = 0; b < NB; ++b)
             if (b < nb)
 #pragma unroll
                 for (int g = 0; g < 2; ++g)
@@ -680,7 +683,7 @@ __device__ __forceinline__ void take_shares(ShareBatch& sb, const PSync& ps, uin
         load_shares(sb, ps, slot, k, index, o0, nb, vo, so);
     }
 #pragma unroll
-    for (uint32_t b = 0; b < kBatch; ++b)
+    for (uint32_t b = 0; b < NB; ++b)
         if (b < nb)
 #pragma unroll
             for (int g = 0; g < 2; ++g)
@@ -711,7 +714,7 @@ __device__ __forceinline__ void put_share(const PSync& ps, const uint32_t (&sv)[
 // ps.gate: the passes of its parties (the index party's last), then -- the index
 // workgroup -- the f-part.  takeover: the index workgroup of this step was not the
 // previous step's; last: this step is one of the last kSlots of the index workgroup's turn
-template <int DG, int METHOD>
+template <int DG, int METHOD, uint32_t NB>
 __device__ __forceinline__ void quadp_step(const StepArgs& a, const Ctx& s0, uint32_t& xs, const PSync& ps,
                                            uint32_t rel, bool takeover, bool last) {
     constexpr bool C = true, FIRST = false;
@@ -739,8 +742,8 @@ __device__ __forceinline__ void quadp_step(const StepArgs& a, const Ctx& s0, uin
     const bool is_index = w == iw;
     // pass order lo + (base - lo + j) mod cnt, j = 1 .. cnt: the index party last
     const uint32_t base = is_index ? index : lo + cnt - 1u;
-    ShareBatch sb;
-    const uint32_t nb0 = is_index ? min(G - 1u, kBatch) : 0u;
+    ShareBatch<NB> sb;
+    const uint32_t nb0 = is_index ? min(G - 1u, NB) : 0u;
     uint32_t sv[kR];   // the workgroup's share: redc-summed over its parties' passes (mac_q)
 #pragma unroll
     for (int r = 0; r < kR; ++r) sv[r] = 0;
@@ -791,8 +794,8 @@ __device__ __forceinline__ void quadp_step(const StepArgs& a, const Ctx& s0, uin
     for (int r = 0; r < kR; ++r) x[r] = sv[r];
     take_shares(sb, ps, slot, G, iw, 1u, nb0, rs.vo, rs.so, tag, Q, x);
 #pragma unroll 1
-    for (uint32_t o0 = 1u + kBatch; o0 < G; o0 += kBatch) {
-        const uint32_t nb = min(G - o0, kBatch);
+    for (uint32_t o0 = 1u + NB; o0 < G; o0 += NB) {
+        const uint32_t nb = min(G - o0, NB);
         load_shares(sb, ps, slot, G, iw, o0, nb, rs.vo, rs.so);
         take_shares(sb, ps, slot, G, iw, o0, nb, rs.vo, rs.so, tag, Q, x);
     }
@@ -916,23 +919,37 @@ __global__ __launch_bounds__(256, 2) void mk_quad2_run_kernel(StepArgs a, LatdRu
     quad_run<DG, METHOD, 2>(a, r, qa, smem);
 }
 
-// steps [t0, t1) party-parallel: B k workgroups, all resident (cooperative launch)
-template <int DG, int METHOD>
-__global__ __launch_bounds__(256, 1) void mk_quadp_run_kernel(StepArgs a, LatdRun r, QuadArgs qa) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    quad::load_tables<true>(smem, a.img, qa.qimg);
-    const quad::Ctx s = quad::make_ctx<true>(a, smem, qa.qimg);
+// steps [t0, t1) party-parallel: B G workgroups, all resident (cooperative launch).
+// OCC = 1: tables in LDS, one workgroup per CU (B <= CUs / 2); OCC = 2: tables in HBM,
+// two per CU (mk_quadp2_run_kernel, CUs / 2 < B <= CUs, dg <= 4)
+template <int DG, int METHOD, int OCC>
+__device__ __forceinline__ void quadp_run(const StepArgs& a, const LatdRun& r, const QuadArgs& qa, uint32_t* smem) {
+    quad::load_tables<OCC == 1>(smem, a.img, qa.qimg);
+    const quad::Ctx s = quad::make_ctx<OCC == 1>(a, smem, qa.qimg);
     const quad::PSync ps = quad::make_psync(qa.sync, qa.abort, a.B, qa.groups, qa.ppw);
     uint32_t xs = 0;
 #pragma unroll 1
     for (uint32_t t = r.t0; t < r.t1; ++t) {
         // the index workgroup of step t is (t / n) / ppw (run_args: index = t / n)
         const uint32_t iw = t / r.n / ps.ppw;
-        quad::quadp_step<DG, METHOD>(run_args(a, r, t), s, xs, ps, t - r.t0, (t - 1u) / r.n / ps.ppw != iw,
+        // the two-per-CU form at dg = 4 loads one share at a time (a batch of four would
+        // spill at 256 VGPRs)
+        constexpr uint32_t kNb = OCC == 2 && DG >= 4 ? 1u : quad::kBatch;
+        quad::quadp_step<DG, METHOD, kNb>(run_args(a, r, t), s, xs, ps, t - r.t0, (t - 1u) / r.n / ps.ppw != iw,
                                      (t + quad::kSlots) / r.n / ps.ppw != iw);
         vcc_fence();   // the loop branch follows the step's last reductions
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+}
+template <int DG, int METHOD>
+__global__ __launch_bounds__(256, 1) void mk_quadp_run_kernel(StepArgs a, LatdRun r, QuadArgs qa) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    quadp_run<DG, METHOD, 1>(a, r, qa, smem);
+}
+template <int DG, int METHOD>
+__global__ __launch_bounds__(256, 2) void mk_quadp2_run_kernel(StepArgs a, LatdRun r, QuadArgs qa) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    quadp_run<DG, METHOD, 2>(a, r, qa, smem);
 }
 
 template <int DG>
@@ -953,6 +970,13 @@ const void* pick_quad(int method, bool first, int occ) {
 template <int DG>
 const void* pick_quad_run(int method, int occ) {
     if (occ == 3) return method == XZW ? (const void*)mk_quadp_run_kernel<DG, XZW> : (const void*)mk_quadp_run_kernel<DG, XZW_B>;
+    if (occ == 4) {
+        if constexpr (DG > 4) {
+            return nullptr;
+        } else {
+            return method == XZW ? (const void*)mk_quadp2_run_kernel<DG, XZW> : (const void*)mk_quadp2_run_kernel<DG, XZW_B>;
+        }
+    }
     if (occ == 2) {
         if constexpr (DG > 4) {
             return nullptr;

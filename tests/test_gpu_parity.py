@@ -389,16 +389,23 @@ QUADP_GROUPED = [
     ("XZW", 5, 3, 45181, 1 << 9, 100),     # G = 2: 3 + 2 parties
     ("XZW_B", 4, 4, 32749, 1 << 9, 128),   # G = 2 (STD100_MKNTRU_LWE_2 shape)
     ("XZW", 2, 5, 45181, 1 << 7, 128),     # G = k = 2 at B = CUs / 2
+    # two workgroups per CU (mk_quadp2_run_kernel, MKACC_QUAD=4, CUs / 2 < B <= CUs, dg <= 4)
+    ("XZW", 8, 3, 45181, 1 << 6, 200),     # G = 2, four parties each, dg = 4 (one share per load)
+    ("XZW_B", 4, 4, 32749, 1 << 9, 256),   # G = 2 at B = CUs
+    ("XZW", 2, 5, 45181, 1 << 7, 256),     # G = 2 = k
+    ("XZW", 3, 3, 45181, 1 << 5, 200),     # dg = 5: no two-per-CU form, one workgroup per gate
 ]
 
 
 @pytest.mark.parametrize("case", QUADP_GROUPED, ids=[f"{c[0]}-k{c[1]}-n{c[2]}-B{c[5]}" for c in QUADP_GROUPED])
-def test_evalacc_quadp_grouped(mk, oracle, case):
-    """mk_quadp_run_kernel where a workgroup owns several parties (its passes run one
+def test_evalacc_quadp_grouped(mk, oracle, case, monkeypatch):
+    """mk_quadp_run_kernel (and above CUs / 2 gates mk_quadp2_run_kernel) where a workgroup owns several parties (its passes run one
     after the other, the index party's last, and it publishes one summed share): every
     gate of the batch equals the oracle; small n turns the index workgroup over every
     few steps, including turns shorter than the four-slot ring."""
     meth, k, n, q, baseG, B = case
+    if B > 128:
+        monkeypatch.setenv("MKACC_QUAD", "4")   # the two-per-CU form (opt-in)
     om = oracle.XZW if meth == "XZW" else oracle.XZW_B
     em = mk.MKNTRU if meth == "XZW" else mk.MKNTRU_LWE
     orc, evk, pkey, ct, acc = make_case(oracle, om, k, n, q, baseG, B, seed=k * 7 + n + B)
@@ -406,7 +413,8 @@ def test_evalacc_quadp_grouped(mk, oracle, case):
     ct[-1, k - 1, n - 1] = q - 1 if om == oracle.XZW else 4096
     exp = orc.evalacc_batch(evk, pkey, ct, acc, 8)
     eng = mk.MKAccumulatorEngine(mk.make_params(em, k, n, 2048, Q_MK, q, baseG))
-    assert eng.step_kernel_name(B) == "mk_quadp_run_kernel"
+    want = "mk_quadp_run_kernel" if B <= 128 else "mk_quadp2_run_kernel" if baseG > 1 << 5 else "mk_quad_run_kernel"
+    assert eng.step_kernel_name(B) == want
     eng.upload_keys(evk.astype(np.uint32), pkey.astype(np.uint32))
     got = eng.eval_batch(ct.astype(np.uint32), acc.astype(np.uint32))
     bad = [b for b in range(B) if not np.array_equal(got[b], exp[b].astype(np.uint32))]

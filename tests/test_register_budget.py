@@ -74,6 +74,7 @@ BUDGET = [
     (r"mk_quad2_kernel<[234], [01], false>", 256, 2),  # two workgroups per CU (B <= 4 x CUs, dg <= 4)
     (r"mk_quad2_run_kernel<[234], [01]>", 256, 2),
     (r"mk_quadp_run_kernel<\d, [01]>", 512, 1),          # party-parallel: a workgroup per party and CU
+    (r"mk_quadp2_run_kernel<[234], [01]>", 256, 2),       # party-parallel, two workgroups per CU
     (r"mk_step_kernel<4, 0, false, true>", 256, 2),      # config-4 step (dg = 4, d_i scratch; spill-free since
                                                           # the alternating reload order)
     (r"mk_step_kernel<4, 1, false, false>", 256, 2),     # MK-LWE at dg = 4 (STD128_MKNTRU_LWE_4): keeps the asm
