@@ -568,8 +568,8 @@ __device__ __forceinline__ void quad_step(const StepArgs& a, const Ctx& s0, uint
 // the step at 256 workgroups, where every CU's waits flushed its XCD's L2
 // (profiles/r6/v15).  A share carries its step in the free top bits of every word
 // (a residue below 2Q < 2^28; tag 1 + rel mod 8, a zeroed slot never matches), so the
-// index party loads the shares without a flag round trip -- the first batch before its
-// own pass, checked after it -- and reloads only what is not there yet.  One counter
+// index party loads the shares without a flag round trip, after its own pass, and
+// reloads only what is not there yet.  One counter
 // per wave, `used`, orders the ring: the index party's wave q posts rel + 1 once it has
 // taken step rel's shares (and, in the last kSlots steps of its turn as index, written
 // its own share of rel to its slot, so no slot keeps a share from 8 steps back); a writer
@@ -580,6 +580,13 @@ __device__ __forceinline__ void quad_step(const StepArgs& a, const Ctx& s0, uint
 // again (the kernel drains, the engine reports MKACC_E_DEVICE).
 constexpr uint32_t kSlots = 4;
 constexpr uint32_t kBatch = 4;              // shares per load batch of the index workgroup
+#ifndef MKACC_QUADP_PRELOAD
+// 1: the index workgroup's first share batch in flight across its pass.  Off: the
+// system-coherent loads queued behind the pass's accumulator loads delayed its keys
+// (vector loads return in order): loading after the pass was 1.5-3 % faster at k = 2,
+// 8 and 16 (profiles/r6/v32)
+#define MKACC_QUADP_PRELOAD 0
+#endif
 constexpr uint32_t kSpinLimit = 1u << 20;   // polls of ~1 us: far beyond any step
 constexpr int kSysCoherent = 1 | 16;        // buffer cache policy sc0 | sc1
 struct PSync {
@@ -762,7 +769,7 @@ __device__ __forceinline__ void quadp_step(const StepArgs& a, const Ctx& s0, uin
             for (int e = 0; e < 4; ++e) st[4 * g + e] = v[e];
         }
         asm volatile("" ::: "memory");
-        if (is_index && j == cnt) load_shares(sb, ps, slot, G, iw, 1u, nb0, rs.vo, rs.so);
+        if (MKACC_QUADP_PRELOAD && is_index && j == cnt) load_shares(sb, ps, slot, G, iw, 1u, nb0, rs.vo, rs.so);
         asm volatile("" ::: "memory");
         if (kPf) issue_keys<DG, METHOD, FIRST, false>(kk, rs, u);
 #pragma unroll
@@ -783,10 +790,10 @@ __device__ __forceinline__ void quadp_step(const StepArgs& a, const Ctx& s0, uin
     // the index workgroup: sumV = its own share + the others', then the f-part.  Taking
     // over from another workgroup, it first waits for the ring to hold nothing older than
     // rel - kSlots (as index of the previous step it posted used = rel itself)
-    if (takeover) {
+    if (takeover || !MKACC_QUADP_PRELOAD) {
         // the batch loaded before the pass may hold a share from 2 kSlots steps back
         // (same tag): load it again once the ring is known to be recent
-        if (rel + 1u > kSlots) wait_at_least(ps.used + q, rel + 1u - kSlots, ps.abort);
+        if (takeover && rel + 1u > kSlots) wait_at_least(ps.used + q, rel + 1u - kSlots, ps.abort);
         load_shares(sb, ps, slot, G, iw, 1u, nb0, rs.vo, rs.so);
     }
     uint32_t x[kR];

@@ -10,9 +10,10 @@ import quadp_protocol as P  # noqa: E402
 
 def test_ring_is_clean():
     assert P.check(seeds=10, ppws=(1, 2, 3)) == []
+    assert P.check(seeds=6, ppws=(1, 2), preload=True) == []   # MKACC_QUADP_PRELOAD=1
 
 
 def test_each_rule_is_needed():
     assert P.check(seeds=30, own_write=False)
     assert P.check(seeds=30, takeover_wait=False)
-    assert P.check(seeds=30, reload=False)
+    assert P.check(seeds=30, reload=False, preload=True)

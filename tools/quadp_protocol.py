@@ -8,9 +8,9 @@ workgroup the one owning it.  Per step a workgroup runs its parties' passes, the
 
   * not the index: waits for used >= rel + 1 - SLOTS, writes its tagged share of rel
     to slot rel % SLOTS, goes on to rel + 1;
-  * the index: loads the other parties' slots when its pass starts (the first batch in
-    flight across the pass); on taking over from another party, waits for used >= rel +
-    1 - SLOTS and loads them again; takes the shares of rel, accepting a slot only when
+  * the index: after its passes (or, with preload, also when its pass starts); on
+    taking over from another party, first waits for used >= rel + 1 - SLOTS (and with
+    preload loads again); takes the shares of rel, accepting a slot only when
     its tag equals 1 + rel mod 8 (zeroed slots never match) and reloading the others;
     in the last SLOTS steps of its turn writes its own share to its slot; posts used =
     rel + 1; goes on to rel + 1.
@@ -31,7 +31,7 @@ SLOTS, TAGS = 4, 8
 
 
 def run(k: int, n: int, seed: int, own_write: bool = True, takeover_wait: bool = True,
-        reload: bool = True, ppw: int = 1) -> str | None:
+        reload: bool = True, ppw: int = 1, preload: bool = False) -> str | None:
     rnd = random.Random(seed)
     steps = k * n - 1
     slot = {}                                 # (slot, workgroup) -> step written
@@ -56,7 +56,7 @@ def run(k: int, n: int, seed: int, own_write: bool = True, takeover_wait: bool =
             if r >= steps:
                 continue
             if phase[w] == "pass":
-                if w == index(r):
+                if w == index(r) and preload:
                     seen[w] = load(w, r)
                 phase[w] = "after"
                 moved = True
@@ -70,7 +70,7 @@ def run(k: int, n: int, seed: int, own_write: bool = True, takeover_wait: bool =
                 if phase[w] == "after":
                     if takeover_wait and takeover and r + 1 > SLOTS and used < r + 1 - SLOTS:
                         continue
-                    if takeover and reload:
+                    if (takeover and reload) or not preload:
                         seen[w] = load(w, r)
                     phase[w] = "take"
                 got = seen[w]
@@ -109,10 +109,11 @@ def check(seeds: int = 200, ppws=(1,), **kw) -> list[str]:
 
 
 def main() -> int:
-    bad = check(ppws=(1, 2, 3, 4))
+    bad = check(ppws=(1, 2, 3, 4)) + check(seeds=60, ppws=(1, 2), preload=True)
     print(f"quadp share ring: {'clean' if not bad else bad[:3]}")
-    weak = [check(seeds=60, own_write=False), check(seeds=60, takeover_wait=False), check(seeds=60, reload=False)]
-    print("failing shapes without the index's own slot write / the takeover wait / the reload after it:",
+    weak = [check(seeds=60, own_write=False), check(seeds=60, takeover_wait=False),
+            check(seeds=60, reload=False, preload=True)]
+    print("failing shapes without the index's own slot writes / the takeover wait / (preloading) the reload:",
           [len(w) for w in weak])
     return 0 if not bad and all(weak) else 1
 
