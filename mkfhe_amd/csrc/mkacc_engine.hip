@@ -290,6 +290,8 @@ struct mkacc_ctx {
     size_t gate_B = 0;
     uint32_t gate_dks = 0;         // dks d_digits was sized for
     uint8_t* d_digits = nullptr;   // [B][k][dks][N]
+    uint32_t* d_kspart = nullptr;  // key-switch slice sums of small batches (ks_slices)
+    size_t kspart_words = 0;
     uint32_t* d_bh = nullptr;      // [B] MK-LWE rotation b
     uint32_t* d_gin = nullptr;     // host API staging of gate inputs (grow-only)
     uint32_t* d_gout = nullptr;
@@ -706,9 +708,36 @@ int launch_batch(mkacc_ctx* c, const uint32_t* d_ct, const uint32_t* d_in, uint3
 
 // ---- gate level (head + EvalAcc + tail) -------------------------------------------
 
+// Key-switch slices of a small batch: the sum over l = (digit, coefficient) split into
+// slices of lper (a multiple of the kernel's reduction / digit-fetch granule) so the
+// blocks cover the CUs about twice; 1 for batches with blocks enough.  One STD128_MKNTRU
+// gate's KeySwitch2 ran 24 blocks (1.38 ms of a 17.7 ms gate, profiles/r6/v25).
+uint32_t ks_slices(const mkacc_ctx* c, size_t B, uint32_t& lper) {
+    const size_t L = (size_t)c->dks * kN;
+    const bool mntru = c->method_class == XZW;
+    const size_t blocks = mntru ? (size_t)(c->n_pad / kKsTile) * ((B + kKsTile - 1) / kKsTile) * c->p.k : B * c->p.k;
+    const size_t gran = mntru ? 4 * kKsChunk : 16;
+    size_t S = blocks >= 2 * (size_t)c->cus ? 1 : (2 * (size_t)c->cus + blocks - 1) / blocks;
+    S = std::max<size_t>(1, std::min<size_t>(S, std::min<size_t>(64, L / gran)));
+    lper = (uint32_t)(((L + S - 1) / S + gran - 1) / gran * gran);
+    return (uint32_t)((L + lper - 1) / lper);
+}
+size_t kspart_words(const mkacc_ctx* c, size_t B) {
+    uint32_t lper;
+    const size_t S = ks_slices(c, B, lper);
+    return S > 1 ? S * B * c->p.k * ((size_t)c->ks.n_out + 1) : 0;
+}
+
 int ensure_gate_ws(mkacc_ctx* c, size_t B) {
     int rc = ensure_ws(c, B);
     if (rc) return rc;
+    if (const size_t w = kspart_words(c, B); w > c->kspart_words) {
+        if (c->d_kspart) HIP_TRY(hipFree(c->d_kspart));
+        c->d_kspart = nullptr;
+        c->kspart_words = 0;
+        HIP_TRY(hipMalloc(&c->d_kspart, w * 4));
+        c->kspart_words = w;
+    }
     // d_digits is sized for the key-switching digit count it was allocated with;
     // a re-upload (or share_ksk) with a different dks must reallocate it
     if (B <= c->gate_B && c->dks == c->gate_dks) return MKACC_OK;
@@ -765,16 +794,32 @@ void launch_tail(mkacc_ctx* c, const uint32_t* acc, uint32_t* out_a, uint32_t* o
     hipLaunchKernelGGL(extract_kernel, dim3((npoly + 3) / 4), dim3(256), 0, c->stream, acc, c->d_digits, npoly,
                        c->d_twi, twl_inv, tail_consts(c));
     const uint32_t L = c->dks * kN;
+    uint32_t lper = 0;
+    uint32_t S = ks_slices(c, B, lper);
+    // the slice sums need ensure_gate_ws's buffer (every gate entry point sizes it)
+    if (S > 1 && c->kspart_words < kspart_words(c, B)) {
+        S = 1;
+        lper = L;
+    }
+    uint32_t* part = S > 1 ? c->d_kspart : nullptr;
+    const uint32_t total = (uint32_t)(B * k * c->ks.n_out);
     if (c->method_class == XZW) {
         const uint32_t qinv = (uint32_t)((1ull << 32) / c->ks.qKS);
-        const dim3 grid(c->n_pad / kKsTile, (unsigned)((B + kKsTile - 1) / kKsTile), k);
+        const dim3 grid(c->n_pad / kKsTile, (unsigned)((B + kKsTile - 1) / kKsTile), k * S);
         hipLaunchKernelGGL(ks_mntru_kernel, grid, dim3(256), 0, c->stream, c->d_digits, c->d_ksk, out_a,
-                           (uint32_t)B, k, L, c->ks.n_out, c->n_pad, (uint32_t)c->ks.qKS, qinv);
+                           (uint32_t)B, k, L, c->ks.n_out, c->n_pad, (uint32_t)c->ks.qKS, qinv, lper, part);
+        if (part)
+            hipLaunchKernelGGL(ks_sum_kernel, dim3((total + 255) / 256), dim3(256), 0, c->stream, part, out_a, S, total,
+                               (uint32_t)c->ks.qKS);
     } else {
         const uint32_t b0 = round_qQ_host((c->p.Q >> 3) + 1, c->ks.qKS, c->p.Q);
-        hipLaunchKernelGGL(ks_mklwe_kernel, dim3((unsigned)(B * k)), dim3(256), 0, c->stream, c->d_digits,
+        uint32_t* pb = part ? part + (size_t)S * total : nullptr;
+        hipLaunchKernelGGL(ks_mklwe_kernel, dim3((unsigned)(B * k * S)), dim3(256), 0, c->stream, c->d_digits,
                            c->d_lweA, c->d_lweB, out_a, c->d_bh, k, c->ks.n_out, c->ks.baseKS, c->dks,
-                           (uint32_t)c->ks.qKS);
+                           (uint32_t)c->ks.qKS, (uint32_t)B, S, lper, part, pb);
+        if (part)
+            hipLaunchKernelGGL(ks_mklwe_sum_kernel, dim3((total + 255) / 256), dim3(256), 0, c->stream, part, pb, out_a,
+                               c->d_bh, S, (uint32_t)(B * k), c->ks.n_out, (uint32_t)c->ks.qKS);
         hipLaunchKernelGGL(ks_mklwe_b_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, c->stream, c->d_bh,
                            out_b, (uint32_t)B, k, (uint32_t)c->ks.qKS, b0);
     }
@@ -1568,7 +1613,7 @@ void mkacc_destroy(mkacc_ctx* c) {
     for (void* p : {(void*)c->d_twf, (void*)c->d_twi, (void*)c->d_img, (void*)c->d_qimg, (void*)c->d_keys, (void*)c->d_pkey,
                     (void*)c->d_acc0, (void*)c->d_acc1, (void*)c->d_cvals, (void*)c->d_dscr, (void*)c->d_ct,
                     (void*)c->d_io, (void*)c->d_ksk, (void*)c->d_lweA, (void*)c->d_lweB, (void*)c->d_tv,
-                    (void*)c->d_digits, (void*)c->d_bh, (void*)c->d_gin, (void*)c->d_gout, (void*)c->d_wtwf,
+                    (void*)c->d_digits, (void*)c->d_kspart, (void*)c->d_bh, (void*)c->d_gin, (void*)c->d_gout, (void*)c->d_wtwf,
                     (void*)c->d_wtwi, (void*)c->d_wpsi, (void*)c->d_ftwf, (void*)c->d_fpsi, (void*)c->d_rtis,
                     (void*)c->d_r2tab,
                     (void*)c->d_wkeys, (void*)c->d_wpkey, (void*)c->d_wacc0,

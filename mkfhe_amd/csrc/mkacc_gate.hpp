@@ -135,29 +135,34 @@ __global__ __launch_bounds__(256) void extract_kernel(const uint32_t* __restrict
 // because KeySwitchGen2 stores KSK2[u][d][l] = d * KSK2[u][1][l] mod qKS
 // (mntru-pke.cpp:744-755).  64 gates x 64 outputs per 256-thread block, 4x4
 // per thread, 32-bit sums (digits < 2^8, keys < 2^16) reduced every 128 l.
+// Small batches split l over slices (blockIdx.z = u + k slice, lper l each, a multiple
+// of 128): a slice writes its sums mod qKS to part[slice] and ks_sum_kernel adds them
+// -- one STD128_MKNTRU gate had 24 blocks for 36.7 MB of key rows.
 constexpr int kKsTile = 64, kKsChunk = 32;
 __global__ __launch_bounds__(256) void ks_mntru_kernel(const uint8_t* __restrict__ D, const uint16_t* __restrict__ K,
                                                        uint32_t* __restrict__ out, uint32_t B, uint32_t k,
                                                        uint32_t L, uint32_t n_out, uint32_t n_pad, uint32_t qKS,
-                                                       uint32_t qinv) {
+                                                       uint32_t qinv, uint32_t lper, uint32_t* __restrict__ part) {
     __shared__ uint32_t sD[kKsChunk][kKsTile + 1];   // [l][gate]
     __shared__ uint32_t sK[kKsChunk][kKsTile];       // [l][col]
-    const uint32_t u = blockIdx.z;
+    const uint32_t u = blockIdx.z % k, sl = blockIdx.z / k;
+    const uint32_t lb = sl * lper, le = min(L, lb + lper);
+    uint32_t* dst = part ? part + (size_t)sl * B * k * n_out : out;
     const uint32_t g0 = blockIdx.y * kKsTile, c0 = blockIdx.x * kKsTile;
     const uint32_t tx = threadIdx.x & 15u, ty = threadIdx.x >> 4;    // 16 x 16
     uint32_t acc[4][4] = {};
     const uint8_t* Du = D + (size_t)u * L;
     const uint16_t* Ku = K + (size_t)u * L * n_pad;
-    for (uint32_t l0 = 0; l0 < L; l0 += kKsChunk) {
+    for (uint32_t l0 = lb; l0 < le; l0 += kKsChunk) {
         // D tile: 64 gates x 32 l (bytes), one byte per thread-iteration
         for (uint32_t e = threadIdx.x; e < kKsTile * kKsChunk; e += 256) {
             const uint32_t g = e / kKsChunk, ll = e % kKsChunk;
             const uint32_t gb = g0 + g;
-            sD[ll][g] = (gb < B && l0 + ll < L) ? Du[(size_t)gb * k * L + l0 + ll] : 0u;
+            sD[ll][g] = (gb < B && l0 + ll < le) ? Du[(size_t)gb * k * L + l0 + ll] : 0u;
         }
         for (uint32_t e = threadIdx.x; e < kKsChunk * kKsTile; e += 256) {
             const uint32_t ll = e / kKsTile, cc = e % kKsTile;
-            sK[ll][cc] = (l0 + ll < L) ? Ku[(size_t)(l0 + ll) * n_pad + c0 + cc] : 0u;
+            sK[ll][cc] = (l0 + ll < le) ? Ku[(size_t)(l0 + ll) * n_pad + c0 + cc] : 0u;
         }
         __syncthreads();
 #pragma unroll 8
@@ -173,7 +178,7 @@ __global__ __launch_bounds__(256) void ks_mntru_kernel(const uint8_t* __restrict
                 for (int bq = 0; bq < 4; ++bq) acc[a][bq] = __umul24(dv[a], kv[bq]) + acc[a][bq];
         }
         __syncthreads();
-        if (((l0 / kKsChunk) & 3u) == 3u || l0 + kKsChunk >= L) {
+        if ((((l0 - lb) / kKsChunk) & 3u) == 3u || l0 + kKsChunk >= le) {
             // every 128 l: sums stay below 128 * 2^8 * 2^16 = 2^31
 #pragma unroll
             for (int a = 0; a < 4; ++a)
@@ -192,9 +197,19 @@ __global__ __launch_bounds__(256) void ks_mntru_kernel(const uint8_t* __restrict
 #pragma unroll
         for (int bq = 0; bq < 4; ++bq) {
             const uint32_t col = c0 + tx * 4 + bq;
-            if (col < n_out) out[((size_t)gb * k + u) * n_out + col] = acc[a][bq];
+            if (col < n_out) dst[((size_t)gb * k + u) * n_out + col] = acc[a][bq];
         }
     }
+}
+
+// sum of the slices' partial sums (each < qKS) mod qKS into out
+__global__ void ks_sum_kernel(const uint32_t* __restrict__ part, uint32_t* __restrict__ out, uint32_t slices,
+                              uint32_t total, uint32_t qKS) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    uint32_t s = 0;
+    for (uint32_t sl = 0; sl < slices; ++sl) s += part[(size_t)sl * total + i];   // slices x 2^16 < 2^32
+    out[i] = s % qKS;
 }
 
 // MK-LWE KeySwitch (mklwe-pke.cpp:260-298): for every party u, coefficient j
@@ -202,21 +217,27 @@ __global__ __launch_bounds__(256) void ks_mntru_kernel(const uint8_t* __restrict
 // of B from b.  One block per (gate, party); threads run over the n output
 // columns and stream the dks*N digit-selected rows, 16 independent row loads
 // in flight per thread (digits fetched 16 at a time, wave-uniform).  Sums of
-// dks*N words < 2^16 stay below 2^32 (dks*N <= 2^16).
+// dks*N words < 2^16 stay below 2^32 (dks*N <= 2^16).  Small batches split l over
+// slices (blockIdx.x = (b k + u) slices + slice, lper l each, a multiple of 16): a
+// slice writes its sums mod qKS (not negated) to pa[slice] / pb[slice] and
+// ks_mklwe_sum_kernel finishes them.
 //   A [k][N][Bks][dks][n] u16, Bv [k][N][Bks][dks] u16, partial_b [B][k]
 __global__ __launch_bounds__(256) void ks_mklwe_kernel(const uint8_t* __restrict__ D, const uint16_t* __restrict__ A,
                                                        const uint16_t* __restrict__ Bv, uint32_t* __restrict__ out_a,
                                                        uint32_t* __restrict__ partial_b, uint32_t k, uint32_t n_out,
-                                                       uint32_t baseKS, uint32_t dks, uint32_t qKS) {
-    const uint32_t u = blockIdx.x % k, b = blockIdx.x / k;
-    const uint32_t L = dks * kN;
+                                                       uint32_t baseKS, uint32_t dks, uint32_t qKS, uint32_t B,
+                                                       uint32_t slices, uint32_t lper, uint32_t* __restrict__ pa,
+                                                       uint32_t* __restrict__ pb) {
+    const uint32_t sl = blockIdx.x % slices, bu = blockIdx.x / slices;
+    const uint32_t u = bu % k, b = bu / k;
+    const uint32_t L = dks * kN, lb = sl * lper, le = min(L, lb + lper);
     const uint4* Dp = reinterpret_cast<const uint4*>(D + ((size_t)b * k + u) * L);
     const size_t rowbase = (size_t)u * kN * baseKS;     // row of (u, j=0, d=0, t=0) / dks
     for (uint32_t c0 = 0; c0 < n_out; c0 += 256) {
         const uint32_t c = c0 + threadIdx.x;
         const bool on = c < n_out;
         uint32_t s = 0, sb = 0;
-        for (uint32_t l0 = 0; l0 < L; l0 += 16) {
+        for (uint32_t l0 = lb; l0 < le; l0 += 16) {
             const uint4 dv = Dp[l0 >> 4];
             const uint32_t dw[4] = {(uint32_t)__builtin_amdgcn_readfirstlane(dv.x),
                                     (uint32_t)__builtin_amdgcn_readfirstlane(dv.y),
@@ -235,8 +256,31 @@ __global__ __launch_bounds__(256) void ks_mklwe_kernel(const uint8_t* __restrict
             for (int e = 0; e < 16; ++e) s += v[e];
         }
         s %= qKS;
+        if (pa) {
+            if (on) pa[((size_t)sl * B * k + (size_t)b * k + u) * n_out + c] = s;
+            if (c0 == 0 && threadIdx.x == 0) pb[(size_t)sl * B * k + (size_t)b * k + u] = sb % qKS;
+            continue;
+        }
         if (on) out_a[((size_t)b * k + u) * n_out + c] = s == 0 ? 0 : qKS - s;
         if (c0 == 0 && threadIdx.x == 0) partial_b[(size_t)b * k + u] = sb % qKS;
+    }
+}
+
+// the slices of ks_mklwe_kernel: out_a = -(sum of pa) and partial_b = sum of pb, mod qKS
+__global__ void ks_mklwe_sum_kernel(const uint32_t* __restrict__ pa, const uint32_t* __restrict__ pb,
+                                    uint32_t* __restrict__ out_a, uint32_t* __restrict__ partial_b, uint32_t slices,
+                                    uint32_t Bk, uint32_t n_out, uint32_t qKS) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x, total = Bk * n_out;
+    if (i < total) {
+        uint32_t s = 0;
+        for (uint32_t sl = 0; sl < slices; ++sl) s += pa[(size_t)sl * total + i];
+        s %= qKS;
+        out_a[i] = s == 0 ? 0 : qKS - s;
+    }
+    if (i < Bk) {
+        uint32_t s = 0;
+        for (uint32_t sl = 0; sl < slices; ++sl) s += pb[(size_t)sl * Bk + i];
+        partial_b[i] = s % qKS;
     }
 }
 
