@@ -37,6 +37,15 @@
 // 2q, 2q + 1 of every lane: the key and accumulator streams are 1 KiB per load.
 #pragma once
 
+#ifndef MKACC_QUAD_KEEP
+#define MKACC_QUAD_KEEP 0   // the same in the one-workgroup-per-gate kernels (quad_step)
+#endif
+#ifndef MKACC_QUADP_KEEP
+// 1: the party-parallel kernel keeps the index party's pass output in registers for the
+// f-part (no store and reload through acc_out on the critical path): -2.2 % for one
+// STD128_MKNTRU gate, -1.6 % at B = 128 (profiles/r6/v36)
+#define MKACC_QUADP_KEEP 1
+#endif
 #ifndef MKACC_QUAD_PF
 #define MKACC_QUAD_PF 1   // the MAC's key groups issued at the start of the pass (before its transforms)
 #endif
@@ -418,10 +427,12 @@ __device__ __forceinline__ void digits_q(const Ctx& s, uint32_t (&x)[kR], uint32
 // the MAC of one pass over this wave's 8 slots (mac2's algebra):
 //   F = false (party u): start = acc_u (st), out -> acc_out[u], sv <- redc(sv r32 + sum G P)
 //   F = true  (f-part):  start = the index party's output (st), out -> acc_out[index]
-template <int DG, int METHOD, bool FIRST, bool F>
+// KEEP: the outputs stay in keep[] instead of going to acc_out (the index party's pass,
+// whose output only the f-part reads)
+template <int DG, int METHOD, bool FIRST, bool F, bool KEEP = false>
 __device__ __forceinline__ void mac_q(const Ctx& s, const QRes& rs, const QKeys<DG, METHOD, FIRST>& kk,
                                       const uint32_t (&G)[DG][kR], const uint32_t (&st)[kR], uint32_t (&sv)[kR],
-                                      const QMono& mp, const QMono& mn, uint32_t u) {
+                                      const QMono& mp, const QMono& mn, uint32_t u, uint32_t* keep = nullptr) {
     using Cf = QCfg<DG, METHOD, FIRST>;
     const uint32_t Q = s.m.Q;
 #pragma unroll
@@ -464,7 +475,12 @@ __device__ __forceinline__ void mac_q(const Ctx& s, const QRes& rs, const QKeys<
             ov[e] = v;
             if (!F) sv[r] = redc(sa, Q, s.m.qinv);
         }
-        bstore4(ov, rs.rout, rs.vo, u * (kN * 4u) + rs.so + (uint32_t)g * 1024u);
+        if constexpr (KEEP) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) keep[4 * g + e] = ov[e];
+        } else {
+            bstore4(ov, rs.rout, rs.vo, u * (kN * 4u) + rs.so + (uint32_t)g * 1024u);
+        }
     }
     vcc_fence();
 }
@@ -494,6 +510,10 @@ __device__ __forceinline__ void quad_step(const StepArgs& a, const Ctx& s0, uint
                   q * 2048u};
     const uint32_t Q = s.m.Q;
     uint32_t sv[kR];
+    uint32_t keep[kR];   // the index party's pass output, the f-part's start (MKACC_QUADP_KEEP)
+    // not in the first (KDM) step: it runs once per gate, and at dg = 5 the kept words
+    // pushed a 16-byte store's data registers into a store-data hazard (isa_audit)
+    constexpr bool kKeep = MKACC_QUAD_KEEP && !FIRST;
 #pragma unroll
     for (int r = 0; r < kR; ++r) sv[r] = 0;
     // passes t = 0 .. k - 1: party index + 1 + t (mod k), the index party last; t = k: the f-part
@@ -524,14 +544,20 @@ __device__ __forceinline__ void quad_step(const StepArgs& a, const Ctx& s0, uint
             }
             vcc_fence();   // the jump over the f-part branch follows the rotation
         } else {
-            // the index party's output: this wave's own stores earlier in the step
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (kPf) issue_keys<DG, METHOD, FIRST, true>(kk, rs, index);
+            if (kKeep) {
+                if (kPf) issue_keys<DG, METHOD, FIRST, true>(kk, rs, index);
 #pragma unroll
-            for (int g = 0; g < 2; ++g) {
-                const u32x4 v = bload4(rs.rout, rs.vo, index * polyB + rs.so + (uint32_t)g * 1024u);
+                for (int r = 0; r < kR; ++r) st[r] = keep[r];
+            } else {
+                // the index party's output: this wave's own stores earlier in the step
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (kPf) issue_keys<DG, METHOD, FIRST, true>(kk, rs, index);
 #pragma unroll
-                for (int e = 0; e < 4; ++e) st[4 * g + e] = v[e];
+                for (int g = 0; g < 2; ++g) {
+                    const u32x4 v = bload4(rs.rout, rs.vo, index * polyB + rs.so + (uint32_t)g * 1024u);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) st[4 * g + e] = v[e];
+                }
             }
 #pragma unroll
             for (int r = 0; r < kR; ++r) x[r] = sv[r];
@@ -542,7 +568,10 @@ __device__ __forceinline__ void quad_step(const StepArgs& a, const Ctx& s0, uint
         vcc_fence();   // the MAC branch follows the last butterflies
         if (!fpart) {
             if (!kPf) issue_keys<DG, METHOD, FIRST, false>(kk, rs, u);
-            mac_q<DG, METHOD, FIRST, false>(s, rs, kk, G, st, sv, mp, mn, u);
+            if (kKeep && u == index)
+                mac_q<DG, METHOD, FIRST, false, true>(s, rs, kk, G, st, sv, mp, mn, u, keep);
+            else
+                mac_q<DG, METHOD, FIRST, false>(s, rs, kk, G, st, sv, mp, mn, u);
         } else {
             if (!kPf) issue_keys<DG, METHOD, FIRST, true>(kk, rs, index);
             mac_q<DG, METHOD, FIRST, true>(s, rs, kk, G, st, sv, mp, mn, index);
@@ -752,6 +781,7 @@ __device__ __forceinline__ void quadp_step(const StepArgs& a, const Ctx& s0, uin
     ShareBatch<NB> sb;
     const uint32_t nb0 = is_index ? min(G - 1u, NB) : 0u;
     uint32_t sv[kR];   // the workgroup's share: redc-summed over its parties' passes (mac_q)
+    uint32_t keep[kR];   // the index party's pass output, the f-part's start (MKACC_QUADP_KEEP)
 #pragma unroll
     for (int r = 0; r < kR; ++r) sv[r] = 0;
 #pragma unroll 1
@@ -779,7 +809,10 @@ __device__ __forceinline__ void quadp_step(const StepArgs& a, const Ctx& s0, uin
         digits_q<DG, C>(s, x, Gd, xs);
         vcc_fence();
         if (!kPf) issue_keys<DG, METHOD, FIRST, false>(kk, rs, u);
-        mac_q<DG, METHOD, FIRST, false>(s, rs, kk, Gd, st, sv, mp, mn, u);
+        if (MKACC_QUADP_KEEP && is_index && j == cnt)
+            mac_q<DG, METHOD, FIRST, false, true>(s, rs, kk, Gd, st, sv, mp, mn, u, keep);
+        else
+            mac_q<DG, METHOD, FIRST, false>(s, rs, kk, Gd, st, sv, mp, mn, u);
     }
     if (!is_index) {
         // publish the tagged share once the index workgroup has taken what the slot held
@@ -810,13 +843,19 @@ __device__ __forceinline__ void quadp_step(const StepArgs& a, const Ctx& s0, uin
     {
         uint32_t st[kR];
         QKeys<DG, METHOD, FIRST> kk;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's acc_out[index] stores
-        if (kPf) issue_keys<DG, METHOD, FIRST, true>(kk, rs, index);
+        if (MKACC_QUADP_KEEP) {
+            if (kPf) issue_keys<DG, METHOD, FIRST, true>(kk, rs, index);
 #pragma unroll
-        for (int g = 0; g < 2; ++g) {
-            const u32x4 v = bload4(rs.rout, rs.vo, index * polyB + rs.so + (uint32_t)g * 1024u);
+            for (int r = 0; r < kR; ++r) st[r] = keep[r];
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's acc_out[index] stores
+            if (kPf) issue_keys<DG, METHOD, FIRST, true>(kk, rs, index);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) st[4 * g + e] = v[e];
+            for (int g = 0; g < 2; ++g) {
+                const u32x4 v = bload4(rs.rout, rs.vo, index * polyB + rs.so + (uint32_t)g * 1024u);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) st[4 * g + e] = v[e];
+            }
         }
         // the index workgroup refreshes its slots in the last kSlots steps of its turn (a
         // share of its last turn as writer could alias the tag later): issued behind the
