@@ -38,7 +38,9 @@
 #pragma once
 
 #ifndef MKACC_QUAD_KEEP
-#define MKACC_QUAD_KEEP 0   // the same in the one-workgroup-per-gate kernels (quad_step)
+// the same in the one-workgroup-per-gate kernels (quad_step): +1.1 % at B = 256, +1.4 %
+// for the two-per-CU form at B = 1024 (profiles/r6/v37)
+#define MKACC_QUAD_KEEP 1
 #endif
 #ifndef MKACC_QUADP_KEEP
 // 1: the party-parallel kernel keeps the index party's pass output in registers for the
