@@ -517,7 +517,7 @@ def run_rank(args, env: dict, make_engine, make_checker, torch_device: str, back
                              f"{slices} concurrent launches of {B // slices}+ gates on {slices} streams; rocprof lists each "
                              "slice launch with its own (overlapping) duration" if slices > 1 else
                              "the pass time / (k n): small batches run the steps after the first in one launch "
-                             "(mk_quadp_run_kernel at B k <= CUs, mk_quad_run_kernel at B <= CUs, mk_quad2_run_kernel "
+                             "(mk_quadp_run_kernel at B <= CUs / 2, mk_quad_run_kernel at B <= CUs, mk_quad2_run_kernel "
                              "up to 4 gates per CU, DESIGN.md s2)"
                              if kname in ("mk_lat_kernel", "mk_latd_kernel", "mk_lat_run_kernel", "mk_latd_run_kernel",
                                           "mk_quad_kernel", "mk_quad_run_kernel", "mk_quad2_kernel",
