@@ -431,7 +431,9 @@ __device__ __forceinline__ void digits_q(const Ctx& s, uint32_t (&x)[kR], uint32
 //   F = true  (f-part):  start = the index party's output (st), out -> acc_out[index]
 // KEEP: the outputs stay in keep[] instead of going to acc_out (the index party's pass,
 // whose output only the f-part reads)
-template <int DG, int METHOD, bool FIRST, bool F, bool KEEP = false>
+// KEEP 2: keep[] gets the outputs and acc_out too (the f-part output the index party's
+// next pass starts from, MKACC_QUADP_CARRY)
+template <int DG, int METHOD, bool FIRST, bool F, int KEEP = 0>
 __device__ __forceinline__ void mac_q(const Ctx& s, const QRes& rs, const QKeys<DG, METHOD, FIRST>& kk,
                                       const uint32_t (&G)[DG][kR], const uint32_t (&st)[kR], uint32_t (&sv)[kR],
                                       const QMono& mp, const QMono& mn, uint32_t u, uint32_t* keep = nullptr) {
@@ -477,12 +479,11 @@ __device__ __forceinline__ void mac_q(const Ctx& s, const QRes& rs, const QKeys<
             ov[e] = v;
             if (!F) sv[r] = redc(sa, Q, s.m.qinv);
         }
-        if constexpr (KEEP) {
+        if constexpr (KEEP != 0) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) keep[4 * g + e] = ov[e];
-        } else {
-            bstore4(ov, rs.rout, rs.vo, u * (kN * 4u) + rs.so + (uint32_t)g * 1024u);
         }
+        if constexpr (KEEP != 1) bstore4(ov, rs.rout, rs.vo, u * (kN * 4u) + rs.so + (uint32_t)g * 1024u);
     }
     vcc_fence();
 }
@@ -571,7 +572,7 @@ __device__ __forceinline__ void quad_step(const StepArgs& a, const Ctx& s0, uint
         if (!fpart) {
             if (!kPf) issue_keys<DG, METHOD, FIRST, false>(kk, rs, u);
             if (kKeep && u == index)
-                mac_q<DG, METHOD, FIRST, false, true>(s, rs, kk, G, st, sv, mp, mn, u, keep);
+                mac_q<DG, METHOD, FIRST, false, 1>(s, rs, kk, G, st, sv, mp, mn, u, keep);
             else
                 mac_q<DG, METHOD, FIRST, false>(s, rs, kk, G, st, sv, mp, mn, u);
         } else {
@@ -611,6 +612,12 @@ __device__ __forceinline__ void quad_step(const StepArgs& a, const Ctx& s0, uint
 // again (the kernel drains, the engine reports MKACC_E_DEVICE).
 constexpr uint32_t kSlots = 4;
 constexpr uint32_t kBatch = 4;              // shares per load batch of the index workgroup
+#ifndef MKACC_QUADP_CARRY
+// 1: a one-party workgroup that stays index keeps its f-part output in registers for the
+// next step's pass (no reload through acc_in, no drain of the step's stores).  Off:
+// 3 % slower for one STD128_MKNTRU gate, 1.4 % for STD128_MKNTRU_3 (profiles/r6/v39)
+#define MKACC_QUADP_CARRY 0
+#endif
 #ifndef MKACC_QUADP_PRELOAD
 // 1: the index workgroup's first share batch in flight across its pass.  Off: the
 // system-coherent loads queued behind the pass's accumulator loads delayed its keys
@@ -752,9 +759,12 @@ __device__ __forceinline__ void put_share(const PSync& ps, const uint32_t (&sv)[
 // ps.gate: the passes of its parties (the index party's last), then -- the index
 // workgroup -- the f-part.  takeover: the index workgroup of this step was not the
 // previous step's; last: this step is one of the last kSlots of the index workgroup's turn
+// carry_in: the index party's accumulator is carry[] (this workgroup's f-part output of
+// the previous step, the same index party); carry_out: keep this step's f-part output
 template <int DG, int METHOD, uint32_t NB>
 __device__ __forceinline__ void quadp_step(const StepArgs& a, const Ctx& s0, uint32_t& xs, const PSync& ps,
-                                           uint32_t rel, bool takeover, bool last) {
+                                           uint32_t rel, bool takeover, bool last, bool carry_in, bool carry_out,
+                                           uint32_t (&carry)[kR]) {
     constexpr bool C = true, FIRST = false;
     constexpr bool kPf = MKACC_QUAD_PF;
     Ctx s = s0;
@@ -794,11 +804,16 @@ __device__ __forceinline__ void quadp_step(const StepArgs& a, const Ctx& s0, uin
         // loads in the order they are needed (vector loads return in order): the party's
         // accumulator for the rotation, then -- the index party -- the first batch of the
         // other workgroups' shares, in flight across the pass, then the keys for the MAC
+        if (carry_in && u == index) {
 #pragma unroll
-        for (int g = 0; g < 2; ++g) {
-            const u32x4 v = bload4(rs.rin, rs.vo, u * polyB + rs.so + (uint32_t)g * 1024u);
+            for (int r = 0; r < kR; ++r) st[r] = carry[r];
+        } else {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) st[4 * g + e] = v[e];
+            for (int g = 0; g < 2; ++g) {
+                const u32x4 v = bload4(rs.rin, rs.vo, u * polyB + rs.so + (uint32_t)g * 1024u);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) st[4 * g + e] = v[e];
+            }
         }
         asm volatile("" ::: "memory");
         if (MKACC_QUADP_PRELOAD && is_index && j == cnt) load_shares(sb, ps, slot, G, iw, 1u, nb0, rs.vo, rs.so);
@@ -812,7 +827,7 @@ __device__ __forceinline__ void quadp_step(const StepArgs& a, const Ctx& s0, uin
         vcc_fence();
         if (!kPf) issue_keys<DG, METHOD, FIRST, false>(kk, rs, u);
         if (MKACC_QUADP_KEEP && is_index && j == cnt)
-            mac_q<DG, METHOD, FIRST, false, true>(s, rs, kk, Gd, st, sv, mp, mn, u, keep);
+            mac_q<DG, METHOD, FIRST, false, 1>(s, rs, kk, Gd, st, sv, mp, mn, u, keep);
         else
             mac_q<DG, METHOD, FIRST, false>(s, rs, kk, Gd, st, sv, mp, mn, u);
     }
@@ -842,6 +857,9 @@ __device__ __forceinline__ void quadp_step(const StepArgs& a, const Ctx& s0, uin
         take_shares(sb, ps, slot, G, iw, o0, nb, rs.vo, rs.so, tag, Q, x);
     }
     vcc_fence();
+    // the shares have landed: outside the last kSlots steps of its turn (no slot write of
+    // its own) the index workgroup frees the slots now, not behind the f-part
+    if (!last) post(ps.used + q, rel + 1u);
     {
         uint32_t st[kR];
         QKeys<DG, METHOD, FIRST> kk;
@@ -868,11 +886,14 @@ __device__ __forceinline__ void quadp_step(const StepArgs& a, const Ctx& s0, uin
         digits_q<DG, C>(s, x, Gd, xs);
         vcc_fence();
         if (!kPf) issue_keys<DG, METHOD, FIRST, true>(kk, rs, index);
-        mac_q<DG, METHOD, FIRST, true>(s, rs, kk, Gd, st, sv, mp, mn, index);
+        if (carry_out)
+            mac_q<DG, METHOD, FIRST, true, 2>(s, rs, kk, Gd, st, sv, mp, mn, index, carry);
+        else
+            mac_q<DG, METHOD, FIRST, true>(s, rs, kk, Gd, st, sv, mp, mn, index);
     }
-    // the shares have landed and its own is written (long since, behind the f-part: the
-    // wait for the write-through store is off the critical path)
-    post(ps.used + q, rel + 1u);
+    // in the last steps of its turn: the shares have landed and its own is written (long
+    // since, behind the f-part: the wait for the write-through store is off the critical path)
+    if (last) post(ps.used + q, rel + 1u);
 }
 
 }  // namespace quad
@@ -976,17 +997,24 @@ __device__ __forceinline__ void quadp_run(const StepArgs& a, const LatdRun& r, c
     const quad::Ctx s = quad::make_ctx<OCC == 1>(a, smem, qa.qimg);
     const quad::PSync ps = quad::make_psync(qa.sync, qa.abort, a.B, qa.groups, qa.ppw);
     uint32_t xs = 0;
+    uint32_t carry[quad::kR];
+    bool carried = false;
 #pragma unroll 1
     for (uint32_t t = r.t0; t < r.t1; ++t) {
         // the index workgroup of step t is (t / n) / ppw (run_args: index = t / n)
         const uint32_t iw = t / r.n / ps.ppw;
+        // a workgroup of one party that stays index for the next step keeps its f-part
+        // output in registers: no reload, and no drain of its stores between the steps
+        const bool carry_out = MKACC_QUADP_CARRY && ps.ppw == 1u && iw == ps.wg && t + 1u < r.t1 &&
+                               (t + 1u) / r.n == t / r.n;
         // the two-per-CU form at dg = 4 loads one share at a time (a batch of four would
         // spill at 256 VGPRs)
         constexpr uint32_t kNb = OCC == 2 && DG >= 4 ? 1u : quad::kBatch;
         quad::quadp_step<DG, METHOD, kNb>(run_args(a, r, t), s, xs, ps, t - r.t0, (t - 1u) / r.n / ps.ppw != iw,
-                                     (t + quad::kSlots) / r.n / ps.ppw != iw);
+                                     (t + quad::kSlots) / r.n / ps.ppw != iw, carried, carry_out, carry);
         vcc_fence();   // the loop branch follows the step's last reductions
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (!carry_out) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        carried = carry_out;
     }
 }
 template <int DG, int METHOD>
